@@ -1,0 +1,88 @@
+"""ctypes binding of libgrace_hip.so (the C ABI declared in include/grace_hip.h).
+
+The library is the only compute path of grace_amd: there is no CPU or eager-PyTorch fallback.
+If the shared object is missing (not built) or a tensor is not on the GPU, calls raise.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GRACE_HIP_LIB", os.path.join(_HERE, "lib", "libgrace_hip.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+ST = ctypes.c_int
+
+# name -> (restype, argtypes); every symbol declared in include/grace_hip.h
+SIGNATURES = {
+    "grace_version": (ctypes.c_int, []),
+    "grace_last_error": (ctypes.c_char_p, []),
+    "grace_read_status": (ST, [P, P, P]),
+    "grace_timer_enable": (ST, [ctypes.c_int]),
+    "grace_timer_collect": (ST, [P, P]),
+    "grace_axpby": (ST, [P, P, F32, F32, P, I64, P]),
+    "grace_sub": (ST, [P, P, P, I64, P]),
+    "grace_div_scalar": (ST, [P, F32, P, I64, P]),
+    "grace_fill": (ST, [P, F32, I64, P]),
+    "grace_accumulate": (ST, [P, P, I64, I32, P]),
+    "grace_sign_encode": (ST, [P, P, I64, P]),
+    "grace_sign_decode": (ST, [P, P, P, I64, P]),
+    "grace_sign_majority": (ST, [P, I32, P, I64, P]),
+    "grace_signum_encode": (ST, [P, P, I32, F32, F32, P, I64, P]),
+    "grace_sign_step_w1": (ST, [P, P, P, I64, P]),
+    "grace_reduce_workspace_bytes": (SZ, [I64]),
+    "grace_abs_mean": (ST, [P, I64, P, P, P]),
+    "grace_onebit_encode": (ST, [P, I64, P, P, P, P]),
+    "grace_onebit_decode": (ST, [P, P, P, I32, P, I64, P]),
+    "grace_topk_workspace_bytes": (SZ, [I64, I64]),
+    "grace_topk_compress": (ST, [P, I64, I64, P, P, P, SZ, P]),
+    "grace_topk_residual_step": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, SZ, P]),
+    "grace_sparse_decode": (ST, [P, P, I64, P, I64, P]),
+    "grace_sparse_decode_i64": (ST, [P, P, I64, P, I64, P]),
+    "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),
+}
+
+
+class GraceNativeError(RuntimeError):
+    """A native call failed or the native library is unavailable."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises GraceNativeError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise GraceNativeError(
+                    f"grace_amd native library not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != 0:
+        msg = lib.grace_last_error()
+        raise GraceNativeError(f"{name} failed ({st}): {msg.decode() if msg else ''}")
+    return st
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)

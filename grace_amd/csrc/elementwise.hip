@@ -1,0 +1,412 @@
+// Elementwise codecs and memory arithmetic: residual axpby/sub, the signSGD family, one-bit,
+// and the small reductions they need.  All kernels stream 16 B per lane (float4 loads of the
+// f32 gradient, one 32-bit word of four u8 codewords per lane) and grid-stride over the bucket.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace grace {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* where, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", where, hipGetErrorString(e));
+}
+void set_error_msg(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+static inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+constexpr int kBlock = 256;
+
+// ------------------------------------------------------------------------------------------------
+// Generic 4-wide streaming driver: Op::vec(i, i4) handles elements [4*i4, 4*i4+4), Op::one(i)
+// a single element.  VEC=false runs the scalar loop (unaligned views).
+template <bool VEC, typename Op>
+__global__ __launch_bounds__(kBlock) void stream_kernel(Op op, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (VEC) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = gid; i < n4; i += stride) op.vec(i);
+    for (int64_t i = (n4 << 2) + gid; i < n; i += stride) op.one(i);
+  } else {
+    for (int64_t i = gid; i < n; i += stride) op.one(i);
+  }
+}
+
+template <typename Op>
+static grace_status_t launch_stream(const char* name, Op op, int64_t n, bool vec_ok, void* stream) {
+  if (n <= 0) return GRACE_OK;
+  if (vec_ok) {
+    stream_kernel<true, Op><<<stream_grid((n + 3) / 4, kBlock), kBlock, 0, as_stream(stream)>>>(op, n);
+  } else {
+    stream_kernel<false, Op><<<stream_grid(n, kBlock), kBlock, 0, as_stream(stream)>>>(op, n);
+  }
+  GRACE_CHECK_LAUNCH(name);
+  return GRACE_OK;
+}
+
+// t = beta*r + gamma*g, two roundings then the add (no contraction: -ffp-contract=off)
+struct AxpbyOp {
+  const float* r; const float* g; float beta, gamma; float* t;
+  __device__ void vec(int64_t i) const {
+    float4 a = reinterpret_cast<const float4*>(r)[i];
+    float4 b = reinterpret_cast<const float4*>(g)[i];
+    float4 o;
+    o.x = beta * a.x + gamma * b.x; o.y = beta * a.y + gamma * b.y;
+    o.z = beta * a.z + gamma * b.z; o.w = beta * a.w + gamma * b.w;
+    reinterpret_cast<float4*>(t)[i] = o;
+  }
+  __device__ void one(int64_t i) const { t[i] = beta * r[i] + gamma * g[i]; }
+};
+
+struct SubOp {
+  const float* a; const float* b; float* o;
+  __device__ void vec(int64_t i) const {
+    float4 x = reinterpret_cast<const float4*>(a)[i];
+    float4 y = reinterpret_cast<const float4*>(b)[i];
+    reinterpret_cast<float4*>(o)[i] = make_float4(x.x - y.x, x.y - y.y, x.z - y.z, x.w - y.w);
+  }
+  __device__ void one(int64_t i) const { o[i] = a[i] - b[i]; }
+};
+
+struct DivOp {
+  const float* a; float d; float* o;
+  __device__ void vec(int64_t i) const {
+    float4 x = reinterpret_cast<const float4*>(a)[i];
+    reinterpret_cast<float4*>(o)[i] = make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
+  }
+  __device__ void one(int64_t i) const { o[i] = a[i] / d; }
+};
+
+struct AccOp {
+  float* acc; const float* x; int first;
+  __device__ void vec(int64_t i) const {
+    float4 b = reinterpret_cast<const float4*>(x)[i];
+    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4*>(acc)[i];
+    reinterpret_cast<float4*>(acc)[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  __device__ void one(int64_t i) const { acc[i] = (first ? 0.f : acc[i]) + x[i]; }
+};
+
+struct FillOp {
+  float v; float* o;
+  __device__ void vec(int64_t i) const { reinterpret_cast<float4*>(o)[i] = make_float4(v, v, v, v); }
+  __device__ void one(int64_t i) const { o[i] = v; }
+};
+
+__device__ __forceinline__ uint32_t pack_ge0(float4 x) {
+  return (uint32_t)(x.x >= 0.f) | ((uint32_t)(x.y >= 0.f) << 8) | ((uint32_t)(x.z >= 0.f) << 16) |
+         ((uint32_t)(x.w >= 0.f) << 24);
+}
+
+struct SignEncOp {
+  const float* x; uint8_t* c;
+  __device__ void vec(int64_t i) const {
+    reinterpret_cast<uint32_t*>(c)[i] = pack_ge0(reinterpret_cast<const float4*>(x)[i]);
+  }
+  __device__ void one(int64_t i) const { c[i] = (uint8_t)(x[i] >= 0.f); }
+};
+
+// decode: (float)c * 2 - 1, then optional * scale (EF-signSGD multiplies mean * decode)
+struct SignDecOp {
+  const uint8_t* c; const float* scale; float* o;
+  __device__ float dec(uint32_t b, float s, bool has_s) const {
+    float v = (float)b * 2.0f - 1.0f;
+    return has_s ? s * v : v;
+  }
+  __device__ void vec(int64_t i) const {
+    uint32_t w = reinterpret_cast<const uint32_t*>(c)[i];
+    const bool hs = scale != nullptr;
+    const float s = hs ? scale[0] : 1.f;
+    reinterpret_cast<float4*>(o)[i] = make_float4(dec(w & 0xFF, s, hs), dec((w >> 8) & 0xFF, s, hs),
+                                                  dec((w >> 16) & 0xFF, s, hs), dec(w >> 24, s, hs));
+  }
+  __device__ void one(int64_t i) const {
+    const bool hs = scale != nullptr;
+    o[i] = dec(c[i], hs ? scale[0] : 1.f, hs);
+  }
+};
+
+// majority: Python sum over ranks ((0 + d0) + d1 ...) then >= 0 -> +-1.  The partial sums of
+// +-1 are small integers, exact in f32, so summing in rank order is trivially reproduced.
+struct SignMajOp {
+  const uint8_t* c; int world; int64_t n; float* o;
+  __device__ void vec(int64_t i) const {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int w = 0; w < world; ++w) {
+      uint32_t v = reinterpret_cast<const uint32_t*>(c + (int64_t)w * n)[i];
+      s0 += (float)(v & 0xFF) * 2.f - 1.f; s1 += (float)((v >> 8) & 0xFF) * 2.f - 1.f;
+      s2 += (float)((v >> 16) & 0xFF) * 2.f - 1.f; s3 += (float)(v >> 24) * 2.f - 1.f;
+    }
+    reinterpret_cast<float4*>(o)[i] = make_float4(s0 >= 0.f ? 1.f : -1.f, s1 >= 0.f ? 1.f : -1.f,
+                                                  s2 >= 0.f ? 1.f : -1.f, s3 >= 0.f ? 1.f : -1.f);
+  }
+  __device__ void one(int64_t i) const {
+    float s = 0.f;
+    for (int w = 0; w < world; ++w) s += (float)c[(int64_t)w * n + i] * 2.f - 1.f;
+    o[i] = s >= 0.f ? 1.f : -1.f;
+  }
+};
+
+// Signum: m = (1-beta)*g + beta*m_prev.  The reference computes (1.0 - momentum) in double and
+// torch casts both Python scalars to f32 before the multiplies; the caller passes beta and the
+// kernel forms the same two f32 coefficients.
+struct SignumOp {
+  const float* g; float* m; int has_prev; float a, b; uint8_t* c;
+  __device__ float upd(float gv, float mv) const { return has_prev ? a * gv + b * mv : gv; }
+  __device__ void vec(int64_t i) const {
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = has_prev ? reinterpret_cast<const float4*>(m)[i] : make_float4(0, 0, 0, 0);
+    float4 o = make_float4(upd(gv.x, mv.x), upd(gv.y, mv.y), upd(gv.z, mv.z), upd(gv.w, mv.w));
+    reinterpret_cast<float4*>(m)[i] = o;
+    reinterpret_cast<uint32_t*>(c)[i] = pack_ge0(o);
+  }
+  __device__ void one(int64_t i) const {
+    float o = upd(g[i], has_prev ? m[i] : 0.f);
+    m[i] = o;
+    c[i] = (uint8_t)(o >= 0.f);
+  }
+};
+
+struct SignStepOp {
+  const float* x; uint8_t* c; float* o;
+  __device__ void vec(int64_t i) const {
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint32_t w = pack_ge0(v);
+    reinterpret_cast<uint32_t*>(c)[i] = w;
+    reinterpret_cast<float4*>(o)[i] =
+        make_float4(v.x >= 0.f ? 1.f : -1.f, v.y >= 0.f ? 1.f : -1.f, v.z >= 0.f ? 1.f : -1.f,
+                    v.w >= 0.f ? 1.f : -1.f);
+  }
+  __device__ void one(int64_t i) const {
+    bool p = x[i] >= 0.f;
+    c[i] = (uint8_t)p;
+    o[i] = p ? 1.f : -1.f;
+  }
+};
+
+// one-bit decode: mask0 * mean0 + notmask * mean1 (two products, then the add)
+struct OneBitDecOp {
+  const uint8_t* m; const float* mean0; const float* mean1; int quirk; float* o;
+  __device__ float dec(uint32_t b, float m0, float m1) const {
+    float nb = quirk ? (float)(255u - b) : (float)(1u - b);
+    return (float)b * m0 + nb * m1;
+  }
+  __device__ void vec(int64_t i) const {
+    const float m0 = mean0[0], m1 = mean1[0];
+    uint32_t w = reinterpret_cast<const uint32_t*>(m)[i];
+    reinterpret_cast<float4*>(o)[i] = make_float4(dec(w & 0xFF, m0, m1), dec((w >> 8) & 0xFF, m0, m1),
+                                                  dec((w >> 16) & 0xFF, m0, m1), dec(w >> 24, m0, m1));
+  }
+  __device__ void one(int64_t i) const { o[i] = dec(m[i], mean0[0], mean1[0]); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Reductions: block partials in f64 (deterministic order per block), then one finishing block
+// that sums the partials in block order.  Used off the headline path (EF-sign mean, one-bit).
+constexpr int kRedBlocks = 1024;
+
+template <int K>
+struct Partials { double v[K]; };
+
+template <typename Acc>
+__global__ __launch_bounds__(kBlock) void reduce_partials(const float* x, int64_t n, Acc acc,
+                                                           double* part) {
+  constexpr int K = Acc::K;
+  double s[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) s[j] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc.add(x[i], s);
+  __shared__ double sh[K][kBlock / kWave];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double v = wave_sum(s[j]);
+    if ((threadIdx.x & 63) == 0) sh[j][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      double t = 0.0;
+      for (int w = 0; w < kBlock / kWave; ++w) t += sh[j][w];
+      part[(int64_t)j * gridDim.x + blockIdx.x] = t;
+    }
+  }
+}
+
+template <typename Fin>
+__global__ __launch_bounds__(kBlock) void reduce_finish(const double* part, int nparts, Fin fin) {
+  constexpr int K = Fin::K;
+  __shared__ double sh[K][kBlock];
+  for (int j = 0; j < K; ++j) {
+    double t = 0.0;
+    for (int b = threadIdx.x; b < nparts; b += blockDim.x) t += part[(int64_t)j * nparts + b];
+    sh[j][threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot[K];
+    for (int j = 0; j < K; ++j) {
+      double t = 0.0;
+      for (int b = 0; b < kBlock; ++b) t += sh[j][b];
+      tot[j] = t;
+    }
+    fin.finish(tot);
+  }
+}
+
+struct AbsSumAcc {
+  static constexpr int K = 1;
+  __device__ void add(float v, double* s) const { s[0] += fabs((double)v); }
+};
+struct AbsMeanFin {
+  static constexpr int K = 1;
+  int64_t n; float* out;
+  __device__ void finish(const double* t) const { out[0] = (float)t[0] / (float)n; }
+};
+
+// one-bit: sum0 over x<0, num0, sum1 over !(x<0) (NaN included, as ~mask0 in onebit.py:18)
+struct OneBitAcc {
+  static constexpr int K = 3;
+  __device__ void add(float v, double* s) const {
+    if (v < 0.f) { s[0] += (double)v; s[1] += 1.0; } else { s[2] += (double)v; }
+  }
+};
+struct OneBitFin {
+  static constexpr int K = 3;
+  int64_t n; float* out;
+  __device__ void finish(const double* t) const {
+    const float sum0 = (float)t[0], num0 = (float)t[1], sum1 = (float)t[2];
+    const float num1 = (float)n - num0;
+    out[0] = num0 > 0.f ? sum0 / num0 : sum0;
+    out[1] = num1 > 0.f ? sum1 / num1 : sum1;
+  }
+};
+
+template <typename Acc, typename Fin>
+static grace_status_t run_reduce(const char* name, const float* x, int64_t n, Acc acc, Fin fin,
+                                 void* ws, void* stream) {
+  const int blocks = (int)stream_grid(n, kBlock, kRedBlocks);
+  double* part = reinterpret_cast<double*>(ws);
+  reduce_partials<Acc><<<blocks, kBlock, 0, as_stream(stream)>>>(x, n, acc, part);
+  GRACE_CHECK_LAUNCH(name);
+  reduce_finish<Fin><<<1, kBlock, 0, as_stream(stream)>>>(part, blocks, fin);
+  GRACE_CHECK_LAUNCH(name);
+  return GRACE_OK;
+}
+
+}  // namespace grace
+
+using namespace grace;
+
+// ================================================================================================
+extern "C" {
+
+int grace_version(void) { return 100; }
+const char* grace_last_error(void) { return g_err; }
+
+grace_status_t grace_axpby(const float* r, const float* g, float beta, float gamma, float* t,
+                           int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && r && g && t, "grace_axpby: bad arguments");
+  return launch_stream("grace_axpby", AxpbyOp{r, g, beta, gamma, t}, n,
+                       aligned16(r) && aligned16(g) && aligned16(t), stream);
+}
+
+grace_status_t grace_sub(const float* t, const float* d, float* r, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && t && d && r, "grace_sub: bad arguments");
+  return launch_stream("grace_sub", SubOp{t, d, r}, n, aligned16(t) && aligned16(d) && aligned16(r),
+                       stream);
+}
+
+grace_status_t grace_div_scalar(const float* x, float divisor, float* out, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && x && out, "grace_div_scalar: bad arguments");
+  return launch_stream("grace_div_scalar", DivOp{x, divisor, out}, n, aligned16(x) && aligned16(out),
+                       stream);
+}
+
+grace_status_t grace_fill(float* x, float value, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && x, "grace_fill: bad arguments");
+  return launch_stream("grace_fill", FillOp{value, x}, n, aligned16(x), stream);
+}
+
+grace_status_t grace_accumulate(float* acc, const float* x, int64_t n, int32_t first, void* stream) {
+  GRACE_REQUIRE(n >= 0 && acc && x, "grace_accumulate: bad arguments");
+  return launch_stream("grace_accumulate", AccOp{acc, x, first}, n, aligned16(acc) && aligned16(x),
+                       stream);
+}
+
+grace_status_t grace_sign_encode(const float* x, uint8_t* codes, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && x && codes, "grace_sign_encode: bad arguments");
+  return launch_stream("grace_sign_encode", SignEncOp{x, codes}, n, aligned16(x) && aligned4(codes),
+                       stream);
+}
+
+grace_status_t grace_sign_decode(const uint8_t* codes, const float* scale_dev, float* out, int64_t n,
+                                 void* stream) {
+  GRACE_REQUIRE(n >= 0 && codes && out, "grace_sign_decode: bad arguments");
+  return launch_stream("grace_sign_decode", SignDecOp{codes, scale_dev, out}, n,
+                       aligned4(codes) && aligned16(out), stream);
+}
+
+grace_status_t grace_sign_majority(const uint8_t* codes_wn, int32_t world, float* out, int64_t n,
+                                   void* stream) {
+  GRACE_REQUIRE(n >= 0 && world >= 1 && codes_wn && out, "grace_sign_majority: bad arguments");
+  return launch_stream("grace_sign_majority", SignMajOp{codes_wn, world, n, out}, n,
+                       aligned4(codes_wn) && (n % 4 == 0) && aligned16(out), stream);
+}
+
+grace_status_t grace_signum_encode(const float* g, float* momentum, int32_t has_prev, float coef_g,
+                                   float coef_m, uint8_t* codes, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && g && momentum && codes, "grace_signum_encode: bad arguments");
+  return launch_stream("grace_signum_encode", SignumOp{g, momentum, has_prev, coef_g, coef_m, codes}, n,
+                       aligned16(g) && aligned16(momentum) && aligned4(codes), stream);
+}
+
+grace_status_t grace_sign_step_w1(const float* x, uint8_t* codes, float* out, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && x && codes && out, "grace_sign_step_w1: bad arguments");
+  return launch_stream("grace_sign_step_w1", SignStepOp{x, codes, out}, n,
+                       aligned16(x) && aligned4(codes) && aligned16(out), stream);
+}
+
+size_t grace_reduce_workspace_bytes(int64_t n) {
+  (void)n;
+  return sizeof(double) * 4 * kRedBlocks;
+}
+
+grace_status_t grace_abs_mean(const float* x, int64_t n, float* out_dev, void* ws, void* stream) {
+  GRACE_REQUIRE(n > 0 && x && out_dev && ws, "grace_abs_mean: bad arguments");
+  return run_reduce("grace_abs_mean", x, n, AbsSumAcc{}, AbsMeanFin{n, out_dev}, ws, stream);
+}
+
+grace_status_t grace_onebit_encode(const float* x, int64_t n, uint8_t* mask0, float* means_dev,
+                                   void* ws, void* stream) {
+  GRACE_REQUIRE(n > 0 && x && mask0 && means_dev && ws, "grace_onebit_encode: bad arguments");
+  // mask0 = (x < 0) is the complement of (x >= 0) only for non-NaN; compute it directly
+  struct LtOp {
+    const float* x; uint8_t* c;
+    __device__ void vec(int64_t i) const {
+      float4 v = reinterpret_cast<const float4*>(x)[i];
+      reinterpret_cast<uint32_t*>(c)[i] = (uint32_t)(v.x < 0.f) | ((uint32_t)(v.y < 0.f) << 8) |
+                                           ((uint32_t)(v.z < 0.f) << 16) | ((uint32_t)(v.w < 0.f) << 24);
+    }
+    __device__ void one(int64_t i) const { c[i] = (uint8_t)(x[i] < 0.f); }
+  };
+  grace_status_t s = launch_stream("grace_onebit_encode", LtOp{x, mask0}, n,
+                                   aligned16(x) && aligned4(mask0), stream);
+  if (s != GRACE_OK) return s;
+  return run_reduce("grace_onebit_encode", x, n, OneBitAcc{}, OneBitFin{n, means_dev}, ws, stream);
+}
+
+grace_status_t grace_onebit_decode(const uint8_t* mask0, const float* mean0_dev, const float* mean1_dev,
+                                   int32_t quirk, float* out, int64_t n, void* stream) {
+  GRACE_REQUIRE(n >= 0 && mask0 && mean0_dev && mean1_dev && out, "grace_onebit_decode: bad arguments");
+  return launch_stream("grace_onebit_decode", OneBitDecOp{mask0, mean0_dev, mean1_dev, quirk, out}, n,
+                       aligned4(mask0) && aligned16(out), stream);
+}
+
+}  // extern "C"

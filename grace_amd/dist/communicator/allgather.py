@@ -1,0 +1,73 @@
+"""Allgather communicator (grace_dl/dist/communicator/allgather.py:7-45) over torch.distributed
+(RCCL on ROCm).
+
+Differences from the reference that callers cannot observe:
+  * each payload tensor moves with one ``all_gather_into_tensor`` into a contiguous rank-major
+    buffer (no per-rank list of tensors), and compressors that provide
+    ``decode_aggregate_gathered`` decode + aggregate + average all W payloads in one native pass;
+  * at world_size 1 no collective is issued (the gathered list is the local payload), so no
+    process group is required;
+  * variable-size payloads exchange their sizes as a tensor on the payload's own device
+    (the reference hard-codes ``.cuda()``, allgather.py:16).
+"""
+import torch
+import torch.distributed as dist
+
+from grace_amd.dist import Communicator
+from grace_amd.dist._util import divide
+
+
+def _gather_flat(t, world_size):
+    flat = t.contiguous().view(-1)
+    if world_size == 1:
+        return flat
+    out = torch.empty(world_size * flat.numel(), dtype=flat.dtype, device=flat.device)
+    dist.all_gather_into_tensor(out, flat)
+    return out
+
+
+class Allgather(Communicator):
+    def send_receive(self, tensors, name, ctx):
+        W = int(self.world_size)
+        if self.compressor.tensors_size_are_same:
+            gathered = [_gather_flat(t, W) for t in tensors]
+            fast = getattr(self.compressor, "decode_aggregate_gathered", None)
+            if fast is not None:
+                out = fast(gathered, ctx, W)
+                if out is not None:
+                    return out
+            per_rank = [[g.view(W, -1)[r].view(t.shape) for g, t in zip(gathered, tensors)] for r in range(W)]
+        else:
+            per_rank = self._gather_variable(tensors, W)
+            fast = getattr(self.compressor, "decode_aggregate_variable", None)
+            if fast is not None:
+                out = fast(per_rank, ctx, W)
+                if out is not None:
+                    return out
+        decompressed_list = [self.compressor.decompress(tc, ctx) for tc in per_rank]
+        tensors_aggregated = self.compressor.aggregate(decompressed_list)
+        return divide(tensors_aggregated, W) if self.compressor.average else tensors_aggregated
+
+    @staticmethod
+    def _gather_variable(tensors, W):
+        """Size exchange + padded all-gather + trim (allgather.py:15-38)."""
+        if W == 1:
+            return [list(tensors)]
+        dev = tensors[0].device
+        local_sizes = torch.tensor([t.numel() for t in tensors], dtype=torch.int64, device=dev)
+        all_sizes = torch.empty(W * len(tensors), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(all_sizes, local_sizes)
+        sizes = all_sizes.view(W, len(tensors)).cpu().tolist()
+        per_rank = [[] for _ in range(W)]
+        for j, t in enumerate(tensors):
+            max_size = max(sizes[r][j] for r in range(W))
+            flat = t.contiguous().view(-1)
+            if flat.numel() != max_size:
+                padded = torch.zeros(max_size, dtype=flat.dtype, device=flat.device)
+                padded[:flat.numel()] = flat
+                flat = padded
+            out = torch.empty(W * max_size, dtype=flat.dtype, device=flat.device)
+            dist.all_gather_into_tensor(out, flat)
+            for r in range(W):
+                per_rank[r].append(out[r * max_size: r * max_size + sizes[r][j]])
+        return per_rank

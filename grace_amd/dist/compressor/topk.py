@@ -1,0 +1,75 @@
+"""Top-k sparsification (grace_dl/dist/compressor/topk.py:32-69) on the HIP top-k engine
+(grace_amd/csrc/topk.hip).
+
+Payload = [values f32[k], indices int32[k]] exactly as the reference (topk.py:41-42), ctx =
+``tensor.size()``.  The selected set equals torch.topk(|x|, k, sorted=False)'s modulo ties at the
+k-th magnitude; ours breaks ties by lower index.  ``kernel`` ('torch' | 'cupy' | 'rdxtopk_cuda',
+topk.py:35-40) is accepted for compatibility: every value selects the same exact native selector.
+"""
+import torch
+import torch.distributed as dist
+
+from grace_amd import ops
+from grace_amd.dist import Compressor
+
+
+class TopKCompressor(Compressor):
+
+    def __init__(self, compress_ratio, kernel='torch'):
+        super().__init__()
+        self.compress_ratio = compress_ratio
+        self.kernel = kernel
+
+    def compress(self, tensor, name):
+        flat = ops.dev_f32(tensor)
+        k = ops.ratio_k(flat.numel(), self.compress_ratio)
+        _, vals, idx = ops.topk_compress(flat, k)
+        return [vals, idx], tensor.size()
+
+    def decompress(self, tensors, ctx):
+        """Zeros with the values scattered back, reshaped to the original shape (topk.py:64-69)."""
+        vals, idx = tensors
+        return ops.sparse_decode(vals, idx, ctx.numel()).view(ctx)
+
+    def decode_aggregate_gathered(self, gathered, ctx, world_size):
+        """Allgather decode + aggregate + average of W same-size payloads in one rank-ordered
+        scatter pass (allgather.py:40-45).  gathered = [vals f32[W*k], idx i32[W*k]]."""
+        vals, idx = gathered
+        if not vals.is_cuda:
+            return None
+        k = vals.numel() // world_size
+        divisor = world_size if self.average else 1
+        out = ops.sparse_aggregate(vals, idx, k, [k] * world_size, world_size, ctx.numel(), divisor)
+        return out.view(ctx)
+
+    def fused_step(self, communicator, tensor, name):
+        """compensate -> compress -> update -> send_receive for (TopK, Residual|None, Allgather)."""
+        from grace_amd.dist.communicator.allgather import Allgather
+        from grace_amd.dist.memory.residual import ResidualMemory
+        mem = communicator.memory
+        if not (isinstance(communicator, Allgather) and type(mem) is ResidualMemory
+                and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
+            return None
+        g = ops.dev_f32(tensor)
+        n = g.numel()
+        k = ops.ratio_k(n, self.compress_ratio)
+        res = mem.residuals.get(name)
+        has = res is not None and res.numel() == n and res.device == g.device
+        if not has:
+            res = torch.empty_like(g)
+        world = int(communicator.world_size)
+        if world == 1:
+            out = torch.empty_like(g)
+            ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out)
+            mem.residuals[name] = res
+            if not self.average:
+                return out.view(tensor.shape)
+            return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
+        buf, _, _ = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None)
+        mem.residuals[name] = res
+        gathered = torch.empty(world * 2 * k, dtype=torch.float32, device=g.device)
+        dist.all_gather_into_tensor(gathered, buf)
+        divisor = world if self.average else 1
+        out = ops.sparse_aggregate(gathered, gathered[k:].view(torch.int32), 2 * k, [k] * world, world,
+                                   n, divisor)
+        return out.view(tensor.shape)

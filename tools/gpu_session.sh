@@ -1,0 +1,35 @@
+#!/bin/bash
+# GPU-box session runner: each GPU step under its own timeout; stop at the first crash / timeout
+# (a plain test failure, exit 1, does not stop the session).  Logs under gpurun_out/.
+# usage: tools/gpu_session.sh STEP [STEP ...]   (steps: smoke pytest bench prof pmc)
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1
+TAG="${SESSION_TAG:-r01}"
+
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 15 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "STOP: $name exited with $rc"; exit $rc
+  fi
+  return 0
+}
+
+for step in "$@"; do
+  case "$step" in
+    smoke)  run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 1200 python3 -m pytest tests -m gpu -x -q ;;
+    pytestall) run pytest_gpu_all 1200 python3 -m pytest tests -m gpu -q ;;
+    bench)  run bench 600 python3 bench.py ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$ROOT/gpurun_out/prof_$TAG" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
