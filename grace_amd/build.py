@@ -39,13 +39,20 @@ def _compile(src, obj, verbose):
     return obj
 
 
-def build(verbose=False, jobs=8):
-    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+def build(verbose=False, jobs=8, variant=""):
+    """variant "stamps" builds the diagnostic libgrace_hip_stamps.so (-DGRACE_STAMPS)."""
+    global FLAGS, LIB
+    if variant:
+        defs = {"stamps": ["-DGRACE_STAMPS"]}
+        FLAGS = FLAGS + defs.get(variant, [f"-DGRACE_{variant.upper()}"])
+        LIB = os.path.join(LIBDIR, f"libgrace_hip_{variant}.so")
+    objdir = os.path.join(LIBDIR, "obj" + (f"_{variant}" if variant else ""))
+    os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     dep_t = _newest_dep()
     todo, objs = [], []
     for s in srcs:
-        o = os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o")
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), dep_t):
             todo.append((s, o))
@@ -62,4 +69,5 @@ def build(verbose=False, jobs=8):
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    var = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")), "")
+    print(build(verbose="-v" in sys.argv, variant=var))

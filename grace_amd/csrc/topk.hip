@@ -41,15 +41,14 @@ enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2 };
 constexpr int kMainBlock = 256;
 constexpr int kMainVec = 16;                               // float4 per thread
 constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 16384 elements per workgroup
-constexpr int kHistBins = 4096;                            // candidate histogram
-constexpr int kStage = 1024;                               // LDS staging entries per list
+constexpr int kHistBins = 2048;                            // candidate histogram
+constexpr int kStage = 512;                                // LDS staging entries per list
 constexpr int kSelBlock = 1024;                            // single-workgroup selectors
 constexpr int kSmallN = 32768;                             // single-workgroup path
 constexpr int kSampleRunLen = 16;
 constexpr int kSampleRuns = 2048;
 constexpr int kSample = kSampleRuns * kSampleRunLen;       // 32768 keys, 32 per thread
 constexpr int kFinBlocks = 256;
-constexpr int kFinBlock = 256;
 
 struct TopkCtl {
   uint32_t thr_lo;
@@ -62,13 +61,40 @@ struct TopkCtl {
   uint32_t n_bnd;
   int32_t boundary_bin;
   uint32_t need;
-  uint32_t pad[6];
+  uint32_t ticket;     // finalize kernel arrival counter
+  uint32_t unused;
+  uint32_t pad[4];
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 
+// Diagnostic build only (-DGRACE_STAMPS): s_memrealtime stamps (100 MHz) at phase boundaries,
+// stored in the free tail of the 256-byte ctl block of the workspace.  Never in shipped builds.
+#ifdef GRACE_STAMPS
+#define STAMP_IF(cond, ctlp, slot)                                                                 \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && (cond))                                                                \
+      reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ctlp) + 64)[slot] =                     \
+          __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
+#else
+#define STAMP_IF(cond, ctlp, slot) do { } while (0)
+#endif
+#define STAMP(ctlp, slot) STAMP_IF(blockIdx.x == 0, ctlp, slot)
+
+constexpr int kSampleMax = 131072;                         // stratified sample size
+constexpr int kSampleBlock = 1024;
+constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
+constexpr int kCursorStride = 32;                          // one placement cursor per 128-B line
+constexpr int kHistStride = 1;
+
+// Workspace layout.  Every counter / histogram region is left zeroed by the step that used it
+// (the select kernel re-zeroes what the next step accumulates into), so the caller only has to
+// zero the workspace once, at allocation.
 struct TopkWs {
   TopkCtl* ctl;
-  uint32_t* hist;
+  uint32_t* hist;      // candidate histogram [kHistBins]
+  uint32_t* cursor;    // per-bin placement cursors [kHistBins * kCursorStride]
+  uint32_t* shist;     // sample histogram [kBracketBins]
   int2* cand;
   int2* bnd;
   int64_t cap;
@@ -88,7 +114,11 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   w.ctl = reinterpret_cast<TopkCtl*>(p);
   p += 256;
   w.hist = reinterpret_cast<uint32_t*>(p);
-  p += align256(sizeof(uint32_t) * kHistBins);
+  p += align256(sizeof(uint32_t) * kHistBins * kHistStride);
+  w.cursor = reinterpret_cast<uint32_t*>(p);
+  p += align256(sizeof(uint32_t) * kHistBins * kCursorStride);
+  w.shist = reinterpret_cast<uint32_t*>(p);
+  p += align256(sizeof(uint32_t) * kBracketBins);
   w.cand = reinterpret_cast<int2*>(p);
   p += align256(sizeof(int2) * w.cap);
   w.bnd = reinterpret_cast<int2*>(p);
@@ -97,7 +127,9 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
 
 static size_t ws_bytes(int64_t n, int64_t k) {
   const int64_t cap = topk_cap(n, k);
-  return 256 + align256(sizeof(uint32_t) * kHistBins) + 2 * align256(sizeof(int2) * cap);
+  return 256 + align256(sizeof(uint32_t) * kHistBins * kHistStride) +
+         align256(sizeof(uint32_t) * kHistBins * kCursorStride) + align256(sizeof(uint32_t) * kBracketBins) +
+         2 * align256(sizeof(int2) * cap);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -152,37 +184,54 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
   return r;
 }
 
-// Given a histogram hist[NBINS] (in LDS or global) find the bin d, scanning from the top, where
-// the running count reaches `rank` (1-based): sum_{b>d} < rank <= sum_{b>=d}.  Returns d and
-// writes above = sum_{b>d}.  All BLOCK threads must call.  NBINS % BLOCK == 0.
-template <int BLOCK, int NBINS>
-__device__ int find_bin_desc(const uint32_t* hist, uint32_t rank, uint32_t* s_w, uint32_t* s_res,
-                             uint32_t* above_out) {
+// Given a histogram hist[NBINS] (in LDS or global) find, scanning from the top, the bin d where
+// the running count reaches `rank` (1-based): sum_{b>d} < rank <= sum_{b>=d}, for NR ranks at
+// once (one block scan).  Returns d[q] and above[q] = sum_{b>d[q]}.  All BLOCK threads must call;
+// NBINS % BLOCK == 0; s_res needs 2*NR words.
+template <int BLOCK, int NBINS, int NR>
+__device__ void find_bins_desc(const uint32_t* hist, const uint32_t (&rank)[NR], uint32_t* s_w,
+                               uint32_t* s_res, int (&d)[NR], uint32_t (&above)[NR]) {
   constexpr int PER = NBINS / BLOCK;
   const int t = threadIdx.x;
   const int top = NBINS - 1 - t * PER;  // this thread covers bins top, top-1, ..., top-PER+1
   uint32_t s = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) s += hist[top - j];
-  if (t == 0) { s_res[0] = 0; s_res[1] = 0; }
+  if (t < 2 * NR) s_res[t] = 0;
   const uint32_t ex = block_excl_scan<BLOCK>(s, s_w, nullptr);
-  if (ex < rank && rank <= ex + s) {
-    uint32_t acc = ex;
-    for (int j = 0; j < PER; ++j) {
-      const uint32_t h = hist[top - j];
-      if (acc + h >= rank) {
-        s_res[0] = (uint32_t)(top - j);
-        s_res[1] = acc;
-        break;
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    if (ex < rank[q] && rank[q] <= ex + s) {
+      uint32_t acc = ex;
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t h = hist[top - j];
+        if (acc + h >= rank[q]) {
+          s_res[2 * q] = (uint32_t)(top - j);
+          s_res[2 * q + 1] = acc;
+          break;
+        }
+        acc += h;
       }
-      acc += h;
     }
   }
   __syncthreads();
-  const int d = (int)s_res[0];
-  if (above_out) *above_out = s_res[1];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    d[q] = (int)s_res[2 * q];
+    above[q] = s_res[2 * q + 1];
+  }
   __syncthreads();
-  return d;
+}
+
+template <int BLOCK, int NBINS>
+__device__ int find_bin_desc(const uint32_t* hist, uint32_t rank, uint32_t* s_w, uint32_t* s_res,
+                             uint32_t* above_out) {
+  const uint32_t r[1] = {rank};
+  int d[1];
+  uint32_t ab[1];
+  find_bins_desc<BLOCK, NBINS, 1>(hist, r, s_w, s_res, d, ab);
+  if (above_out) *above_out = ab[0];
+  return d[0];
 }
 
 // composite selection key: larger |t| first, then lower index first; unique per element
@@ -217,9 +266,15 @@ __device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Streaming accesses of the bucket are non-temporal (touched once per step): on gfx950 the
+// nt 16-B loads+stores lift the 2-read/2-write stream from ~5.1 to ~6.4 TB/s (tools/hbm_probe).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <bool VEC>
 __device__ __forceinline__ float4 load4(const float* p, int64_t i, int64_t n) {
-  if (VEC && i + 3 < n) return *reinterpret_cast<const float4*>(p + i);
+  if (VEC && i + 3 < n) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
   float4 v;
   v.x = i < n ? p[i] : 0.f;
   v.y = i + 1 < n ? p[i + 1] : 0.f;
@@ -230,7 +285,8 @@ __device__ __forceinline__ float4 load4(const float* p, int64_t i, int64_t n) {
 template <bool VEC>
 __device__ __forceinline__ void store4(float* p, int64_t i, int64_t n, float4 v) {
   if (VEC && i + 3 < n) {
-    *reinterpret_cast<float4*>(p + i) = v;
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p + i));
     return;
   }
   if (i < n) p[i] = v.x;
@@ -253,6 +309,8 @@ struct StepArgs {
   float* vals;
   int32_t* idx;
   float* out;          // dense output (kDenseFused)
+  int64_t sample_n;    // stratified sample size (<= kSampleMax)
+  int64_t stratum;     // n / sample_n
 };
 
 template <bool HAS_RES>
@@ -262,91 +320,110 @@ __device__ __forceinline__ float compensate(const StepArgs& a, int64_t i) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// 1. bracket: one workgroup of 1024 threads
+// 1. bracket = sample (sample_n/1024 workgroups) + select (one workgroup).
+//
+// sample: every thread takes one element from its stratum of n / sample_n at a hashed offset
+// (single elements, so spatially correlated gradients do not inflate the sample variance) and
+// counts its key's top 16 bits (key >> 16: 1/64-octave bins) in an LDS histogram; non-zero bins
+// are flushed with one global atomic each.
+// select: reads the 32768-bin histogram with coalesced loads, finds both bracketing sample ranks
+// with one block scan, rounds the thresholds OUTWARD to bin edges (the rounding only widens the
+// candidate band) and re-zeroes the histogram and every counter the next kernels accumulate into.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+
 template <bool HAS_RES>
-__global__ __launch_bounds__(kSelBlock) void topk_bracket(StepArgs a, TopkWs w) {
-  __shared__ uint32_t hist1[16384];
-  __shared__ uint32_t hist2[2][2048];
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
+__global__ __launch_bounds__(kSampleBlock) void topk_sample(StepArgs a, TopkWs w) {
+  __shared__ uint32_t lh[kBracketBins];
   const int tid = threadIdx.x;
-  // zero this step's global state
-  if (tid < (int)(sizeof(TopkCtl) / 4)) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
-  for (int b = tid; b < kHistBins; b += kSelBlock) w.hist[b] = 0;
-  for (int b = tid; b < 16384; b += kSelBlock) hist1[b] = 0;
-
-  // sample: 2048 runs of 16 contiguous elements, one run start per stratum
-  const int64_t n = a.n;
-  const int64_t stratum = n / kSampleRuns;   // n > kSmallN guarantees stratum >= 16
-  const int lane16 = tid & 15;
-  constexpr int PER = kSample / kSelBlock;   // 32 keys per thread
-  uint32_t keys[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int run = (tid >> 4) + j * (kSelBlock / 16);
-    const uint64_t off = mix64(0x5EEDull + (uint64_t)run) % (uint64_t)(stratum - kSampleRunLen + 1);
-    const int64_t i = (int64_t)run * stratum + (int64_t)off + lane16;
-    keys[j] = abs_key(compensate<HAS_RES>(a, i));
+  STAMP(w.ctl, 0);
+  // issue the sample load first: its latency hides the LDS clear
+  const int64_t sidx = (int64_t)blockIdx.x * kSampleBlock + tid;
+  const bool valid = sidx < a.sample_n;
+  float t = 0.f;
+  if (valid) {
+    const uint32_t st = (uint32_t)a.stratum;
+    const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+    t = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
   }
+  for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
   __syncthreads();
+  STAMP(w.ctl, 1);
+  if (valid) atomicAdd(&lh[abs_key(t) >> 16], 1u);
+  __syncthreads();
+  for (int b = tid; b < kBracketBins; b += kSampleBlock)
+    if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
+  STAMP(w.ctl, 2);
+}
+
+// Conflict-free chunk sums of an LDS histogram: thread t owns bins [PER*t, PER*t+PER) but reads
+// them in a lane-rotated order so the 32 lanes of a half-wave hit 32 different banks.
+template <int BLOCK, int NBINS>
+__device__ __forceinline__ uint32_t chunk_sum_rot(const uint32_t* h, int t) {
+  constexpr int PER = NBINS / BLOCK;
+  uint32_t s = 0;
+#pragma unroll 8
+  for (int j = 0; j < PER; ++j) s += h[t * PER + ((j + t) & (PER - 1))];
+  return s;
+}
+
+__global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
+  constexpr int PER = kBracketBins / kSelBlock;   // 32
+  __shared__ uint32_t lh[kBracketBins];
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  __shared__ uint32_t s_res[4];
+  const int tid = threadIdx.x;
+  STAMP(w.ctl, 3);
+  // coalesced copy of the global sample histogram into LDS, re-zeroing it behind us
+  const uint4* gh = reinterpret_cast<const uint4*>(w.shist);
+  uint4* lh4 = reinterpret_cast<uint4*>(lh);
+#pragma unroll
+  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) lh4[tid + j * kSelBlock] = gh[tid + j * kSelBlock];
+  __syncthreads();
+  uint4* gz = reinterpret_cast<uint4*>(w.shist);
+#pragma unroll
+  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
+  STAMP(w.ctl, 4);
+  const int64_t S = a.sample_n;
   // sample ranks (descending, 0-based) bracketing the k-th largest with ~6 sigma
-  const double p = (double)a.k / (double)n;
-  const double mu = p * kSample;
+  const double p = (double)a.k / (double)a.n;
+  const double mu = p * (double)S;
   const double sd = sqrt(mu * (1.0 - p) + 1.0);
-  const double hi_d = floor(mu - 6.0 * sd - 2.0);
-  const double lo_d = ceil(mu + 6.0 * sd + 2.0);
-  const int64_t rank_hi = (int64_t)hi_d;   // may be negative: nothing is "sure"
-  const int64_t rank_lo = (int64_t)lo_d;   // may be >= kSample: everything is a candidate
-
-  // pass 1: 14-bit digit = key >> 17
+  const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
+  const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
+  const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
+                          (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1)};
+  // descending scan: thread t owns the chunk of bins [PER*(NT-1-t), PER*(NT-1-t)+PER)
+  const int chunk = kSelBlock - 1 - tid;
+  const uint32_t sum = chunk_sum_rot<kSelBlock, kBracketBins>(lh, chunk);
+  if (tid < 4) s_res[tid] = 0;
+  const uint32_t ex = block_excl_scan<kSelBlock>(sum, s_w, nullptr);
 #pragma unroll
-  for (int j = 0; j < PER; ++j) atomicAdd(&hist1[keys[j] >> 17], 1u);
-  __syncthreads();
-  uint32_t thr[2];
-  const int64_t ranks[2] = {rank_hi, rank_lo};
-  uint32_t d1[2], rem[2];
   for (int q = 0; q < 2; ++q) {
-    const int64_t rk = ranks[q];
-    const uint32_t r1 = (uint32_t)((rk < 0 ? 0 : (rk >= kSample ? kSample - 1 : rk)) + 1);  // 1-based
-    uint32_t above;
-    d1[q] = (uint32_t)find_bin_desc<kSelBlock, 16384>(hist1, r1, s_w, s_res, &above);
-    rem[q] = r1 - above;
-  }
-  // pass 2: 11-bit digit (key >> 6) & 2047 within each target's 14-bit prefix
-  for (int b = tid; b < 2048; b += kSelBlock) { hist2[0][b] = 0; hist2[1][b] = 0; }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t kk = keys[j];
-    for (int q = 0; q < 2; ++q)
-      if ((kk >> 17) == d1[q]) atomicAdd(&hist2[q][(kk >> 6) & 2047], 1u);
+    if (ex < r1[q] && r1[q] <= ex + sum) {
+      uint32_t acc = ex;
+      for (int j = PER - 1; j >= 0; --j) {
+        const uint32_t h = lh[chunk * PER + j];
+        if (acc + h >= r1[q]) { s_res[q] = (uint32_t)(chunk * PER + j); break; }
+        acc += h;
+      }
+    }
   }
   __syncthreads();
-  uint32_t d2[2];
-  for (int q = 0; q < 2; ++q) {
-    uint32_t above;
-    d2[q] = (uint32_t)find_bin_desc<kSelBlock, 2048>(hist2[q], rem[q], s_w, s_res, &above);
-    rem[q] -= above;
-  }
-  // pass 3: 6-bit digit key & 63 within the 25-bit prefix
-  for (int b = tid; b < 2048; b += kSelBlock) { hist2[0][b] = 0; hist2[1][b] = 0; }
+  const uint32_t d0 = s_res[0], d1 = s_res[1];
+  // re-zero the state the next kernels accumulate into
+  for (int b = tid; b < kHistBins; b += kSelBlock) { w.hist[b * kHistStride] = 0; w.cursor[b * kCursorStride] = 0; }
+  if (tid < (int)(sizeof(TopkCtl) / 4)) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const uint32_t kk = keys[j];
-    for (int q = 0; q < 2; ++q)
-      if ((kk >> 6) == ((d1[q] << 11) | d2[q])) atomicAdd(&hist2[q][kk & 63], 1u);
-  }
-  __syncthreads();
-  for (int q = 0; q < 2; ++q) {
-    uint32_t above;
-    const uint32_t d3 = (uint32_t)find_bin_desc<kSelBlock, 2048>(hist2[q], rem[q], s_w, s_res, &above);
-    thr[q] = (d1[q] << 17) | (d2[q] << 6) | d3;
-  }
   if (tid == 0) {
-    uint32_t hi = thr[0], lo = thr[1];
-    if (rank_hi < 0) hi = 0x7FFFFFFFu;          // no element can exceed: nothing is sure
-    if (rank_lo >= kSample) lo = 0u;            // everything is a candidate
+    // sure = key > hi: round up to the top of the bin (fewer sure); candidates start at the bottom
+    // of the low bin (more candidates)
+    uint32_t hi = (d0 << 16) | 0xFFFFu;
+    uint32_t lo = d1 << 16;
+    if (rank_hi < 0) hi = 0x7FFFFFFFu;
+    if (rank_lo >= S) lo = 0u;
     if (lo > hi) lo = hi;
     uint32_t sh = 0;
     const uint64_t span = (uint64_t)hi - (uint64_t)lo;   // keys lo..hi -> bins 0..span>>sh
@@ -355,211 +432,215 @@ __global__ __launch_bounds__(kSelBlock) void topk_bracket(StepArgs a, TopkWs w) 
     w.ctl->thr_hi = hi;
     w.ctl->shift = sh;
   }
+  STAMP(w.ctl, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
 // 2. main streaming pass
+//
+// Each workgroup streams one 16384-element chunk: 4 groups of 4 float4 per lane per array, with
+// the next group's loads issued before the current group is classified (16-B loads, 8 in flight
+// per lane).  Per group every lane counts its sure / candidate elements, one wave-wide prefix
+// scan (packed 16|16 bits) places them, and ONE LDS atomic per wave per group reserves staging
+// space; the staged entries leave with one global atomic per workgroup at the end.
+constexpr int kGroup = 4;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// FAST = aligned buffers and a chunk entirely inside the bucket: unconditional nt 16-B loads and
+// stores (a guarded load makes hipcc wait vmcnt(0) at the merge, serialising every load).
+template <bool FAST>
+__device__ __forceinline__ float4 ld4(const float* p, int64_t i, int64_t n) {
+  if constexpr (FAST) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return load4<false>(p, i, n);
+  }
+}
+template <bool FAST>
+__device__ __forceinline__ void st4(float* p, int64_t i, int64_t n, float4 v) {
+  if constexpr (FAST) {
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p + i));
+  } else {
+    store4<false>(p, i, n, v);
+  }
+}
+
+template <bool HAS_RES, bool FAST>
+__device__ __forceinline__ void load_group(const StepArgs& a, int64_t gbase, float4 (&rv)[kGroup],
+                                           float4 (&gv)[kGroup]) {
+#pragma unroll
+  for (int u = 0; u < kGroup; ++u) {
+    const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
+    if constexpr (HAS_RES) rv[u] = ld4<FAST>(a.r, i0, a.n);
+    gv[u] = ld4<FAST>(a.g, i0, a.n);
+  }
+}
+
+struct MainShared {
+  uint32_t hist[kHistBins];
+  int2 sure[kStage];
+  int2 cand[kStage];
+  uint32_t cnt[4];   // packed staged counts (sure | cand << 16), base_sure, base_cand
+};
+
+template <bool HAS_RES, int MODE, bool FAST>
+__device__ __forceinline__ void main_chunk(const StepArgs& a, const TopkWs& w, MainShared& sm,
+                                           uint32_t lo, uint32_t hi, uint32_t sh) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int64_t n = a.n;
+  constexpr int NG = kMainVec / kGroup;
+  const int64_t cbase = (int64_t)blockIdx.x * kMainChunk + (int64_t)tid * 4;
+  float4 rc[kGroup], gc[kGroup];
+  load_group<HAS_RES, FAST>(a, cbase, rc, gc);
+#pragma unroll 1
+  for (int q = 0; q < NG; ++q) {
+    const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
+    float4 rn[kGroup], gn[kGroup];
+    if (q + 1 < NG) load_group<HAS_RES, FAST>(a, gbase + kGroup * (kMainBlock * 4), rn, gn);
+    float4 t[kGroup];
+    uint32_t msure = 0, mcand = 0;   // bit u*4+j
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) {
+      if constexpr (HAS_RES) {
+        t[u].x = a.beta * rc[u].x + a.gamma * gc[u].x;
+        t[u].y = a.beta * rc[u].y + a.gamma * gc[u].y;
+        t[u].z = a.beta * rc[u].z + a.gamma * gc[u].z;
+        t[u].w = a.beta * rc[u].w + a.gamma * gc[u].w;
+      } else {
+        t[u] = gc[u];
+      }
+      const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
+      float4 rout = t[u], dout = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float tv = comp4(t[u], j);
+        const uint32_t key = abs_key(tv);
+        const bool valid = FAST || i0 + j < n;
+        const bool sure = valid && key > hi;
+        const bool cand = valid && !sure && key >= lo;
+        msure |= (uint32_t)sure << (u * 4 + j);
+        mcand |= (uint32_t)cand << (u * 4 + j);
+        if constexpr (MODE == kDenseFused) {
+          if (sure) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
+        }
+        if (cand) atomicAdd(&sm.hist[(key - lo) >> sh], 1u);
+      }
+      if constexpr (MODE == kDenseRes || MODE == kDenseFused) st4<FAST>(a.r, i0, n, rout);
+      if constexpr (MODE == kDenseFused) st4<FAST>(a.out, i0, n, dout);
+    }
+    // ---- place this group's sure / candidate elements
+    const uint32_t cs = __popc(msure), cc = __popc(mcand);
+    const uint32_t packed = cs | (cc << 16);
+    if (__ballot(packed != 0)) {
+      const uint32_t incl = wave_incl_scan(packed);
+      const uint32_t excl = incl - packed;
+      uint32_t bse = 0;
+      if (lane == 63) bse = atomicAdd(&sm.cnt[0], incl);
+      bse = __shfl(bse, 63, 64);
+      // this lane's entries occupy staging slots [ps0, ps0 + cs) and [pc0, pc0 + cc); slots past
+      // kStage overflow to the global lists (contiguous at the end of the lane's range)
+      const uint32_t ps0 = (bse & 0xFFFFu) + (excl & 0xFFFFu);
+      const uint32_t pc0 = (bse >> 16) + (excl >> 16);
+      const uint32_t over_s = ps0 + cs > (uint32_t)kStage ? min(ps0 + cs - (uint32_t)kStage, cs) : 0u;
+      const uint32_t over_c = pc0 + cc > (uint32_t)kStage ? min(pc0 + cc - (uint32_t)kStage, cc) : 0u;
+      uint32_t gs0 = 0, gc0 = 0;
+      if (__builtin_expect(__ballot(over_s | over_c) != 0, 0)) {
+        const uint32_t sp = over_s | (over_c << 16);
+        const uint32_t sincl = wave_incl_scan(sp);
+        uint32_t bs = 0, bc = 0;
+        if (lane == 63) {
+          if (sincl & 0xFFFFu) bs = atomicAdd(&w.ctl->n_sure, sincl & 0xFFFFu);
+          if (sincl >> 16) bc = atomicAdd(&w.ctl->n_cand, sincl >> 16);
+        }
+        gs0 = __shfl(bs, 63, 64) + ((sincl - sp) & 0xFFFFu);
+        gc0 = __shfl(bc, 63, 64) + ((sincl - sp) >> 16);
+      }
+      const uint32_t lim_s = max(ps0, (uint32_t)kStage), lim_c = max(pc0, (uint32_t)kStage);
+      uint32_t ps = ps0, pc = pc0;
+#pragma unroll
+      for (int u = 0; u < kGroup; ++u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int b = u * 4 + j;
+          const int64_t i = gbase + (int64_t)u * (kMainBlock * 4) + j;
+          const float tv = comp4(t[u], j);
+          if ((msure >> b) & 1u) {
+            if (ps < (uint32_t)kStage) {
+              sm.sure[ps] = make_int2((int)i, (int)f2u(tv));
+            } else {
+              const uint32_t gp = gs0 + (ps - lim_s);
+              if (gp < (uint32_t)a.k) { a.vals[gp] = tv; a.idx[gp] = (int32_t)i; }
+            }
+            ++ps;
+          }
+          if ((mcand >> b) & 1u) {
+            if (pc < (uint32_t)kStage) {
+              sm.cand[pc] = make_int2((int)i, (int)f2u(tv));
+            } else {
+              const uint32_t gp = gc0 + (pc - lim_c);
+              if (gp < (uint32_t)w.cap) w.cand[gp] = make_int2((int)i, (int)f2u(tv));
+            }
+            ++pc;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
+  }
+}
+
 template <bool HAS_RES, int MODE, bool VEC>
 __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
-  __shared__ uint32_t s_hist[kHistBins];
-  __shared__ int2 s_sure[kStage];
-  __shared__ int2 s_cand[kStage];
-  __shared__ uint32_t s_cnt[4];   // n_sure, n_cand, base_sure, base_cand
+  __shared__ MainShared sm;
   const int tid = threadIdx.x;
-  for (int b = tid; b < kHistBins; b += kMainBlock) s_hist[b] = 0;
-  if (tid < 4) s_cnt[tid] = 0;
+  for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
+  if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
   __syncthreads();
-
-  const int64_t n = a.n;
-  const int64_t base = (int64_t)blockIdx.x * kMainChunk;
-#pragma unroll 4
-  for (int it = 0; it < kMainVec; ++it) {
-    const int64_t i0 = base + (int64_t)it * (kMainBlock * 4) + (int64_t)tid * 4;
-    float4 t;
-    if constexpr (HAS_RES) {
-      const float4 rv = load4<VEC>(a.r, i0, n);
-      const float4 gv = load4<VEC>(a.g, i0, n);
-      t.x = a.beta * rv.x + a.gamma * gv.x;
-      t.y = a.beta * rv.y + a.gamma * gv.y;
-      t.z = a.beta * rv.z + a.gamma * gv.z;
-      t.w = a.beta * rv.w + a.gamma * gv.w;
-    } else {
-      t = load4<VEC>(a.g, i0, n);
-    }
-    float4 rout = t, dout = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t i = i0 + j;
-      const float tv = comp4(t, j);
-      const uint32_t key = abs_key(tv);
-      const bool valid = i < n;
-      const bool sure = valid && key > hi;
-      const bool cand = valid && !sure && key >= lo;
-      if constexpr (MODE == kDenseFused) {
-        if (sure) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
-      }
-      // ---- sure: straight into the payload
-      const uint64_t ms = __ballot(sure);
-      if (ms) {
-        uint32_t bse = 0;
-        if (lane_id() == 0) bse = atomicAdd(&s_cnt[0], (uint32_t)__popcll(ms));
-        bse = __shfl(bse, 0, 64);
-        const uint32_t pos = bse + lane_rank(ms);
-        const bool spill = sure && pos >= (uint32_t)kStage;
-        if (sure && !spill) s_sure[pos] = make_int2((int)i, (int)f2u(tv));
-        const uint64_t mspill = __ballot(spill);
-        if (mspill) {
-          uint32_t gb = 0;
-          if (lane_id() == 0) gb = atomicAdd(&w.ctl->n_sure, (uint32_t)__popcll(mspill));
-          gb = __shfl(gb, 0, 64);
-          const uint32_t gp = gb + lane_rank(mspill);
-          if (spill && gp < (uint32_t)a.k) { a.vals[gp] = tv; a.idx[gp] = (int32_t)i; }
-        }
-      }
-      // ---- candidates: list + histogram
-      const uint64_t mc = __ballot(cand);
-      if (mc) {
-        uint32_t bse = 0;
-        if (lane_id() == 0) bse = atomicAdd(&s_cnt[1], (uint32_t)__popcll(mc));
-        bse = __shfl(bse, 0, 64);
-        const uint32_t pos = bse + lane_rank(mc);
-        const bool spill = cand && pos >= (uint32_t)kStage;
-        if (cand) atomicAdd(&s_hist[(key - lo) >> sh], 1u);
-        if (cand && !spill) s_cand[pos] = make_int2((int)i, (int)f2u(tv));
-        const uint64_t mspill = __ballot(spill);
-        if (mspill) {
-          uint32_t gb = 0;
-          if (lane_id() == 0) gb = atomicAdd(&w.ctl->n_cand, (uint32_t)__popcll(mspill));
-          gb = __shfl(gb, 0, 64);
-          const uint32_t gp = gb + lane_rank(mspill);
-          if (spill && gp < (uint32_t)w.cap) w.cand[gp] = make_int2((int)i, (int)f2u(tv));
-        }
-      }
-    }
-    if constexpr (MODE == kDenseRes || MODE == kDenseFused) store4<VEC>(a.r, i0, n, rout);
-    if constexpr (MODE == kDenseFused) store4<VEC>(a.out, i0, n, dout);
-  }
+  if (VEC && (int64_t)(blockIdx.x + 1) * kMainChunk <= a.n)
+    main_chunk<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh);
+  else
+    main_chunk<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh);
   __syncthreads();
+  const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
+  const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
   if (tid == 0) {
-    const uint32_t ns = min(s_cnt[0], (uint32_t)kStage);
-    const uint32_t nc = min(s_cnt[1], (uint32_t)kStage);
-    s_cnt[2] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
-    s_cnt[3] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+    sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
+    sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
   }
   __syncthreads();
-  const uint32_t ns = min(s_cnt[0], (uint32_t)kStage), nc = min(s_cnt[1], (uint32_t)kStage);
   for (uint32_t j = tid; j < ns; j += kMainBlock) {
-    const uint32_t gp = s_cnt[2] + j;
+    const uint32_t gp = sm.cnt[1] + j;
     if (gp < (uint32_t)a.k) {
-      const int2 e = s_sure[j];
+      const int2 e = sm.sure[j];
       a.vals[gp] = u2f((uint32_t)e.y);
       a.idx[gp] = e.x;
     }
   }
   for (uint32_t j = tid; j < nc; j += kMainBlock) {
-    const uint32_t gp = s_cnt[3] + j;
-    if (gp < (uint32_t)w.cap) w.cand[gp] = s_cand[j];
+    const uint32_t gp = sm.cnt[2] + j;
+    if (gp < (uint32_t)w.cap) w.cand[gp] = sm.cand[j];
   }
   for (int b = tid; b < kHistBins; b += kMainBlock) {
-    const uint32_t h = s_hist[b];
-    if (h) atomicAdd(&w.hist[b], h);
+    const uint32_t h = sm.hist[b];
+    if (h) atomicAdd(&w.hist[b * kHistStride], h);
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// 3. finalize: boundary bin + candidate routing
-template <int MODE>
-__global__ __launch_bounds__(kFinBlock) void topk_finalize(StepArgs a, TopkWs w) {
-  __shared__ uint32_t s_w[kFinBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_cnt[4];
-  const TopkCtl c = *w.ctl;
-  const uint32_t k = (uint32_t)a.k;
-  const bool ok = c.n_sure <= k && (uint64_t)c.n_sure + c.n_cand >= k && c.n_cand <= (uint64_t)w.cap;
-  if (!ok) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->status = 1;
-    return;
-  }
-  const uint32_t target = k - c.n_sure;
-  int B = -1;
-  uint32_t need = 0;
-  if (target > 0) {
-    uint32_t above;
-    B = find_bin_desc<kFinBlock, kHistBins>(w.hist, target, s_w, s_res, &above);
-    need = target - above;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.ctl->boundary_bin = B;
-    w.ctl->need = need;
-  }
-  if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  // this workgroup's slice of the candidate list
-  const uint32_t nc = c.n_cand;
-  const uint32_t per = (nc + gridDim.x - 1) / gridDim.x;
-  const uint32_t b0 = blockIdx.x * per, b1 = min(nc, b0 + per);
-  uint32_t my_sel = 0, my_bnd = 0;
-  if (B >= 0) {
-    for (uint32_t j = b0 + threadIdx.x; j < b1; j += kFinBlock) {
-      const int2 e = w.cand[j];
-      const int bin = (int)((abs_key(u2f((uint32_t)e.y)) - c.thr_lo) >> c.shift);
-      my_sel += bin > B;
-      my_bnd += bin == B;
-    }
-  }
-  my_sel = wave_sum(my_sel);
-  my_bnd = wave_sum(my_bnd);
-  if ((threadIdx.x & 63) == 0) {
-    if (my_sel) atomicAdd(&s_cnt[0], my_sel);
-    if (my_bnd) atomicAdd(&s_cnt[1], my_bnd);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    s_cnt[2] = s_cnt[0] ? atomicAdd(&w.ctl->n_sel, s_cnt[0]) : 0u;
-    s_cnt[3] = s_cnt[1] ? atomicAdd(&w.ctl->n_bnd, s_cnt[1]) : 0u;
-    s_cnt[0] = 0;
-    s_cnt[1] = 0;
-  }
-  __syncthreads();
-  if (B >= 0) {
-    for (uint32_t j0 = b0; j0 < b1; j0 += kFinBlock) {
-      const uint32_t j = j0 + threadIdx.x;
-      int2 e = make_int2(0, 0);
-      int bin = -1;
-      if (j < b1) {
-        e = w.cand[j];
-        bin = (int)((abs_key(u2f((uint32_t)e.y)) - c.thr_lo) >> c.shift);
-      }
-      const bool sel = bin > B, bd = bin == B;
-      const uint64_t ms = __ballot(sel), mb = __ballot(bd);
-      uint32_t bs = 0, bb = 0;
-      if (lane_id() == 0) {
-        if (ms) bs = atomicAdd(&s_cnt[0], (uint32_t)__popcll(ms));
-        if (mb) bb = atomicAdd(&s_cnt[1], (uint32_t)__popcll(mb));
-      }
-      bs = __shfl(bs, 0, 64);
-      bb = __shfl(bb, 0, 64);
-      if (sel) {
-        const uint32_t gp = c.n_sure + s_cnt[2] + bs + lane_rank(ms);
-        const float v = u2f((uint32_t)e.y);
-        a.vals[gp] = v;
-        a.idx[gp] = e.x;
-        if constexpr (MODE != kDenseNone) a.r[e.x] = v - v;
-        if constexpr (MODE == kDenseFused) a.out[e.x] = 0.f + v;
-      }
-      if (bd) w.bnd[s_cnt[3] + bb + lane_rank(mb)] = e;
-    }
-  }
-  // residual-only mode: sure entries still hold t in r; zero them now
-  if constexpr (MODE == kDenseRes) {
-    for (uint32_t j = blockIdx.x * kFinBlock + threadIdx.x; j < c.n_sure; j += gridDim.x * kFinBlock) {
-      const float v = a.vals[j];
-      a.r[a.idx[j]] = v - v;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // selected element sinks shared by the boundary / fallback / small kernels
 template <int MODE>
@@ -610,17 +691,19 @@ __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, u
   }
 }
 
+// 3. finalize (+ boundary): every workgroup scans the candidate histogram (2 bins per thread) for
+// the boundary bin B and the payload base of every bin above it; each selected candidate takes its
+// slot from a per-bin cursor (atomics spread over the ~1000 live bins, one 128-B line each, not one
+// hot counter), the boundary bin's entries go to the boundary list.  The last workgroup to arrive
+// (release -> ticket -> acquire) then ranks the boundary list exactly by (key, -index) -- or, if
+// the sampled bracket failed or a list overflowed, runs the exact single-workgroup radix select
+// over the whole bucket (slow, rare, same result).
 template <int MODE>
-__global__ __launch_bounds__(kSelBlock) void topk_boundary(StepArgs a, TopkWs w) {
-  __shared__ uint32_t hist[2048];
-  __shared__ uint64_t s_comp[kSelBlock];
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_pos;
-  const TopkCtl c = *w.ctl;
+__device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint32_t need, uint32_t nb,
+                              uint32_t* hist, uint64_t* s_comp, uint32_t* s_w, uint32_t* s_res,
+                              uint32_t* s_pos) {
   const uint32_t k = (uint32_t)a.k;
-  if (c.status == 0) {
-    const uint32_t need = c.need, nb = c.n_bnd;
+  if (ok) {
     if (need == 0) return;
     const uint32_t pos0 = k - need;
     if (nb <= (uint32_t)kSelBlock) {
@@ -647,22 +730,129 @@ __global__ __launch_bounds__(kSelBlock) void topk_boundary(StepArgs a, TopkWs w)
       return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
     };
     const uint64_t T = block_select_comp(src, nb, need, hist, s_w, s_res);
-    if (threadIdx.x == 0) s_pos = 0;
+    if (threadIdx.x == 0) *s_pos = 0;
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += kSelBlock) {
       const int2 e = bnd[j];
       if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) {
-        const uint32_t p = atomicAdd(&s_pos, 1u);
+        const uint32_t p = atomicAdd(s_pos, 1u);
         emit<MODE>(a, pos0 + p, e.x, u2f((uint32_t)e.y));
       }
     }
     return;
   }
   // ---- exact fallback over the whole bucket (bracket failed or a list overflowed)
+  if (threadIdx.x == 0) w.ctl->status = 1;
   const MainT<MODE> f{a.g, a.r, a.out};
   auto src = [f](int64_t i) { return comp_key(abs_key(f(i)), (uint32_t)i); };
   const uint64_t T = block_select_comp(src, a.n, k, hist, s_w, s_res);
   block_write_selected<MODE>(a, f, a.n, T, 0u, s_w);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
+  constexpr int PER = kHistBins / kSelBlock;
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  __shared__ uint32_t s_base[kHistBins];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint64_t s_comp[kSelBlock];
+  __shared__ uint32_t s_res[2];
+  __shared__ int s_B;
+  __shared__ uint32_t s_need, s_pos, s_last;
+  STAMP(w.ctl, 8);
+  const TopkCtl c = *w.ctl;
+  const uint32_t k = (uint32_t)a.k;
+  const bool ok = c.n_sure <= k && (uint64_t)c.n_sure + c.n_cand >= k && c.n_cand <= (uint64_t)w.cap;
+  const int t = threadIdx.x;
+  int B = -1;
+  uint32_t need = 0, nb = 0;
+  if (ok) {
+    const uint32_t target = k - c.n_sure;
+    const int top = kHistBins - 1 - t * PER;
+    uint32_t h[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { h[j] = w.hist[(top - j) * kHistStride]; sum += h[j]; }
+    if (t == 0) { s_B = -1; s_need = 0; }
+    const uint32_t ex = block_excl_scan<kSelBlock>(sum, s_w, nullptr);
+    uint32_t acc = ex;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      s_base[top - j] = acc;                       // candidates in bins above this one
+      if (target > 0 && acc < target && target <= acc + h[j]) { s_B = top - j; s_need = target - acc; }
+      acc += h[j];
+    }
+    __syncthreads();
+    B = s_B;
+    need = s_need;
+    nb = B >= 0 ? w.hist[B * kHistStride] : 0u;
+    if (blockIdx.x == 0 && t == 0) {
+      w.ctl->boundary_bin = B;
+      w.ctl->need = need;
+      w.ctl->n_bnd = nb;
+    }
+    STAMP(w.ctl, 9);
+    // residual-only mode: sure entries still hold t in r; zero them now
+    if constexpr (MODE == kDenseRes) {
+      for (uint32_t j = blockIdx.x * kSelBlock + t; j < c.n_sure; j += gridDim.x * kSelBlock) {
+        const float v = a.vals[j];
+        a.r[a.idx[j]] = v - v;
+      }
+    }
+    if (B >= 0) {
+      // two candidates per thread per round, loads and cursor atomics issued back to back
+      const uint32_t stride = gridDim.x * kSelBlock;
+      for (uint32_t j0 = blockIdx.x * kSelBlock + t; j0 < c.n_cand; j0 += 2 * stride) {
+        int2 e[2];
+        bool have[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t j = j0 + u * stride;
+          have[u] = j < c.n_cand;
+          e[u] = have[u] ? w.cand[j] : make_int2(0, 0);
+        }
+        int bin[2];
+        uint32_t slot[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          bin[u] = have[u] ? (int)((abs_key(u2f((uint32_t)e[u].y)) - c.thr_lo) >> c.shift) : -1;
+          slot[u] = bin[u] >= B ? atomicAdd(&w.cursor[bin[u] * kCursorStride], 1u) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (bin[u] > B) {
+            const uint32_t gp = c.n_sure + s_base[bin[u]] + slot[u];
+            const float v = u2f((uint32_t)e[u].y);
+            a.vals[gp] = v;
+            a.idx[gp] = e[u].x;
+            if constexpr (MODE != kDenseNone) a.r[e[u].x] = v - v;
+            if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
+          } else if (bin[u] == B) {
+            w.bnd[slot[u]] = e[u];
+          }
+        }
+      }
+    }
+  }
+  // arrival: every wave's stores complete, one release + ticket per workgroup; the last one
+  // acquires and finishes the boundary bin
+  STAMP(w.ctl, 10);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  STAMP_IF(true, w.ctl, 11);
+  boundary_work<MODE>(a, w, ok, need, nb, hist, s_comp, s_w, s_res, &s_pos);
+  __syncthreads();
+  STAMP_IF(true, w.ctl, 12);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -713,8 +903,12 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   TopkWs w = carve(ws, a.n, a.k);
   const bool vec = ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r) |
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
-  topk_bracket<HAS_RES><<<1, kSelBlock, 0, s>>>(a, w);
-  GRACE_CHECK_LAUNCH("topk_bracket");
+  a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
+  a.stratum = a.n / a.sample_n;
+  topk_sample<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
+  GRACE_CHECK_LAUNCH("topk_sample");
+  topk_select<<<1, kSelBlock, 0, s>>>(a, w);
+  GRACE_CHECK_LAUNCH("topk_select");
   const unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
   {
     TimerScope ts(s);
@@ -724,10 +918,8 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
       topk_main<HAS_RES, MODE, false><<<nblk, kMainBlock, 0, s>>>(a, w);
   }
   GRACE_CHECK_LAUNCH("topk_main");
-  topk_finalize<MODE><<<kFinBlocks, kFinBlock, 0, s>>>(a, w);
+  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_finalize");
-  topk_boundary<MODE><<<1, kSelBlock, 0, s>>>(a, w);
-  GRACE_CHECK_LAUNCH("topk_boundary");
   return GRACE_OK;
 }
 

@@ -52,7 +52,8 @@ def workspace(slot, nbytes, device):
     key = (str(device), slot, torch.cuda.current_stream(device).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        # zeroed once: the codecs leave their counters / histograms zeroed after every use
+        buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf
 

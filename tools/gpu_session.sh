@@ -26,10 +26,19 @@ for step in "$@"; do
   case "$step" in
     smoke)  run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 1200 python3 -m pytest tests -m gpu -x -q ;;
+    pytopk) run pytest_topk 900 python3 -m pytest tests/test_gpu_topk.py -x -q ;;
     pytestall) run pytest_gpu_all 1200 python3 -m pytest tests -m gpu -q ;;
     bench)  run bench 600 python3 bench.py ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/gpurun_out/prof_$TAG" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
+    probe)  run hbm_probe 300 tools/hbm_probe ;;
+    ab)     run ab 600 python3 tools/ab_topk.py ${AB_LIBS} ;;
+    pmc)    for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT"; do
+              tag=$(echo $c | cut -d' ' -f1)
+              run "pmc_$tag" 600 rocprofv3 --pmc $c --output-format csv -d "$ROOT/gpurun_out/pmc_${TAG}_$tag" -o pmc \
+                  -- python3 "$ROOT/bench.py" --steps 3 --warmup 3 --no-cpu-baseline
+            done ;;
+    stamps) run stamps 300 env GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so python3 tools/exp_stamps.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
