@@ -14,6 +14,7 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64
 F32 = ctypes.c_float
+U64 = ctypes.c_uint64
 SZ = ctypes.c_size_t
 ST = ctypes.c_int
 
@@ -44,6 +45,29 @@ SIGNATURES = {
     "grace_sparse_decode": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_decode_i64": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),
+    "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
+    "grace_qsgd_decompress": (ST, [P, P, I64, I64, I32, P, P, I32, I64, I32, I32, I32, I32, F32, P, P]),
+    "grace_terngrad_unit": (I32, []),
+    "grace_terngrad_workspace_bytes": (SZ, [I64]),
+    "grace_terngrad_compress": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
+    "grace_terngrad_decompress": (ST, [P, P, I64, I64, I32, P, I32, I64, I32, F32, P, P]),
+    "grace_natural_compress": (ST, [P, I64, P, U64, P, P]),
+    "grace_cnat_compress": (ST, [P, I64, P, I32, U64, P, P]),
+    "grace_natural_decompress": (ST, [P, I64, I32, I64, I32, I32, F32, P, P]),
+    "grace_fp16_compress": (ST, [P, P, I64, P]),
+    "grace_fp16_decompress": (ST, [P, P, I64, P]),
+    "grace_randomk_indices": (ST, [U64, I64, I64, P, P]),
+    "grace_gather": (ST, [P, P, I64, P, P]),
+    "grace_threshold_workspace_bytes": (SZ, [I64]),
+    "grace_threshold_count": (ST, [P, I64, F32, P, P]),
+    "grace_threshold_recount": (ST, [P, I64, F32, P, P]),
+    "grace_threshold_write": (ST, [P, I64, P, P, P, P]),
+    "grace_powersgd_p": (ST, [P, I64, I64, P, I32, P, P]),
+    "grace_powersgd_workspace_bytes": (SZ, [I64, I64, I32]),
+    "grace_powersgd_qt": (ST, [P, I64, I64, P, I32, P, P, P]),
+    "grace_orthogonalize": (ST, [P, I64, I32, P]),
+    "grace_powersgd_outer": (ST, [P, P, I64, I64, I32, P, P, P, P]),
+    "grace_normal_fill": (ST, [P, I64, U64, P]),
 }
 
 

@@ -1,0 +1,234 @@
+// Random-k and threshold sparsifiers for CDNA4.
+//
+// Random-k (grace_dl/dist/compressor/randomk.py:6-41): k indices drawn WITH replacement from
+// [0, numel) from a generator seeded by sum(bytes(name)) + global_step (identical on every rank),
+// payload = values at those indices.  Device mode: a counter-based hash of (seed, j); torch_cpu
+// mode (exact parity) passes the reference generator's indices in.
+//
+// Threshold (grace_dl/dist/compressor/threshold.py:6-27): idx = where(|x| >= min(thr, max(x)))
+// in ascending index order (bit-exact with torch.where).  Three short launches: per-chunk
+// (signed max, count at thr) -> one workgroup derives the bound and the chunk offsets (and flags
+// a recount if max(x) < thr) -> ordered compaction per chunk with a block scan.
+#include <math.h>
+
+#include "common.h"
+
+namespace grace {
+
+constexpr int kSBlock = 256;
+constexpr int kThrChunk = 16384;
+
+__global__ __launch_bounds__(kSBlock) void randomk_idx_kernel(uint64_t seed, int64_t numel, int64_t k,
+                                                             int64_t* __restrict__ idx) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock) {
+    const uint64_t h = mix64(seed * 0x9E3779B97F4A7C15ull ^ mix64((uint64_t)j + 0x632BE59BD9B4E019ull));
+    // unbiased enough for numel < 2^31: 64-bit product high word
+    idx[j] = (int64_t)__umul64hi(h, (uint64_t)numel);
+  }
+}
+
+__global__ __launch_bounds__(kSBlock) void gather_kernel(const float* __restrict__ x, const int64_t* __restrict__ idx,
+                                                        int64_t k, float* __restrict__ vals) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock)
+    vals[j] = x[idx[j]];
+}
+
+// ------------------------------------------------------------------------------------------------
+// threshold
+struct ThrPart { float mx; uint32_t nan; uint32_t cnt; uint32_t pad; };
+
+template <int BLOCK>
+__device__ __forceinline__ uint32_t blk_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  constexpr int NW = BLOCK / kWave;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < NW; ++i) { const uint32_t t = s_w[i]; s_w[i] = acc; acc += t; }
+    s_w[NW] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = s_w[w] + inc - v;
+  if (total) *total = s_w[NW];
+  __syncthreads();
+  return r;
+}
+
+// pass 1: per chunk signed max (NaN flagged) and count(|x| >= bound)
+__global__ __launch_bounds__(kSBlock) void thr_stats_kernel(const float* __restrict__ x, int64_t n, float bound,
+                                                           ThrPart* __restrict__ part) {
+  const int64_t base = (int64_t)blockIdx.x * kThrChunk;
+  const int64_t end = min(base + (int64_t)kThrChunk, n);
+  float mx = -INFINITY;
+  uint32_t nan = 0, cnt = 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += kSBlock) {
+    const float v = x[i];
+    if (v != v) nan = 1; else mx = fmaxf(mx, v);
+    cnt += fabsf(v) >= bound;
+  }
+  __shared__ float sm[kSBlock / kWave];
+  __shared__ uint32_t sn[kSBlock / kWave], sc[kSBlock / kWave];
+  mx = wave_max(mx);
+  cnt = wave_sum(cnt);
+  nan = __ballot(nan != 0) != 0;
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = mx; sn[w] = nan; sc[w] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ThrPart p{-INFINITY, 0u, 0u, 0u};
+    for (int j = 0; j < kSBlock / kWave; ++j) { p.mx = fmaxf(p.mx, sm[j]); p.nan |= sn[j]; p.cnt += sc[j]; }
+    part[blockIdx.x] = p;
+  }
+}
+
+// pass 2 (one workgroup): global max -> bound = min(thr, max) with Python's min (NaN max -> thr);
+// exclusive offsets of the chunk counts; meta = {bound bits, total, recount flag}
+__global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ part, int64_t nchunks, float thr,
+                                                        uint32_t* __restrict__ offs, uint32_t* __restrict__ meta,
+                                                        int final_pass) {
+  __shared__ uint32_t s_w[1024 / kWave + 1];
+  __shared__ float s_mx;
+  __shared__ uint32_t s_nan;
+  if (threadIdx.x == 0) { s_mx = -INFINITY; s_nan = 0; }
+  __syncthreads();
+  float mx = -INFINITY;
+  uint32_t nan = 0;
+  for (int64_t j = threadIdx.x; j < nchunks; j += 1024) { mx = fmaxf(mx, part[j].mx); nan |= part[j].nan; }
+  mx = wave_max(mx);
+  nan = __ballot(nan != 0) != 0;
+  // reduce per-wave maxima through LDS
+  __shared__ float s_wm[1024 / kWave];
+  __shared__ uint32_t s_wn[1024 / kWave];
+  if ((threadIdx.x & 63) == 0) { s_wm[threadIdx.x >> 6] = mx; s_wn[threadIdx.x >> 6] = nan; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = -INFINITY;
+    uint32_t nn = 0;
+    for (int w = 0; w < 1024 / kWave; ++w) { m = fmaxf(m, s_wm[w]); nn |= s_wn[w]; }
+    s_mx = m;
+    s_nan = nn;
+  }
+  __syncthreads();
+  // torch.max propagates NaN; Python min(thr, NaN) returns thr (NaN < thr is False)
+  const float gmax = s_nan ? __int_as_float(0x7FC00000) : s_mx;
+  const bool use_max = !s_nan && gmax < thr;
+  const float bound = use_max ? gmax : thr;
+  // chunk offsets (valid when the counts were taken at `bound`)
+  uint32_t run = 0;
+  for (int64_t j0 = 0; j0 < nchunks; j0 += 1024) {
+    const int64_t j = j0 + threadIdx.x;
+    const uint32_t c = j < nchunks ? part[j].cnt : 0u;
+    uint32_t tot;
+    const uint32_t ex = blk_excl_scan<1024>(c, s_w, &tot);
+    if (j < nchunks) offs[j] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) {
+    meta[0] = __float_as_uint(bound);
+    meta[1] = run;
+    meta[2] = (!final_pass && use_max) ? 1u : 0u;   // counts were taken at thr: recount at max
+  }
+}
+
+// pass 3: ordered compaction of |x| >= bound
+__global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restrict__ x, int64_t n,
+                                                           const uint32_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ meta,
+                                                           float* __restrict__ vals, int32_t* __restrict__ idx) {
+  __shared__ uint32_t s_w[kSBlock / kWave + 1];
+  const float bound = __uint_as_float(meta[0]);
+  const int64_t base = (int64_t)blockIdx.x * kThrChunk;
+  const int64_t end = min(base + (int64_t)kThrChunk, n);
+  uint32_t run = offs[blockIdx.x];
+  for (int64_t j0 = base; j0 < end; j0 += kSBlock) {
+    const int64_t i = j0 + threadIdx.x;
+    float v = 0.f;
+    bool sel = false;
+    if (i < end) { v = x[i]; sel = fabsf(v) >= bound; }
+    uint32_t tot;
+    const uint32_t ex = blk_excl_scan<kSBlock>(sel ? 1u : 0u, s_w, &tot);
+    if (sel) { vals[run + ex] = v; idx[run + ex] = (int32_t)i; }
+    run += tot;
+  }
+}
+
+}  // namespace grace
+
+using namespace grace;
+
+extern "C" {
+
+grace_status_t grace_randomk_indices(uint64_t seed, int64_t numel, int64_t k, int64_t* idx, void* stream) {
+  GRACE_REQUIRE(idx && numel >= 1 && k >= 0, "grace_randomk_indices: bad arguments");
+  if (k == 0) return GRACE_OK;
+  randomk_idx_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(seed, numel, k, idx);
+  GRACE_CHECK_LAUNCH("grace_randomk_indices");
+  return GRACE_OK;
+}
+
+grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float* vals, void* stream) {
+  GRACE_REQUIRE(x && idx && vals && k >= 0, "grace_gather: bad arguments");
+  if (k == 0) return GRACE_OK;
+  gather_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(x, idx, k, vals);
+  GRACE_CHECK_LAUNCH("grace_gather");
+  return GRACE_OK;
+}
+
+size_t grace_threshold_workspace_bytes(int64_t n) {
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  return 64 + sizeof(ThrPart) * (size_t)nch + sizeof(uint32_t) * (size_t)nch + 256;
+}
+
+// Stage 1: statistics and offsets.  The caller reads meta (bound bits, count, recount flag) from
+// the workspace (first 16 bytes) to size the outputs, then calls grace_threshold_write.
+grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void* ws, void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_count: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(p);
+  ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
+  uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  hipStream_t s = as_stream(stream);
+  thr_stats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, thr, part);
+  GRACE_CHECK_LAUNCH("grace_threshold_count");
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 0);
+  GRACE_CHECK_LAUNCH("grace_threshold_count");
+  return GRACE_OK;
+}
+
+// Recount at max(x) (only when max(x) < thr, flagged by stage 1).
+grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, void* ws, void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_recount: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(p);
+  ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
+  uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  hipStream_t s = as_stream(stream);
+  thr_stats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, bound, part);
+  GRACE_CHECK_LAUNCH("grace_threshold_recount");
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, bound, offs, meta, 1);
+  GRACE_CHECK_LAUNCH("grace_threshold_recount");
+  return GRACE_OK;
+}
+
+grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, float* vals, int32_t* idx,
+                                     void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_write: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  const char* p = reinterpret_cast<const char*>(ws);
+  const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  thr_write_kernel<<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
+  GRACE_CHECK_LAUNCH("grace_threshold_write");
+  return GRACE_OK;
+}
+
+}  // extern "C"

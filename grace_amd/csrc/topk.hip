@@ -48,7 +48,8 @@ constexpr int kSmallN = 32768;                             // single-workgroup p
 constexpr int kSampleRunLen = 16;
 constexpr int kSampleRuns = 2048;
 constexpr int kSample = kSampleRuns * kSampleRunLen;       // 32768 keys, 32 per thread
-constexpr int kFinBlocks = 256;
+constexpr int kFinBlocks = 64;
+constexpr int kFinPer = 8;                                 // candidates per thread per round
 
 struct TopkCtl {
   uint32_t thr_lo;
@@ -62,7 +63,7 @@ struct TopkCtl {
   int32_t boundary_bin;
   uint32_t need;
   uint32_t ticket;     // finalize kernel arrival counter
-  uint32_t unused;
+  uint32_t n_bacc;     // boundary-list fill counter
   uint32_t pad[4];
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
@@ -799,36 +800,42 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
       }
     }
     if (B >= 0) {
-      // two candidates per thread per round, loads and cursor atomics issued back to back
-      const uint32_t stride = gridDim.x * kSelBlock;
-      for (uint32_t j0 = blockIdx.x * kSelBlock + t; j0 < c.n_cand; j0 += 2 * stride) {
-        int2 e[2];
-        bool have[2];
+      // contiguous slice per workgroup, kFinPer candidates per thread per round held in registers;
+      // one block scan places them, one global atomic per list per round reserves the space
+      const uint32_t per = (c.n_cand + gridDim.x - 1) / gridDim.x;
+      const uint32_t b0 = blockIdx.x * per, b1 = min(c.n_cand, b0 + per);
+      for (uint32_t r0 = b0; r0 < b1; r0 += kSelBlock * kFinPer) {
+        int2 e[kFinPer];
+        uint32_t fs = 0, fb = 0;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint32_t j = j0 + u * stride;
-          have[u] = j < c.n_cand;
-          e[u] = have[u] ? w.cand[j] : make_int2(0, 0);
+        for (int u = 0; u < kFinPer; ++u) {
+          const uint32_t j = r0 + u * kSelBlock + t;
+          e[u] = j < b1 ? w.cand[j] : make_int2(0, 0);
+          const int bin = j < b1 ? (int)((abs_key(u2f((uint32_t)e[u].y)) - c.thr_lo) >> c.shift) : -1;
+          fs |= (uint32_t)(bin > B) << u;
+          fb |= (uint32_t)(bin == B) << u;
         }
-        int bin[2];
-        uint32_t slot[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          bin[u] = have[u] ? (int)((abs_key(u2f((uint32_t)e[u].y)) - c.thr_lo) >> c.shift) : -1;
-          slot[u] = bin[u] >= B ? atomicAdd(&w.cursor[bin[u] * kCursorStride], 1u) : 0u;
+        const uint32_t packed = (uint32_t)__popc(fs) | ((uint32_t)__popc(fb) << 16);
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<kSelBlock>(packed, s_w, &tot);
+        if (t == 0) {
+          s_res[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
+          s_res[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
         }
+        __syncthreads();
+        uint32_t ps = c.n_sure + s_res[0] + (ex & 0xFFFFu), pb = s_res[1] + (ex >> 16);
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (bin[u] > B) {
-            const uint32_t gp = c.n_sure + s_base[bin[u]] + slot[u];
+        for (int u = 0; u < kFinPer; ++u) {
+          if ((fs >> u) & 1u) {
             const float v = u2f((uint32_t)e[u].y);
-            a.vals[gp] = v;
-            a.idx[gp] = e[u].x;
+            a.vals[ps] = v;
+            a.idx[ps] = e[u].x;
             if constexpr (MODE != kDenseNone) a.r[e[u].x] = v - v;
             if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
-          } else if (bin[u] == B) {
-            w.bnd[slot[u]] = e[u];
+            ++ps;
           }
+          if ((fb >> u) & 1u) w.bnd[pb++] = e[u];
         }
       }
     }

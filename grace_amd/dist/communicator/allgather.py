@@ -38,36 +38,38 @@ class Allgather(Communicator):
                     return out
             per_rank = [[g.view(W, -1)[r].view(t.shape) for g, t in zip(gathered, tensors)] for r in range(W)]
         else:
-            per_rank = self._gather_variable(tensors, W)
+            gathered, sizes = self._gather_variable(tensors, W)
             fast = getattr(self.compressor, "decode_aggregate_variable", None)
             if fast is not None:
-                out = fast(per_rank, ctx, W)
+                out = fast(gathered, sizes, ctx, W)
                 if out is not None:
                     return out
+            per_rank = [[g.view(W, -1)[r][:sizes[r][j]] for j, g in enumerate(gathered)] for r in range(W)]
         decompressed_list = [self.compressor.decompress(tc, ctx) for tc in per_rank]
         tensors_aggregated = self.compressor.aggregate(decompressed_list)
         return divide(tensors_aggregated, W) if self.compressor.average else tensors_aggregated
 
     @staticmethod
     def _gather_variable(tensors, W):
-        """Size exchange + padded all-gather + trim (allgather.py:15-38)."""
+        """Size exchange + padded all-gather (allgather.py:15-38).  Returns the rank-major padded
+        buffers (one per payload tensor, W * max_size) and sizes[rank][tensor]."""
         if W == 1:
-            return [list(tensors)]
+            return [t.contiguous().view(-1) for t in tensors], [[t.numel() for t in tensors]]
         dev = tensors[0].device
         local_sizes = torch.tensor([t.numel() for t in tensors], dtype=torch.int64, device=dev)
         all_sizes = torch.empty(W * len(tensors), dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(all_sizes, local_sizes)
         sizes = all_sizes.view(W, len(tensors)).cpu().tolist()
-        per_rank = [[] for _ in range(W)]
+        gathered = []
         for j, t in enumerate(tensors):
             max_size = max(sizes[r][j] for r in range(W))
             flat = t.contiguous().view(-1)
             if flat.numel() != max_size:
-                padded = torch.zeros(max_size, dtype=flat.dtype, device=flat.device)
+                padded = torch.zeros(max(max_size, 1), dtype=flat.dtype, device=flat.device)[:max_size]
                 padded[:flat.numel()] = flat
                 flat = padded
             out = torch.empty(W * max_size, dtype=flat.dtype, device=flat.device)
-            dist.all_gather_into_tensor(out, flat)
-            for r in range(W):
-                per_rank[r].append(out[r * max_size: r * max_size + sizes[r][j]])
-        return per_rank
+            if max_size:
+                dist.all_gather_into_tensor(out, flat)
+            gathered.append(out)
+        return gathered, sizes

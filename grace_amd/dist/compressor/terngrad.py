@@ -1,0 +1,40 @@
+"""TernGrad (grace_dl/dist/compressor/terngrad.py:5-30) on the HIP quantiser.
+
+Payload (codes int8[n] in {-1,0,1}, scalar f32[1]).  The std / max reductions run in f64 on the
+device (the reference's f32 CPU reduction order is not reproducible on a GPU; the scalar agrees
+within a few ulp and codewords are bit-exact given the same clamp bound and uniforms, see
+tests/test_gpu_quant.py).  ``rng`` as for QSGD.
+"""
+import torch
+
+from grace_amd import ops
+from grace_amd.dist import Compressor
+
+
+class TernGradCompressor(Compressor):
+
+    def __init__(self, rng="device"):
+        super().__init__()
+        self.rng = rng
+        self._step = 0
+
+    def compress(self, tensor, name):
+        flat = ops.dev_f32(tensor)
+        self._step += 1
+        if self.rng == "torch_cpu":
+            u, seed = torch.empty(flat.numel()).uniform_(0, 1).to(flat.device), 0
+        else:
+            u, seed = None, ops.step_seed("terngrad", ops.rank_of_process(), name, self._step)
+        codes, scalar = ops.terngrad_compress(flat, u=u, seed=seed)
+        return (codes, scalar), tensor.size()
+
+    def decompress(self, tensor_compressed, ctx):
+        codes, scalar = tensor_compressed
+        return ops.terngrad_decompress(codes, scalar, ctx.numel()).view(ctx)
+
+    def decode_aggregate_gathered(self, gathered, shape, world_size):
+        codes, scalars = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.terngrad_decompress(codes, scalars, shape.numel(), world=world_size, aggregate=True,
+                                       divisor=world_size if self.average else 1.0).view(shape)

@@ -255,3 +255,209 @@ def isclose_f32_ulps(a, b, ulps):
     b = torch.as_tensor(b, dtype=torch.float32)
     spacing = torch.abs(torch.nextafter(b, torch.full_like(b, math.inf)) - b)
     return bool(torch.all(torch.abs(a - b) <= ulps * spacing))
+
+
+# ----------------------------------------------------------------------------- segmented tables
+_seg_cache = {}
+
+
+def seg_tables(sizes, unit, device):
+    """Device offset tables for a segmented bucket: (seg_off[nseg+1], sub_off[nseg+1], nsub) where
+    sub_off counts ceil(n_s / unit) sub-blocks (QSGD buckets, TernGrad work units) per segment.
+    Cached: built (one small H2D copy) once per shape."""
+    key = (tuple(int(s) for s in sizes), int(unit), str(device))
+    hit = _seg_cache.get(key)
+    if hit is None:
+        seg = [0]
+        sub = [0]
+        for s in key[0]:
+            seg.append(seg[-1] + s)
+            sub.append(sub[-1] + (s + unit - 1) // unit)
+        hit = (torch.tensor(seg, dtype=torch.int64).to(device), torch.tensor(sub, dtype=torch.int64).to(device),
+               sub[-1])
+        _seg_cache[key] = hit
+    return hit
+
+
+def _opt(t):
+    return t.data_ptr() if t is not None else None
+
+
+# ----------------------------------------------------------------------------- QSGD
+def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, seed=0, norms_in=None):
+    """x: flat f32 device buffer (one tensor, or `sizes` segments back to back)."""
+    x = dev_f32(x)
+    sizes = [x.numel()] if sizes is None else sizes
+    seg_off, bkt_off, nb = seg_tables(sizes, bucket_size, x.device)
+    codes = torch.empty(x.numel(), dtype=torch.int8 if quantum_num < 128 else torch.float16, device=x.device)
+    norms = torch.empty(nb, dtype=F32, device=x.device)
+    _lib.call("grace_qsgd_compress", _p(x), _p(seg_off), _p(bkt_off), len(sizes), nb, int(quantum_num),
+              int(bucket_size), int(variant), _opt(u), int(seed) & (2 ** 64 - 1), _opt(norms_in), _p(norms),
+              _p(codes), _stream())
+    return codes, norms
+
+
+def qsgd_decompress(codes, norms, quantum_num, bucket_size, n, sizes=None, variant=0, world=1,
+                    aggregate=False, divisor=1.0):
+    codes, norms = require_dev(codes), require_dev(norms)
+    sizes = [n] if sizes is None else sizes
+    seg_off, bkt_off, nb = seg_tables(sizes, bucket_size, codes.device)
+    out = torch.empty(n, dtype=F32, device=codes.device)
+    _lib.call("grace_qsgd_decompress", _p(codes), _p(norms), n, nb, int(world), _p(seg_off), _p(bkt_off),
+              len(sizes), n, int(quantum_num), int(bucket_size), int(variant), 1 if aggregate else 0,
+              float(divisor), _p(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- TernGrad
+def terngrad_compress(x, sizes=None, clip=None, u=None, seed=0):
+    x = dev_f32(x)
+    sizes = [x.numel()] if sizes is None else sizes
+    unit = _lib.query("grace_terngrad_unit")
+    seg_off, unit_off, nunits = seg_tables(sizes, unit, x.device)
+    codes = torch.empty(x.numel(), dtype=torch.int8, device=x.device)
+    scalars = torch.empty(len(sizes), dtype=F32, device=x.device)
+    ws = workspace("terngrad", _lib.query("grace_terngrad_workspace_bytes", nunits), x.device)
+    _lib.call("grace_terngrad_compress", _p(x), _p(seg_off), _p(unit_off), len(sizes), nunits, _opt(clip),
+              _opt(u), int(seed) & (2 ** 64 - 1), _p(codes), _p(scalars), _p(ws), _stream())
+    return codes, scalars
+
+
+def terngrad_decompress(codes, scalars, n, sizes=None, world=1, aggregate=False, divisor=1.0):
+    codes, scalars = require_dev(codes), require_dev(scalars)
+    sizes = [n] if sizes is None else sizes
+    unit = _lib.query("grace_terngrad_unit")
+    seg_off, _, _ = seg_tables(sizes, unit, codes.device)
+    out = torch.empty(n, dtype=F32, device=codes.device)
+    _lib.call("grace_terngrad_decompress", _p(codes), _p(scalars), n, len(sizes), int(world), _p(seg_off),
+              len(sizes), n, 1 if aggregate else 0, float(divisor), _p(out), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- natural / fp16
+def natural_compress(x, rand_int=None, seed=0):
+    x = dev_f32(x)
+    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    _lib.call("grace_natural_compress", _p(x), x.numel(), _opt(rand_int), int(seed) & (2 ** 64 - 1),
+              _p(codes), _stream())
+    return codes
+
+
+def cnat_compress(x, rand=None, deterministic=False, seed=0):
+    x = dev_f32(x)
+    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    _lib.call("grace_cnat_compress", _p(x), x.numel(), _opt(rand), 1 if deterministic else 0,
+              int(seed) & (2 ** 64 - 1), _p(codes), _stream())
+    return codes
+
+
+def natural_decompress(codes, n, flavour, world=1, aggregate=False, divisor=1.0):
+    codes = require_dev(codes)
+    out = torch.empty(n, dtype=F32, device=codes.device)
+    _lib.call("grace_natural_decompress", _p(codes), n, int(world), n, int(flavour), 1 if aggregate else 0,
+              float(divisor), _p(out), _stream())
+    return out
+
+
+def fp16_compress(x):
+    x = dev_f32(x)
+    h = torch.empty(x.numel(), dtype=torch.float16, device=x.device)
+    _lib.call("grace_fp16_compress", _p(x), _p(h), x.numel(), _stream())
+    return h
+
+
+def fp16_decompress(h):
+    h = require_dev(h)
+    out = torch.empty(h.numel(), dtype=F32, device=h.device)
+    _lib.call("grace_fp16_decompress", _p(h), _p(out), h.numel(), _stream())
+    return out
+
+
+# ----------------------------------------------------------------------------- seeds
+def step_seed(*parts):
+    """Deterministic 64-bit seed for the device generator from (rank, name, step, ...)."""
+    import hashlib
+    h = hashlib.blake2b(repr(parts).encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little")
+
+
+def rank_of_process():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+# ----------------------------------------------------------------------------- random-k / threshold
+def randomk_indices(seed, numel, k, device):
+    idx = torch.empty(k, dtype=torch.int64, device=device)
+    _lib.call("grace_randomk_indices", int(seed) & (2 ** 64 - 1), int(numel), int(k), _p(idx), _stream())
+    return idx
+
+
+def gather(x, idx):
+    x = dev_f32(x)
+    idx = require_dev(idx)
+    vals = torch.empty(idx.numel(), dtype=F32, device=x.device)
+    _lib.call("grace_gather", _p(x), _p(idx), idx.numel(), _p(vals), _stream())
+    return vals
+
+
+def threshold_compress(x, thr):
+    """(vals f32[m], idx int32[m]) with m data-dependent: one host sync to size the outputs."""
+    import numpy as np
+    x = dev_f32(x)
+    n = x.numel()
+    ws = workspace("threshold", _lib.query("grace_threshold_workspace_bytes", n), x.device)
+    thr32 = float(np.float32(thr))
+    _lib.call("grace_threshold_count", _p(x), n, thr32, _p(ws), _stream())
+    meta = ws[:12].view(torch.int32).cpu()
+    if int(meta[2]) != 0:
+        bound = float(meta[0:1].view(torch.float32)[0])
+        _lib.call("grace_threshold_recount", _p(x), n, bound, _p(ws), _stream())
+        meta = ws[:12].view(torch.int32).cpu()
+    m = int(meta[1])
+    vals = torch.empty(m, dtype=F32, device=x.device)
+    idx = torch.empty(m, dtype=torch.int32, device=x.device)
+    if m:
+        _lib.call("grace_threshold_write", _p(x), n, _p(ws), _p(vals), _p(idx), _stream())
+    return vals, idx
+
+
+# ----------------------------------------------------------------------------- PowerSGD
+def powersgd_p(M2d, q):
+    n, m = M2d.shape
+    r = q.shape[1]
+    P = torch.empty(n, r, dtype=F32, device=M2d.device)
+    _lib.call("grace_powersgd_p", _p(M2d), n, m, _p(require_dev(q)), r, _p(P), _stream())
+    return P
+
+
+def powersgd_qt(M2d, P):
+    n, m = M2d.shape
+    r = P.shape[1]
+    Q = torch.empty(m, r, dtype=F32, device=M2d.device)
+    ws = workspace("powersgd", _lib.query("grace_powersgd_workspace_bytes", n, m, r), M2d.device)
+    _lib.call("grace_powersgd_qt", _p(M2d), n, m, _p(require_dev(P)), r, _p(Q), _p(ws), _stream())
+    return Q
+
+
+def orthogonalize_(A):
+    A = require_dev(A)
+    _lib.call("grace_orthogonalize", _p(A), A.shape[0], A.shape[1], _stream())
+    return A
+
+
+def powersgd_outer(P, Q, M2d=None, want_out=True, want_residual=False):
+    n, r = P.shape
+    m = Q.shape[0]
+    dev = P.device
+    out = torch.empty(n, m, dtype=F32, device=dev) if want_out else None
+    res = torch.empty(n, m, dtype=F32, device=dev) if want_residual else None
+    _lib.call("grace_powersgd_outer", _p(P), _p(Q), n, m, r, _p(out) if out is not None else None,
+              _p(M2d) if M2d is not None else None, _p(res) if res is not None else None, _stream())
+    return out, res
+
+
+def normal(shape, seed, device):
+    x = torch.empty(shape, dtype=F32, device=device)
+    _lib.call("grace_normal_fill", _p(x), x.numel(), int(seed) & (2 ** 64 - 1), _stream())
+    return x

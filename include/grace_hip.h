@@ -122,6 +122,86 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
                                       const int64_t* counts_host, int32_t world, float divisor,
                                       float* out, int32_t* tags, int64_t n, void* stream);
 
+/* ------------------------------------------------------------------------------ quantisers */
+/* Segmented buckets: x is one flat f32 buffer holding nseg tensors; seg_off[nseg + 1] (device)
+ * gives their element offsets.  A single tensor is nseg = 1, seg_off = {0, n}.
+ * Randomness: u (uniform [0,1) per element, the reference's torch stream) may be injected; when
+ * NULL a counter-based device generator keyed by `seed` is used. */
+
+/* QSGD (grace_dl/dist/compressor/qsgd.py:12-39; variant 1 = QSGDCompressor_CUDA semantics of
+ * qsgd_cuda.cu:320-388).  bkt_off[nseg + 1] (device) = per-segment bucket offsets, bucket =
+ * ceil(n_s / bucket_size) per segment; norms_out[nbuckets] f32; codes int8 (q < 128) or fp16.
+ * norms_in (optional) injects the bucket norms (parity of codewords). */
+grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const int64_t* bkt_off,
+                                   int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
+                                   int32_t variant, const float* u, uint64_t seed, const float* norms_in,
+                                   float* norms_out, void* codes, void* stream);
+/* (norm / q) * code (qsgd.py:44-49).  world > 1 with rank-major payload strides: decode +
+ * aggregate in rank order, aggregate != 0 adds the Python-sum 0 (allgather.py:40-45); divisor
+ * applies the average. */
+grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int64_t code_stride,
+                                     int64_t norm_stride, int32_t world, const int64_t* seg_off,
+                                     const int64_t* bkt_off, int32_t nseg, int64_t n, int32_t quantum_num,
+                                     int32_t bucket_size, int32_t variant, int32_t aggregate, float divisor,
+                                     float* out, void* stream);
+/* TernGrad (terngrad.py:7-30).  unit_off[nseg + 1] (device) = per-segment offsets of
+ * grace_terngrad_unit()-element work units; ws = grace_terngrad_workspace_bytes(nunits).
+ * clip_in[nseg] (optional) injects the clamp bound c = f32(2.5 * std). */
+int32_t grace_terngrad_unit(void);
+size_t grace_terngrad_workspace_bytes(int64_t nunits);
+grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, const int64_t* unit_off,
+                                       int32_t nseg, int64_t nunits, const float* clip_in, const float* u,
+                                       uint64_t seed, int8_t* codes, float* scalars, void* ws,
+                                       void* stream);
+grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scalars, int64_t code_stride,
+                                         int64_t scal_stride, int32_t world, const int64_t* seg_off,
+                                         int32_t nseg, int64_t n, int32_t aggregate, float divisor, float* out,
+                                         void* stream);
+/* natural compression: cupy flavour (natural.py:12-29; rand_int = randint(0, 2^23-1) stream) and
+ * cnat_cuda flavour (cnat_cuda.cu:68-123; rand = uniform stream, or deterministic threshold 0.5). */
+grace_status_t grace_natural_compress(const float* x, int64_t n, const int32_t* rand_int, uint64_t seed,
+                                      uint8_t* codes, void* stream);
+grace_status_t grace_cnat_compress(const float* x, int64_t n, const float* rand, int32_t deterministic,
+                                   uint64_t seed, uint8_t* codes, void* stream);
+/* flavour 0 = natural.py:35-39 decode, 1 = cnat_cuda.cu:125-134 decode */
+grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, int32_t world, int64_t n,
+                                        int32_t flavour, int32_t aggregate, float divisor, float* out,
+                                        void* stream);
+/* fp16 (fp16.py): round-to-nearest-even cast and back */
+grace_status_t grace_fp16_compress(const float* x, void* half_out, int64_t n, void* stream);
+grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------------- random-k / threshold */
+/* Random-k indices (randomk.py:11: randint(numel, [k]), WITH replacement) from a counter-based
+ * device generator keyed by the reference's seed sum(bytes(name)) + step: identical on every
+ * rank.  (Bit-parity with torch's CPU generator: draw on the host and pass the indices.) */
+grace_status_t grace_randomk_indices(uint64_t seed, int64_t numel, int64_t k, int64_t* idx, void* stream);
+/* vals[j] = x[idx[j]]  (randomk.py:12 tensor[indices]) */
+grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float* vals, void* stream);
+/* Threshold (threshold.py:16-19): idx = where(|x| >= min(thr, max(x))) in ascending order.
+ * count -> (host reads meta = ws[0..2]: bound bits, count, recount flag) -> [recount] -> write.
+ * The caller synchronises once to size the variable-length payload. */
+size_t grace_threshold_workspace_bytes(int64_t n);
+grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void* ws, void* stream);
+grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, void* ws, void* stream);
+grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, float* vals, int32_t* idx,
+                                     void* stream);
+
+/* ---------------------------------------------------------------------------------- PowerSGD */
+/* PowerSGD (powersgd.py:30-65) on M[n x m] row-major, rank r <= 16, f32 MFMA contractions.
+ * P = M q;  Q = M^T P (ws = grace_powersgd_workspace_bytes);  orthogonalize in place;
+ * out = P Q^T and/or residual = M - P Q^T (memory/powersgd.py:32-37) in one pass. */
+grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
+                                void* stream);
+size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r);
+grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const float* P, int32_t r, float* Q,
+                                 void* ws, void* stream);
+grace_status_t grace_orthogonalize(float* A, int64_t n, int32_t r, void* stream);
+grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, int64_t m, int32_t r, float* out,
+                                    const float* M, float* residual, void* stream);
+/* standard normal fill (q draws, powersgd.py:41 / memory/powersgd.py:27), device generator */
+grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

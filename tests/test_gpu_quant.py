@@ -1,0 +1,172 @@
+"""GPU parity of the quantisation codecs (grace_amd/csrc/quant.hip) against the reference's golden
+vectors.  Codewords are bit-exact given the reference's injected randomness and scale (norms / clamp
+bound); scales computed on the device agree with the reference's CPU f32 reductions within 4 ulp."""
+import numpy as np
+import pytest
+import torch
+
+from grace_amd import ops
+from oracle import grace_oracle as O
+from tests.golden_util import same_bits
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def test_qsgd_golden(golden):
+    cases = golden.cases("quant", codec="qsgd")
+    assert cases
+    for c in cases:
+        q, b = c.meta["quantum_num"], c.meta["bucket_size"]
+        x = _t(c["x"].ravel())
+        u = _t(c["u"])
+        norms_ref = _t(c["norms"])
+        # codewords with the reference's uniforms and norms: bit-exact
+        codes, _ = ops.qsgd_compress(x, q, b, u=u, norms_in=norms_ref)
+        assert same_bits(_np(codes), c["codes"].ravel()), c.name
+        # norms computed on the device: within 4 ulp of torch's CPU f32 reduction
+        codes2, norms = ops.qsgd_compress(x, q, b, u=u)
+        assert ops.isclose_f32_ulps(_np(norms), c["norms"], 4), c.name
+        agree = np.mean(_np(codes2).view(np.uint8 if q < 128 else np.uint16) ==
+                        c["codes"].ravel().view(np.uint8 if q < 128 else np.uint16))
+        assert agree > 0.999, (c.name, agree)
+        # decompress with the reference payload: bit-exact
+        dec = ops.qsgd_decompress(_t(c["codes"].ravel()), norms_ref, q, b, x.numel())
+        assert same_bits(_np(dec), c["dec"].ravel()), c.name
+
+
+def test_qsgd_compressor_torch_rng_matches_reference(golden):
+    """rng='torch_cpu' consumes torch's global CPU generator exactly like the reference."""
+    from grace_amd.dist.compressor.qsgd import QSGDCompressor
+    for c in golden.cases("quant", codec="qsgd")[:6]:
+        q, b = c.meta["quantum_num"], c.meta["bucket_size"]
+        comp = QSGDCompressor(q, b, rng="torch_cpu")
+        torch.manual_seed(c.meta["seed"])
+        (codes, norms), shape = comp.compress(_t(c["x"]), "w")
+        # norms may differ by ulps, so compare through the oracle given our norms
+        exp, _ = O.qsgd_compress(c["x"], c["u"], q, b, norms=_np(norms))
+        assert same_bits(_np(codes), exp), c.name
+
+
+def test_terngrad_golden(golden):
+    for c in golden.cases("quant", codec="terngrad"):
+        x = c["x"].ravel()
+        clip = np.array([O.terngrad_clip(x)], dtype=np.float32)
+        codes, scal = ops.terngrad_compress(_t(x), clip=_t(clip), u=_t(c["u"]))
+        assert np.array_equal(_np(codes), c["codes"].ravel()), c.name
+        assert same_bits(_np(scal), c["scalar"].ravel()), c.name
+        codes2, scal2 = ops.terngrad_compress(_t(x), u=_t(c["u"]))
+        assert ops.isclose_f32_ulps(_np(scal2), c["scalar"].ravel(), 4), (c.name, _np(scal2), c["scalar"])
+        dec = ops.terngrad_decompress(_t(c["codes"].ravel()), _t(c["scalar"].ravel()), x.size)
+        assert same_bits(_np(dec), c["dec"].ravel()), c.name
+
+
+def test_segmented_qsgd_and_terngrad_match_per_tensor():
+    """One launch over many tensors == per-tensor launches (ResNet-style mixed shapes)."""
+    rng = np.random.default_rng(0)
+    sizes = [9408, 64, 64, 4096, 36864, 1, 129, 2048 * 10, 1000]
+    xs = [(rng.standard_normal(n) * 0.01).astype(np.float32) for n in sizes]
+    flat = _t(np.concatenate(xs))
+    u = rng.random(flat.numel(), dtype=np.float32)
+    codes, norms = ops.qsgd_compress(flat, 127, 128, sizes=sizes, u=_t(u))
+    tcodes, tscal = ops.terngrad_compress(flat, sizes=sizes, u=_t(u))
+    off = 0
+    noff = 0
+    for i, (n, x) in enumerate(zip(sizes, xs)):
+        c1, n1 = ops.qsgd_compress(_t(x), 127, 128, u=_t(u[off:off + n]))
+        nb = -(-n // 128)
+        assert same_bits(_np(codes[off:off + n]), _np(c1))
+        assert same_bits(_np(norms[noff:noff + nb]), _np(n1))
+        t1, s1 = ops.terngrad_compress(_t(x), u=_t(u[off:off + n]))
+        assert same_bits(_np(tcodes[off:off + n]), _np(t1))
+        assert same_bits(_np(tscal[i:i + 1]), _np(s1))
+        off += n
+        noff += nb
+    dec = ops.qsgd_decompress(codes, norms, 127, 128, flat.numel(), sizes=sizes)
+    exp = np.concatenate([O.qsgd_decode(*O.qsgd_compress(x, u[o:o + n], 127, 128, norms=None), 127, 128, n)
+                          for x, n, o in zip(xs, sizes, np.cumsum([0] + sizes[:-1]))])
+    assert np.allclose(_np(dec), exp, rtol=1e-5, atol=1e-7)
+
+
+def test_world2_qsgd_terngrad_aggregate(golden):
+    r0, r1 = golden.case("world2", "rank0"), golden.case("world2", "rank1")
+    codes = _t(np.concatenate([r0["qsgd_codes"], r1["qsgd_codes"]]))
+    norms = _t(np.concatenate([r0["qsgd_norms"], r1["qsgd_norms"]]))
+    out = ops.qsgd_decompress(codes, norms, 127, 128, 4099, world=2, aggregate=True, divisor=2.0)
+    assert same_bits(_np(out), r0["qsgd_out"].ravel())
+    codes = _t(np.concatenate([r0["tern_codes"], r1["tern_codes"]]))
+    scal = _t(np.concatenate([r0["tern_scalar"], r1["tern_scalar"]]))
+    out = ops.terngrad_decompress(codes, scal, 4099, world=2, aggregate=True, divisor=2.0)
+    assert same_bits(_np(out), r0["tern_out"].ravel())
+
+
+def test_qsgd_device_rng_properties():
+    x = np.random.default_rng(1).standard_normal(1 << 20).astype(np.float32) * 0.01
+    codes, norms = ops.qsgd_compress(_t(x), 127, 128, seed=1234)
+    norms_np = _np(norms)
+    level = (np.float32(1) / np.repeat(norms_np, 128)[: x.size] * np.float32(127)) * np.abs(x)
+    c = np.abs(_np(codes).astype(np.int32))
+    assert np.all((c == np.floor(level)) | (c == np.floor(level) + 1))
+    # unbiased: mean of the decode matches x in aggregate
+    dec = _np(ops.qsgd_decompress(codes, norms, 127, 128, x.size))
+    assert abs(float(np.mean(dec - x))) < 1e-5
+    # deterministic for a given seed
+    codes2, _ = ops.qsgd_compress(_t(x), 127, 128, seed=1234)
+    assert torch.equal(codes, codes2)
+
+
+def test_natural_vs_oracle():
+    rng = np.random.default_rng(2)
+    x = np.concatenate([rng.standard_normal(100000).astype(np.float32) * 3,
+                        np.array([0, -0.0, np.inf, -np.inf, np.nan, 1e-45, 2 ** -110, 2.0 ** 20], dtype=np.float32)])
+    ri = rng.integers(0, 0x7FFFFF, x.size, dtype=np.int32)
+    codes = ops.natural_compress(_t(x), rand_int=_t(ri))
+    exp = O.natural_compress(x, ri)
+    assert np.array_equal(_np(codes), exp)
+    assert same_bits(_np(ops.natural_decompress(codes, x.size, 0)), O.natural_decode(exp))
+
+
+def test_cnat_vs_oracle():
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.standard_normal(100000).astype(np.float32),
+                        np.array([1.0, 0.75, -1.0, 0.0, 2.0 ** -109, 2.0 ** -110, 2.0 ** 20, -(2.0 ** -120)],
+                                 dtype=np.float32)])
+    codes = ops.cnat_compress(_t(x), deterministic=True)
+    exp = O.cnat_compress(x)
+    assert np.array_equal(_np(codes), exp)
+    r = rng.random(x.size, dtype=np.float32)
+    codes = ops.cnat_compress(_t(x), rand=_t(r))
+    exp = O.cnat_compress(x, r)
+    assert np.array_equal(_np(codes), exp)
+    assert same_bits(_np(ops.natural_decompress(codes, x.size, 1)), O.cnat_decode(exp))
+
+
+def test_fp16_golden(golden):
+    from grace_amd.dist.compressor.fp16 import FP16Compressor
+    comp = FP16Compressor()
+    for c in golden.cases("quant", codec="fp16"):
+        (h,), ctx = comp.compress(_t(c["x"]), "w")
+        assert same_bits(_np(h), c["half"]), c.name
+        assert same_bits(_np(comp.decompress([h], ctx)), c["dec"]), c.name
+
+
+@pytest.mark.parametrize("cls", ["qsgd", "terngrad", "natural", "natural_cuda"])
+def test_allgather_world1_step(cls):
+    """Communicator.step through each quantiser at world 1 = (0 + decompress(compress(x))) / 1."""
+    from grace_amd.dist.helper import grace_from_params
+    comm = grace_from_params({"compressor": cls, "memory": "none", "communicator": "allgather", "world_size": 1})
+    x = _t(np.random.default_rng(4).standard_normal(5000).astype(np.float32) * 0.01)
+    torch.manual_seed(0)
+    out = comm.step(x, "w")
+    assert out.shape == x.shape and torch.isfinite(out).all()
+    # stochastic codecs are unbiased: the mean error is small against the spread of x
+    bias = abs(float((out - x).mean()))
+    assert bias < 0.1 * float(x.std())

@@ -1,0 +1,101 @@
+"""GPU parity of random-k and threshold (grace_amd/csrc/sparse.hip) against golden vectors."""
+import numpy as np
+import pytest
+import torch
+
+from grace_amd import ops
+from oracle import grace_oracle as O
+from tests.golden_util import same_bits
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def test_randomk_golden_torch_rng(golden):
+    from grace_amd.dist.compressor.randomk import RandomKCompressor
+    for c in golden.cases("sparse", codec="randomk"):
+        if "steps" in c.meta:
+            continue
+        comp = RandomKCompressor(c.meta["ratio"], rng="torch_cpu")
+        comp.global_step = c.meta["seed"] - sum(bytes(c.meta["name"], encoding="utf8"))
+        (vals,), ctx = comp.compress(_t(c["x"]), c.meta["name"])
+        assert np.array_equal(_np(ctx[0]), c["idx"]), c.name
+        assert same_bits(_np(vals), c["vals"]), c.name
+        assert same_bits(_np(comp.decompress([vals], ctx)), c["dec"]), c.name
+
+
+def test_randomk_device_rng_properties():
+    from grace_amd.dist.compressor.randomk import RandomKCompressor
+    x = np.random.default_rng(0).standard_normal(100003).astype(np.float32)
+    a, b = RandomKCompressor(0.01), RandomKCompressor(0.01)
+    (va,), ca = a.compress(_t(x), "layer.w")
+    (vb,), cb = b.compress(_t(x), "layer.w")
+    idx = _np(ca[0])
+    assert idx.size == 1000 and idx.min() >= 0 and idx.max() < x.size
+    assert np.array_equal(idx, _np(cb[0]))                      # same seed on every rank
+    assert same_bits(_np(va), x[idx])
+    (vc,), cc = a.compress(_t(x), "layer.w")                     # next step: new indices
+    assert not np.array_equal(idx, _np(cc[0]))
+    dec = _np(a.decompress([va], ca))
+    assert same_bits(dec, O.randomk_decode(x[idx], idx, x.size))
+
+
+def test_randomk_allreduce_residual_sequence(golden):
+    from grace_amd.dist.communicator.allreduce import Allreduce
+    from grace_amd.dist.compressor.randomk import RandomKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    c = golden.case("sparse", "randomk_residual_allreduce")
+    comm = Allreduce(RandomKCompressor(0.1, rng="torch_cpu"), ResidualMemory(), 1)
+    for s in range(2):
+        out = comm.step(_t(c[f"g{s}"]), "w")
+        assert same_bits(_np(out), c[f"out{s}"].ravel()), s
+        assert same_bits(_np(comm.memory.residuals["w"]).ravel(), c[f"res{s}"].ravel()), s
+
+
+def test_threshold_golden(golden):
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    for c in golden.cases("sparse", codec="threshold"):
+        comp = ThresholdCompressor(c.meta["threshold"])
+        (vals, idx), ctx = comp.compress(_t(c["x"]), "w")
+        assert np.array_equal(_np(idx), c["idx"]), c.name
+        assert same_bits(_np(vals), c["vals"]), c.name
+        assert same_bits(_np(comp.decompress([vals, idx], ctx)), c["dec"]), c.name
+
+
+@pytest.mark.parametrize("n", [1, 5000, 16384, 16385, 1 << 20])
+@pytest.mark.parametrize("thr", [0.01, 1.0, 3.0, 1e9])
+def test_threshold_vs_oracle(n, thr):
+    x = np.random.default_rng(n).standard_normal(n).astype(np.float32)
+    vals, idx = ops.threshold_compress(_t(x), thr)
+    ov, oi = O.threshold_select(x, thr)
+    assert np.array_equal(_np(idx), oi)
+    assert same_bits(_np(vals), ov)
+
+
+def test_threshold_nan_max_uses_threshold():
+    x = np.array([0.5, np.nan, -2.0, 0.01, 3.0], dtype=np.float32)
+    vals, idx = ops.threshold_compress(_t(x), 1.0)
+    ov, oi = O.threshold_select(x, 1.0)
+    assert np.array_equal(_np(idx), oi)
+
+
+def test_threshold_allgather_world1_variable_path():
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    x = np.random.default_rng(9).standard_normal(20000).astype(np.float32)
+    comm = Allgather(ThresholdCompressor(1.5), ResidualMemory(), 1)
+    out = _np(comm.step(_t(x), "w"))
+    ov, oi = O.threshold_select(x, 1.5)
+    exp = (O.python_sum([O.sparse_decode(ov, oi, x.size)]) / np.float32(1)).astype(np.float32)
+    assert same_bits(out, exp)
+    res = _np(comm.memory.residuals["w"])
+    assert same_bits(res, O.residual_update(x, O.sparse_decode(ov, oi, x.size)))
