@@ -1,13 +1,21 @@
 """Headline benchmark: grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket.
 
-Workload (BASELINE.json configs[1]): one ``Allgather(TopKCompressor(0.01), ResidualMemory(), N)
-.step(g, name)`` per step on a 256 MiB fp32 gradient bucket already resident in HBM:
-compensate (t = r + g) -> top-k 1 % -> residual update -> payload exchange -> decode+aggregate.
-value = N * 4n bytes / step time (whole job), n = 67,108,864.
+Default workload (BASELINE.json configs[1]): one ``Allgather(TopKCompressor(0.01),
+ResidualMemory(), N).step(g, name)`` per step on a 256 MiB fp32 gradient bucket already resident in
+HBM: compensate (t = r + g) -> top-k 1 % -> residual update -> payload exchange -> decode +
+aggregate.  value = N * 4n bytes / step time (whole job), n = 67,108,864.
 
-At N > 1 every rank runs its own bucket (data-parallel replicas of the reference's Allgather
+At N > 1 every rank runs its own bucket (data-parallel replicas, the reference's Allgather
 semantics); the fixed-size payloads (k f32 values + k i32 indices) move with one RCCL
 all_gather_into_tensor per step and are decoded + aggregated in rank order on every rank.
+
+Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, not the headline):
+  sign       signSGD Allgather step, 4 MiB fp32 (configs[0])
+  sign256    signSGD Allgather step, 256 MiB fp32
+  qsgd       QSGD(127, 128) compress + decompress over the 161-tensor ResNet-50 set, one
+             segmented launch per stage (configs[2])
+  terngrad   TernGrad, same set (configs[2])
+  powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
 
 Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
@@ -26,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+F32_PEAK_TFLOPS = 157.3        # MI355X dense f32 MFMA peak (spec)
 
 
 def parse():
@@ -33,6 +42,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="topk",
+                    choices=["topk", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -41,19 +52,73 @@ def parse():
     return ap.parse_args()
 
 
+def resnet50_shapes():
+    """The 161 parameter shapes of torchvision's ResNet-50 (25,557,032 elements)."""
+    shapes = [(64, 3, 7, 7), (64,), (64,)]
+    inplanes = 64
+    for planes, blocks in ((64, 3), (128, 4), (256, 6), (512, 3)):
+        for b in range(blocks):
+            shapes += [(planes, inplanes, 1, 1), (planes,), (planes,), (planes, planes, 3, 3), (planes,), (planes,),
+                       (planes * 4, planes, 1, 1), (planes * 4,), (planes * 4,)]
+            if b == 0:
+                shapes += [(planes * 4, inplanes, 1, 1), (planes * 4,), (planes * 4,)]
+            inplanes = planes * 4
+    shapes += [(1000, 2048), (1000,)]
+    return shapes
+
+
+def timed(fn, steps, warmup, world, dev):
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn(warmup + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+    if args.gpus > 1 and world == 1:
+        raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    run = {"topk": bench_topk, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+           "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
+    line = run(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def base_line(args, world, elapsed, nbytes_per_rank, metric=METRIC):
+    ms = elapsed / args.steps * 1e3
+    return {
+        "metric": metric, "value": round(world * nbytes_per_rank * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (torch.randn, buckets rotated per rank)",
+    }
+
+
+# ------------------------------------------------------------------------------------------ top-k
+def bench_topk(args, world, rank, dev):
     from grace_amd import ops
     from grace_amd.dist.communicator.allgather import Allgather
     from grace_amd.dist.compressor.topk import TopKCompressor
@@ -73,45 +138,31 @@ def main():
         j = i % args.buffers
         return comm.step(grads[j], names[j])
 
-    # warm-up (first step per name has no residual; run every name at least once)
-    for i in range(max(args.warmup, args.buffers)):
+    for i in range(args.buffers):       # every name's first step has no residual
         step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-
     ops.timer_enable(True)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
     main_ms, launches = ops.timer_collect()
     ops.timer_enable(False)
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = world * 4.0 * n * args.steps / elapsed / 1e9
-
-    # roofline of the dominant kernel (topk_main), timed with HIP events on its own stream
+    line = base_line(args, world, elapsed, 4.0 * n)
+    line["config"] = {"workload": "Allgather(TopK 1%, ResidualMemory).step on a 256 MiB fp32 bucket "
+                                  "(BASELINE configs[1])",
+                      "numel": n, "k": k, "parallelism": f"dp{world} replicas, RCCL allgather of payloads"}
+    # roofline of the dominant kernel (topk_main), HIP events on the stream it runs on; only the
+    # timed steps are counted (warm-up launches ran with the timer off)
     main_avg_ms = main_ms / max(launches, 1)
     bytes_per_elem = 16 if world == 1 else 12          # g, r read; r' (+ dense out at W=1) written
     main_bytes = bytes_per_elem * n
     achieved = main_bytes / (main_avg_ms * 1e-3) / 1e9
-    step_bytes = 16 * n + 16 * k if world == 1 else None
-    roofline = {
-        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-        "kernel": "topk_main", "kernel_avg_us": round(main_avg_ms * 1e3, 2),
-        "algorithmic_bytes_per_launch": main_bytes,
-    }
-    if step_bytes:
-        roofline["step_frac"] = round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "topk_main", "kernel_avg_us": round(main_avg_ms * 1e3, 2), "launches": launches,
+                "algorithmic_bytes_per_launch": main_bytes}
+    if world == 1:
+        step_bytes = 16 * n + 16 * k
+        roofline["step_algorithmic_bytes"] = step_bytes
+        roofline["step_frac"] = round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
     prof = os.path.join(ROOT, "profiles", "pmc_topk_main.json")
     if os.path.exists(prof):
         try:
@@ -121,29 +172,14 @@ def main():
                 roofline["traffic"] = pmc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
-
-    cpu = None
+    line["roofline"] = roofline
+    line["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_steps > 0:
-        cpu = cpu_baseline(n, args.ratio, args.cpu_baseline_steps)
-
-    if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (torch.randn buckets, 3 rotated per rank)",
-            "config": {"workload": "Allgather(TopK 1% , ResidualMemory).step on a 256 MiB fp32 bucket "
-                                   "(BASELINE configs[1])",
-                       "numel": n, "k": k, "parallelism": f"dp{world} replicas, RCCL allgather of payloads"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        line["cpu_baseline"] = cpu_baseline_topk(n, args.ratio, args.cpu_baseline_steps)
+    return line
 
 
-def cpu_baseline(n, ratio, steps):
+def cpu_baseline_topk(n, ratio, steps):
     """The oracle's top-k + residual step on the host cores over the same bucket size."""
     import numpy as np
     from oracle import grace_oracle as O
@@ -158,7 +194,85 @@ def cpu_baseline(n, ratio, steps):
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{steps} full 256 MiB top-k 1% + residual steps of oracle/grace_oracle.py "
-                      f"(numpy partition + torch CPU ops), {dt * 1e3:.0f} ms/step"}
+                      f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step"}
+
+
+# ------------------------------------------------------------------------------------------ sign
+def bench_sign(args, world, rank, dev):
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.signsgd import SignSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    n = (1 << 20) if args.workload == "sign" else args.numel
+    comm = Allgather(SignSGDCompressor(), NoneMemory(), world)
+    nbuf = max(args.buffers, 64 if n <= (1 << 20) else 3)     # 4 MiB buckets: rotate past the MALL
+    grads = [torch.randn(n, device=dev) for _ in range(nbuf)]
+    elapsed = timed(lambda i: comm.step(grads[i % nbuf], "w"), args.steps, args.warmup, world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric=f"grad-codec GB/s (device-resident encode+decode), {4 * n >> 20} MiB fp32 signSGD")
+    line["config"] = {"workload": f"Allgather(SignSGD, NoneMemory).step, {4 * n >> 20} MiB fp32", "numel": n,
+                      "rotated_buffers": nbuf}
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(10.0 * n / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(10.0 * n / t / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "note": "10n algorithmic bytes per step (SURVEY.md §8d config 1)"}
+    return line
+
+
+# ------------------------------------------------------------------------------------------ QSGD / TernGrad
+def bench_quant(args, world, rank, dev):
+    from grace_amd import ops
+    shapes = resnet50_shapes()
+    sizes = [int(torch.Size(s).numel()) for s in shapes]
+    total = sum(sizes)
+    nbuf = 3
+    flats = [torch.randn(total, device=dev) * 0.01 for _ in range(nbuf)]
+    if args.workload == "qsgd":
+        def step(i):
+            x = flats[i % nbuf]
+            codes, norms = ops.qsgd_compress(x, 127, 128, sizes=sizes, seed=i)
+            return ops.qsgd_decompress(codes, norms, 127, 128, total, sizes=sizes)
+        nb = sum((s + 127) // 128 for s in sizes)
+        alg = 10 * total + 8 * nb
+    else:
+        def step(i):
+            x = flats[i % nbuf]
+            codes, scal = ops.terngrad_compress(x, sizes=sizes, seed=i)
+            return ops.terngrad_decompress(codes, scal, total, sizes=sizes)
+        alg = 10 * total + 8 * len(sizes)
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
+    t = elapsed / args.steps
+    line = base_line(args, world, elapsed, 4.0 * total,
+                     metric=f"grad-codec GB/s (device-resident encode+decode), ResNet-50 set {args.workload}")
+    line["config"] = {"workload": f"{args.workload} compress+decompress, 161 ResNet-50 tensors in one segmented "
+                                  "launch per stage (BASELINE configs[2])", "numel": total, "tensors": len(sizes)}
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": alg}
+    return line
+
+
+# ------------------------------------------------------------------------------------------ PowerSGD
+def bench_powersgd(args, world, rank, dev):
+    from grace_amd.dist.communicator.allreduce import Allreduce
+    from grace_amd.dist.compressor.powersgd import PowerSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    n = m = 4096
+    r = 4
+    comm = Allreduce(PowerSGDCompressor(rank=r, world_size=world), NoneMemory(), world)
+    grads = [torch.randn(n, m, device=dev) for _ in range(3)]
+    elapsed = timed(lambda i: comm.step(grads[i % 3], "w"), args.steps, args.warmup, world, dev)
+    t = elapsed / args.steps
+    flops = 3 * 2 * n * m * r
+    line = base_line(args, world, elapsed, 4.0 * n * m,
+                     metric="grad-codec GB/s (device-resident encode+decode), PowerSGD rank 4, 4096x4096")
+    line["config"] = {"workload": "Allreduce(PowerSGD rank 4, NoneMemory).step, 4096x4096 fp32 (BASELINE configs[3])",
+                      "numel": n * m, "rank": r}
+    line["roofline"] = {"bound": "hbm", "achieved": round(12 * n * m / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "mfma_tflops": round(flops / t / 1e12, 3),
+                        "mfma_util": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 5),
+                        "note": "12n algorithmic bytes, 6nmr flops (SURVEY.md §8d config 4; AI = 2 flop/B)"}
+    return line
 
 
 if __name__ == "__main__":
