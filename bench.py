@@ -15,6 +15,8 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   qsgd       QSGD(127, 128) compress + decompress over the 161-tensor ResNet-50 set, one
              segmented launch per stage (configs[2])
   terngrad   TernGrad, same set (configs[2])
+  topk_e2e   the headline step with the bucket arriving from pinned host memory (H2D) and the
+             aggregated dense gradient returned to it (D2H): the PCIe-inclusive rate in DESIGN.md
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
 
 Launch: ``python bench.py`` (N=1) or
@@ -43,7 +45,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
-                    choices=["topk", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
+                    choices=["topk", "topk_e2e", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -98,7 +100,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    run = {"topk": bench_topk, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
     line = run(args, world, rank, dev)
     if rank == 0:
@@ -195,6 +197,37 @@ def cpu_baseline_topk(n, ratio, steps):
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{steps} full 256 MiB top-k 1% + residual steps of oracle/grace_oracle.py "
                       f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step"}
+
+
+def bench_topk_e2e(args, world, rank, dev):
+    """H2D (pinned) -> Allgather(TopK, Residual).step -> D2H (pinned), serial on the current stream."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = args.numel
+    comm = Allgather(TopKCompressor(args.ratio), ResidualMemory(), world)
+    hosts = [torch.randn(n).pin_memory() for _ in range(2)]
+    back = torch.empty(n).pin_memory()
+    dbuf = torch.empty(n, device=dev)
+
+    def step(i):
+        dbuf.copy_(hosts[i % 2], non_blocking=True)
+        out = comm.step(dbuf, "bucket")
+        back.copy_(out, non_blocking=True)
+
+    step(0)
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
+    # the copies alone, for the split
+    def copies(i):
+        dbuf.copy_(hosts[i % 2], non_blocking=True)
+        back.copy_(dbuf, non_blocking=True)
+    t_copy = timed(copies, args.steps, args.warmup, world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric="grad-codec GB/s (host-resident bucket: H2D + encode+decode + D2H), 256 MiB fp32")
+    line["config"] = {"workload": "pinned host bucket -> H2D -> Allgather(TopK 1%, ResidualMemory).step -> D2H",
+                      "numel": n, "h2d_plus_d2h_ms": round(t_copy / args.steps * 1e3, 4)}
+    line["roofline"] = None
+    return line
 
 
 # ------------------------------------------------------------------------------------------ sign

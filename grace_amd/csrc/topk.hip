@@ -10,23 +10,24 @@
 //
 // The reference's native selector (radixtopk_cuda/rdxtopk_cuda.cu:410-534) makes 4 histogram
 // passes over the keys with a device->host sync per digit.  Here the whole selection stays on the
-// device and the bucket is streamed ONCE:
+// device, the bucket is streamed ONCE, and no step ever syncs the host:
 //
-//   1. bracket  (1 workgroup)   strided sample of 32768 |t| keys (2048 runs of 16) -> two keys
-//                               thr_hi >= thr_lo that bracket the k-th largest key with ~6 sigma
-//                               binomial margin; zeroes this step's counters / histogram.
-//   2. main     (n/16384 WGs)   one streaming pass: t = beta r + gamma g, write r' (and the dense
+//   1. sample   (<=128 WGs)     stratified sample of up to 131072 |t| keys (hash-offset strata)
+//                               into a 32768-bin LDS histogram of key>>16, flushed with atomics.
+//   2. select   (1 WG)          ranks of the k-th key in the sample +-6 sigma (binomial) ->
+//                               thr_hi >= thr_lo bracketing the k-th largest key; zeroes this
+//                               step's counters, cursors and histograms.
+//   3. main     (n/16384 WGs)   one streaming pass: t = beta r + gamma g, write r' (and the dense
 //                               world-1 output), key > thr_hi  -> "sure": appended to the payload;
-//                               thr_lo <= key <= thr_hi -> candidate list + 4096-bin LDS histogram
+//                               thr_lo <= key <= thr_hi -> candidate list + 2048-bin histogram
 //                               of the candidate key range.  Appends use wave64 ballot + mbcnt
-//                               into LDS staging, one global atomic per workgroup.
-//   3. finalize (256 WGs)       every WG finds the boundary histogram bin B from the global
-//                               histogram, then candidates above B go to the payload and those in
-//                               B to a short boundary list.
-//   4. boundary (1 WG)          exact selection of the last `need` entries of bin B by (key, -idx);
-//                               if the sample bracket failed (or a list overflowed) this workgroup
-//                               runs the exact single-workgroup radix select over the whole bucket
-//                               instead (slow, rare, same result).
+//                               into LDS staging, one global atomic per workgroup and list.
+//   4. finalize (64 WGs)        every WG finds the boundary bin B from the global histogram;
+//                               candidates above B go to the payload and those in B to a short
+//                               boundary list (block scan + one atomic per round); the last WG
+//                               to arrive selects the final `need` entries of B by (key, -idx).
+//                               If the bracket missed (or a list overflowed) that WG runs the
+//                               exact single-workgroup radix select instead (rare, same result).
 // Small buckets (n <= 32768) run a single-workgroup kernel with the bucket held in LDS.
 #include <math.h>
 #include <string.h>

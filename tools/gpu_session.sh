@@ -29,9 +29,17 @@ for step in "$@"; do
     pytopk) run pytest_topk 900 python3 -m pytest tests/test_gpu_topk.py -x -q ;;
     pytestall) run pytest_gpu_all 1200 python3 -m pytest tests -m gpu -q ;;
     bench)  run bench 600 python3 bench.py ;;
-    benchall) for wl in sign sign256 qsgd terngrad powersgd; do run "bench_$wl" 300 python3 bench.py --workload $wl; done ;;
+    benchall) for wl in ${BENCH_WL:-sign sign256 qsgd terngrad powersgd topk_e2e}; do run "bench_$wl" 300 python3 bench.py --workload $wl; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/gpurun_out/prof_$TAG" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
+    profwl) for wl in ${PROF_WL:-sign qsgd terngrad powersgd}; do
+              run "prof_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d "$ROOT/gpurun_out/prof_${TAG}_$wl" -o bench -- python3 "$ROOT/bench.py" --workload $wl --steps 10 --warmup 3
+            done ;;
+    pmcmem) for c in FETCH_SIZE WRITE_SIZE; do
+              run "pmc_$c" 600 rocprofv3 --pmc $c --output-format csv -d "$ROOT/gpurun_out/pmc_${TAG}_$c" -o pmc \
+                  -- python3 "$ROOT/bench.py" --steps 3 --warmup 3 --no-cpu-baseline
+            done ;;
     probe)  run hbm_probe 300 tools/hbm_probe ;;
     ab)     run ab 600 python3 tools/ab_topk.py ${AB_LIBS} ;;
     pmc)    for c in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT"; do
