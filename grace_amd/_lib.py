@@ -62,10 +62,11 @@ SIGNATURES = {
     "grace_threshold_count": (ST, [P, I64, F32, P, P]),
     "grace_threshold_recount": (ST, [P, I64, F32, P, P]),
     "grace_threshold_write": (ST, [P, I64, P, P, P, P]),
-    "grace_powersgd_p": (ST, [P, I64, I64, P, I32, P, P]),
+    "grace_powersgd_p": (ST, [P, I64, I64, P, I32, P, P, P]),
     "grace_powersgd_workspace_bytes": (SZ, [I64, I64, I32]),
     "grace_powersgd_qt": (ST, [P, I64, I64, P, I32, P, P, P]),
     "grace_orthogonalize": (ST, [P, I64, I32, P]),
+    "grace_normal_orthogonal": (ST, [P, I64, I32, U64, P]),
     "grace_powersgd_outer": (ST, [P, P, I64, I64, I32, P, P, P, P]),
     "grace_normal_fill": (ST, [P, I64, U64, P]),
 }

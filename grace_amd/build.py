@@ -44,7 +44,9 @@ def build(verbose=False, jobs=8, variant=""):
     global FLAGS, LIB
     if variant:
         defs = {"stamps": ["-DGRACE_STAMPS"]}
-        FLAGS = FLAGS + defs.get(variant, [f"-DGRACE_{variant.upper()}"])
+        extra = os.environ.get("GRACE_BUILD_DEFS", "")
+        FLAGS = FLAGS + defs.get(variant, [f"-DGRACE_{variant.upper()}"] if not extra else []) + \
+            [f"-D{d}" for d in extra.split(",") if d]
         LIB = os.path.join(LIBDIR, f"libgrace_hip_{variant}.so")
     objdir = os.path.join(LIBDIR, "obj" + (f"_{variant}" if variant else ""))
     os.makedirs(objdir, exist_ok=True)

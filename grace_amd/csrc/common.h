@@ -73,9 +73,25 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+// 32 random bits for element i of the stream keyed by seed.  mix64(seed) is loop-invariant, so a
+// grid-stride loop pays three 32-bit multiplies per element (64-bit multiplies are 4x dearer on
+// CDNA and would make the streaming codecs ALU-bound).
+__device__ __forceinline__ uint32_t rand32(uint64_t seed, uint64_t i) {
+  const uint64_t k = mix64(seed);
+  const uint32_t h = ((uint32_t)i * 0x9E3779B1u) ^ (uint32_t)k ^ ((uint32_t)(i >> 32) * 0x7FEB352Du);
+  return fmix32(h + (uint32_t)(k >> 32));
+}
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
   // 24 random bits -> [0, 1)
-  return (float)(uint32_t)(mix64(seed ^ mix64(i)) >> 40) * (1.0f / 16777216.0f);
+  return (float)(rand32(seed, i) >> 8) * (1.0f / 16777216.0f);
 }
 
 // Wave-level reductions (64 lanes) via cross-lane shuffles.
@@ -83,6 +99,13 @@ template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// Reduction over the 32 lanes of each half-wave (xor offsets < 32 never cross halves).
+template <typename T>
+__device__ __forceinline__ T half_sum(T v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {

@@ -1,7 +1,7 @@
 // PowerSGD rank-r compression (grace_dl/dist/compressor/powersgd.py:7-65) for CDNA4.
 //
 //   P = M q        (n x m) . (m x r)  -- f32 MFMA v_mfma_f32_16x16x4_f32, K split over 8 waves
-//   orthogonalize(P)                  -- modified Gram-Schmidt, one workgroup
+//   orthogonalize(P)                  -- Cholesky-QR in f64 (= MGS's Q), one workgroup
 //   Q = M^T P      (m x n) . (n x r)  -- f32 MFMA, rows split into slabs, deterministic reduce
 //   out = P Q^T, residual = M - P Q^T -- one streaming pass (decompress + ResidualMemory update)
 //
@@ -16,10 +16,6 @@ namespace grace {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-constexpr int kPWaves = 8;                  // K split of P = M q
-constexpr int kPBlock = kPWaves * kWave;
-constexpr int kQWaves = 4;                  // 4 x 64 columns per workgroup of Q = M^T P
-constexpr int kQBlock = kQWaves * kWave;
 constexpr int kMaxRank = 16;
 
 __device__ __forceinline__ f32x4v mfma4(float a, float b, f32x4v c) {
@@ -27,180 +23,497 @@ __device__ __forceinline__ f32x4v mfma4(float a, float b, f32x4v c) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// P[n x r] = M[n x m] q[m x r].  One workgroup per 16-row tile; wave w covers the K range
-// [w*kspan, (w+1)*kspan) in steps of 16: lane l loads M[i0 + (l&15)][k + 4(l>>4) .. +3] (float4)
-// and issues 4 MFMAs, MFMA s taking element s (the k-slice {k + 4g + s}) with the matching q rows.
+// Workspace: [tickets u32 x kTickets | partials f32].  Split-K / split-row partial products are
+// summed by the LAST workgroup to finish a tile (ticket counter), in a fixed order, so results
+// are deterministic and no separate reduce launch is needed; that workgroup re-zeroes its ticket,
+// so the workspace stays zeroed between calls.
+constexpr int64_t kTickets = 65536;
+constexpr size_t kTicketBytes = sizeof(uint32_t) * kTickets;
+
+// Cross-workgroup partials.  The workgroups of one tile run on different XCDs, whose L2s are not
+// coherent with each other, so the partials are written with agent-scope (sc1, write-through)
+// stores and read back with agent-scope loads.  That makes the usual release/acquire fences --
+// a full L2 writeback (buffer_wbl2) and invalidate (buffer_inv) per workgroup -- unnecessary:
+// the ticket increment only has to wait for the workgroup's own partial stores (vmcnt(0)).
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of p[0], p[stride], ... p[(cnt-1) stride] in that order, 8 loads in flight
+__device__ __forceinline__ float sum_partials(const float* __restrict__ p, int64_t stride, int cnt) {
+  float t = 0.f;
+  int k = 0;
+  for (; k + 8 <= cnt; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld_agent(p + (k + u) * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; k < cnt; ++k) t += ld_agent(p + k * stride);
+  return t;
+}
+
+constexpr int kFan = 8;                     // slabs per first-level reduction group
+
+// t[i] = sum over k < cnt (in order) of p[k * stride + f0 + threadIdx.x + i * 256], i < 4, for
+// entries below `nent`; 4 x 8 loads in flight per round
+__device__ __forceinline__ void sum_partials4(const float* __restrict__ p, int64_t stride, int cnt, int f0,
+                                              int nent, float (&t)[4]) {
+  int fi[4];
+  bool ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    fi[i] = f0 + (int)threadIdx.x + i * 256;
+    ok[i] = fi[i] < nent;
+    t[i] = 0.f;
+  }
+  for (int k = 0; k < cnt; k += 8) {
+    float v[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[i][u] = ld_agent(p + (k + u < cnt ? k + u : 0) * stride + (ok[i] ? fi[i] : 0));   // clamped, unconditional
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < cnt) t[i] += v[i][u];
+  }
+}
+
+// returns true in exactly one (the last-arriving) workgroup of the tile; every thread's partial
+// stores (st_agent) are complete before the workgroup takes its ticket
+__device__ __forceinline__ bool last_arrival(uint32_t* ticket, uint32_t expected) {
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == expected - 1) ? 1u : 0u;
+    if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Both contractions stream M through LDS in tiles of 16 rows x 256 columns: every global load is
+// one row's 1 KB contiguous run (64 lanes x 16 B, non-temporal), the next tile's loads are in
+// flight while the MFMAs consume the current one, and the MFMA operand reads come from LDS (rows
+// padded by 4 floats so the 16-row operand reads spread over the banks).
+constexpr int kTileR = 16;
+constexpr int kTileC = 256;
+constexpr int kTileLd = kTileC + 4;
+constexpr int kPW = 4;                      // waves per workgroup (both kernels)
+constexpr int kPBlockT = kPW * kWave;
+
+// prefetch tile (row0, col0) of M into registers: wave w loads rows w, w+4, w+8, w+12
 template <bool VEC>
-__global__ __launch_bounds__(kPBlock) void psgd_p_kernel(const float* __restrict__ M, int64_t n, int64_t m,
-                                                        const float* __restrict__ q, int r,
-                                                        float* __restrict__ P) {
-  __shared__ float red[kPWaves][16][17];
+__device__ __forceinline__ void tile_load(const float* __restrict__ M, int64_t n, int64_t m, int64_t rlo,
+                                          int64_t rhi, int64_t row0, int64_t col0, f32x4v (&pre)[4]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t i0 = (int64_t)blockIdx.x * 16;
-  const int64_t row = i0 + (lane & 15);
+  const int64_t col = col0 + 4 * lane;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t row = row0 + w + 4 * j;
+    const bool rv = row >= rlo && row < rhi && row < n;
+    if (VEC) {
+      const int64_t rc = rv ? row : rlo;
+      const int64_t cc = col < m ? col : m - 4;
+      const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + rc * m + cc));
+      const bool in = rv && col < m;
+      pre[j] = in ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
+    } else {
+      f32x4v v;
+      v.x = (rv && col + 0 < m) ? M[row * m + col + 0] : 0.f;
+      v.y = (rv && col + 1 < m) ? M[row * m + col + 1] : 0.f;
+      v.z = (rv && col + 2 < m) ? M[row * m + col + 2] : 0.f;
+      v.w = (rv && col + 3 < m) ? M[row * m + col + 3] : 0.f;
+      pre[j] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void tile_store(float (*tile)[kTileLd], const f32x4v (&pre)[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4v*>(&tile[w + 4 * j][4 * lane]) = pre[j];
+}
+
+// prefetch `cnt` rows [row0, row0 + cnt) of a small row-major [rows x r] factor (q or P) as a
+// flat run of cnt * r floats, zero past row `rhi`; thread t holds flat entries t, t + 256, ...
+template <int PER>
+__device__ __forceinline__ void fac_load(const float* __restrict__ F, int r, int64_t row0, int64_t rhi, int cnt,
+                                         float (&pre)[PER]) {
+  const int64_t total = (int64_t)cnt * r;
+  const int64_t lim = (rhi - row0) * r;        // valid flat entries
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int64_t e = threadIdx.x + (int64_t)j * kPBlockT;
+    const bool ok = e < total && e < lim;
+    const float v = F[row0 * r + (ok ? e : 0)];
+    pre[j] = ok ? v : 0.f;
+  }
+}
+template <int PER>
+__device__ __forceinline__ void fac_store(float* fs, int r, int cnt, const float (&pre)[PER]) {
+  const int total = cnt * r;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + j * kPBlockT;
+    if (e < total) fs[e] = pre[j];
+  }
+}
+constexpr int kQPer = kTileC * kMaxRank / kPBlockT;   // 16: q rows of one K tile
+constexpr int kPPer = kTileR * kMaxRank / kPBlockT;   // 1: P rows of one row tile
+
+// ------------------------------------------------------------------------------------------------
+// P[n x r] = M[n x m] q[m x r].  Grid = (K chunks, 16-row tiles).  Per tile wave w owns columns
+// [64w, 64w + 64): per 16-wide k-step lane l reads A = M[l&15][k + 4(l>>4) .. +3] and B = the
+// matching q rows from LDS and issues 4 MFMAs (MFMA s = k-slice {k + 4g + s}).  The only global
+// loads in the loop are the NEXT tile's (M and its q rows), so they overlap the MFMAs instead of
+// being serialised behind in-loop loads.  The 4 waves and the K chunks are reduced
+// deterministically (LDS, then the last workgroup of the row tile).
+template <bool VEC>
+__global__ __launch_bounds__(kPBlockT) void psgd_p_kernel(const float* __restrict__ M, int64_t n, int64_t m,
+                                                         const float* __restrict__ q, int r,
+                                                         float* __restrict__ P, float* __restrict__ part,
+                                                         uint32_t* __restrict__ tickets) {
+  __shared__ float tile[kTileR][kTileLd];
+  __shared__ float qs[kTileC * kMaxRank];
+  __shared__ float red[kPW][16][17];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ks = blockIdx.x, nks = gridDim.x;
+  const int64_t rt = blockIdx.y;
+  const int64_t i0 = rt * kTileR;
   const int g = lane >> 4;
   const int col = lane & 15;
-  const int64_t ksteps = (m + 15) / 16;
-  const int64_t per = (ksteps + kPWaves - 1) / kPWaves;
-  const int64_t s0 = w * per, s1 = min(ksteps, s0 + per);
+  const int64_t nkt = (m + kTileC - 1) / kTileC;
+  const int64_t per = (nkt + nks - 1) / nks;
+  const int64_t kt0 = ks * per, kt1 = min(nkt, kt0 + per);
   f32x4v acc = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t st = s0; st < s1; ++st) {
-    const int64_t k = st * 16 + 4 * g;
-    float a[4];
-    if (VEC && row < n && k + 3 < m) {
-      const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + row * m + k));
-      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) a[s] = (row < n && k + s < m) ? M[row * m + k + s] : 0.f;
+  f32x4v pre[4];
+  float qpre[kQPer];
+  if (kt0 < kt1) {
+    tile_load<VEC>(M, n, m, i0, i0 + kTileR, i0, kt0 * kTileC, pre);
+    fac_load(q, r, kt0 * kTileC, m, kTileC, qpre);
+  }
+  for (int64_t kt = kt0; kt < kt1; ++kt) {
+    tile_store(tile, pre);
+    fac_store(qs, r, kTileC, qpre);
+    __syncthreads();
+    if (kt + 1 < kt1) {
+      tile_load<VEC>(M, n, m, i0, i0 + kTileR, i0, (kt + 1) * kTileC, pre);
+      fac_load(q, r, (kt + 1) * kTileC, m, kTileC, qpre);
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float b = (col < r && k + s < m) ? q[(k + s) * r + col] : 0.f;
-      acc = mfma4(a[s], b, acc);
+    for (int st = 0; st < 4; ++st) {
+      const int kl = 64 * w + 16 * st + 4 * g;
+      const f32x4v av = *reinterpret_cast<const f32x4v*>(&tile[lane & 15][kl]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma4(av[s], col < r ? qs[(kl + s) * r + col] : 0.f, acc);
     }
+    __syncthreads();
   }
   // D layout: col = lane & 15, row = (lane >> 4) * 4 + j
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w][(lane >> 4) * 4 + j][lane & 15] = acc[j];
   __syncthreads();
-  if (threadIdx.x < 16 * 16) {
-    const int rr = threadIdx.x / 16, cc = threadIdx.x % 16;
-    float s = 0.f;
+  const int rr = threadIdx.x / 16, cc = threadIdx.x % 16;   // 256 threads = the 16 x 16 tile
+  float sum = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kPWaves; ++ww) s += red[ww][rr][cc];
-    if (cc < r && i0 + rr < n) P[(i0 + rr) * r + cc] = s;
+  for (int ww = 0; ww < kPW; ++ww) sum += red[ww][rr][cc];
+  const bool valid = cc < r && i0 + rr < n;
+  if (nks == 1) {
+    if (valid) P[(i0 + rr) * r + cc] = sum;
+    return;
   }
+  if (valid) st_agent(part + ((int64_t)ks * n + i0 + rr) * r + cc, sum);
+  if (!last_arrival(tickets + rt, (uint32_t)nks)) return;
+  if (valid) P[(i0 + rr) * r + cc] = sum_partials(part + (i0 + rr) * r + cc, (int64_t)n * r, nks);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Q partials: part[slab][m x r] = M[slab rows]^T P[slab rows].  Workgroup = 4 waves x 64 columns;
-// per 4-row step lane l loads M[i + (l>>4)][j0 + 4(l&15) .. +3] (1 KB per wave-instruction) and
-// issues 4 MFMAs (tile s = columns j0 + 4jj + s) against A = P^T[c = l&15][k = l>>4].
+// Q = M^T P.  Grid = (256-column groups, row slabs).  Per 16-row tile wave w owns columns
+// [64w, 64w + 64) of the group: per 4-row step lane l reads B = M[4st + (l>>4)][64w + 4(l&15) ..
+// +3] and A = P^T[c = l&15][row] from LDS and issues 4 MFMAs (tile s = columns 4jj + s).  As in
+// P, the loop's only global loads are the next tile's (M rows and their P rows).  The slabs are
+// reduced in two fixed-order levels (groups of kFan slabs, then the groups), each by the last
+// workgroup to arrive.
 template <bool VEC>
-__global__ __launch_bounds__(kQBlock) void psgd_qt_kernel(const float* __restrict__ M, int64_t n, int64_t m,
-                                                         const float* __restrict__ P, int r, int64_t slab,
-                                                         float* __restrict__ part) {
+__global__ __launch_bounds__(kPBlockT) void psgd_qt_kernel(const float* __restrict__ M, int64_t n, int64_t m,
+                                                          const float* __restrict__ P, int r, int64_t slab,
+                                                          float* __restrict__ Q, float* __restrict__ part,
+                                                          uint32_t* __restrict__ tickets) {
+  __shared__ float tile[kTileR][kTileLd];
+  __shared__ float ps[kTileR * kMaxRank];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t j0 = ((int64_t)blockIdx.x * kQWaves + w) * 64;
+  const int64_t cg = blockIdx.x;
+  const int64_t j0 = cg * kTileC;
   const int64_t ilo = (int64_t)blockIdx.y * slab, ihi = min(n, ilo + slab);
   const int kk = lane >> 4, jj = lane & 15;
-  const int64_t jc = j0 + 4 * jj;
   f32x4v acc[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  if (j0 < m) {
-    for (int64_t i = ilo; i < ihi; i += 4) {
-      const int64_t row = i + kk;
-      const bool rv = row < ihi;
-      const float a = (rv && jj < r) ? P[row * r + jj] : 0.f;
-      float b[4];
-      if (VEC && rv && jc + 3 < m) {
-        const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + row * m + jc));
-        b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
-      } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = (rv && jc + s < m) ? M[row * m + jc + s] : 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[s] = mfma4(a, b[s], acc[s]);
-    }
+  f32x4v pre[4];
+  float ppre[kPPer];
+  if (ilo < ihi) {
+    tile_load<VEC>(M, n, m, ilo, ihi, ilo, j0, pre);
+    fac_load(P, r, ilo, ihi, kTileR, ppre);
   }
-  // tile s, lane l, reg j: column j0 + 4 (l & 15) + s, rank row c = (l >> 4) * 4 + j
-  float* pp = part + (int64_t)blockIdx.y * m * r;
+  for (int64_t i = ilo; i < ihi; i += kTileR) {
+    tile_store(tile, pre);
+    fac_store(ps, r, kTileR, ppre);
+    __syncthreads();
+    if (i + kTileR < ihi) {
+      tile_load<VEC>(M, n, m, ilo, ihi, i + kTileR, j0, pre);
+      fac_load(P, r, i + kTileR, ihi, kTileR, ppre);
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int rl = 4 * st + kk;
+      const float a = jj < r ? ps[rl * r + jj] : 0.f;
+      const f32x4v bv = *reinterpret_cast<const f32x4v*>(&tile[rl][64 * w + 4 * jj]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[s] = mfma4(a, bv[s], acc[s]);
+    }
+    __syncthreads();
+  }
+  // tile s, lane l, reg q4: column j0 + 64w + 4 (l & 15) + s, rank row c = (l >> 4) * 4 + q4
+  const int nslab = gridDim.y;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t j = j0 + 4 * (lane & 15) + s;
+    const int64_t j = j0 + 64 * w + 4 * (lane & 15) + s;
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
       const int c = (lane >> 4) * 4 + q4;
-      if (j < m && c < r) pp[j * r + c] = acc[s][q4];
+      if (j < m && c < r) {
+        if (nslab == 1) Q[j * r + c] = acc[s][q4];
+        else st_agent(part + ((int64_t)blockIdx.y * m + j) * r + c, acc[s][q4]);
+      }
     }
   }
-}
-
-__global__ __launch_bounds__(256) void psgd_qreduce_kernel(const float* __restrict__ part, int64_t nslab,
-                                                          int64_t mr, float* __restrict__ Q) {
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < mr; e += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int64_t sl = 0; sl < nslab; ++sl) s += part[sl * mr + e];
-    Q[e] = s;
+  if (nslab == 1) return;
+  // two-level deterministic reduction over the slabs: groups of kFan slabs, then the groups
+  const int ngroups = (nslab + kFan - 1) / kFan;
+  const int sg = blockIdx.y / kFan;
+  const int in_group = min(kFan, nslab - sg * kFan);
+  if (!last_arrival(tickets + cg * ngroups + sg, (uint32_t)in_group)) return;
+  float* part2 = part + (int64_t)nslab * m * r;
+  // the group's entries are one contiguous run of (columns x r) floats per slab; each thread
+  // sums up to 4 of them at once so all of their partial loads are in flight together
+  const int64_t ncol = min((int64_t)kTileC, m - j0);
+  const int nent = (int)(ncol * r);
+  const int64_t sstride = (int64_t)m * r;
+  for (int f0 = 0; f0 < nent; f0 += 4 * kPBlockT) {
+    float t[4];
+    sum_partials4(part + ((int64_t)sg * kFan) * sstride + j0 * r, sstride, in_group, f0, nent, t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + threadIdx.x + i * kPBlockT;
+      if (f < nent) {
+        if (ngroups == 1) Q[j0 * r + f] = t[i];
+        else st_agent(part2 + (int64_t)sg * sstride + j0 * r + f, t[i]);
+      }
+    }
+  }
+  if (ngroups == 1) return;
+  if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
+  for (int f0 = 0; f0 < nent; f0 += 4 * kPBlockT) {
+    float t[4];
+    sum_partials4(part2 + j0 * r, sstride, ngroups, f0, nent, t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + threadIdx.x + i * kPBlockT;
+      if (f < nent) Q[j0 * r + f] = t[i];
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Modified Gram-Schmidt on the columns of A[n x r] in place (powersgd.py:7-18): one workgroup,
-// column norms and projections reduced in f64 through LDS.
-__global__ __launch_bounds__(1024) void psgd_orth_kernel(float* __restrict__ A, int64_t n, int r) {
-  __shared__ double sh[1024 / kWave][kMaxRank];
-  __shared__ float sres[kMaxRank];
+// orthogonalize(A[n x r]) in place (powersgd.py:7-18), one workgroup, as Cholesky-QR in f64:
+//   G = A^T A (f64 accumulation of the f32 entries, one read of A)
+//   R = chol(G)  (upper, positive diagonal)  -- the R of modified Gram-Schmidt
+//   A <- A R^-1  (row-wise forward substitution in f64, one write of A)
+// In exact arithmetic this is the reference's MGS result; with f64 Gram and solve the difference
+// from the f32 MGS is far below the parity tolerance for any A whose condition number the f32
+// MGS itself can handle.  A zero / dependent column gives R_cc = 0 and non-finite output, as MGS.
+constexpr int kOrthBlock = 1024;
+
+// standard normal draw of element i (Box-Muller on the counter-based generator)
+__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t i) {
+  const uint64_t h = mix64(seed ^ mix64(i * 2 + 1));
+  const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);   // (0, 1]
+  const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+}
+
+// R = r rounded up to a power of two (the Gram accumulators live in registers: R(R+1)/2 doubles).
+// DRAW: fill A with normal draws first (powersgd.py:41 q = normal_(); orthogonalize(q)) -- one
+// launch instead of two.  A with n <= kOrthBlock * kOrthRows rows (4096 at r <= 4) is read (or drawn) once into
+// registers and written once; taller A is streamed twice in chunks whose loads are all issued
+// together.
+template <int R, bool DRAW>
+__global__ __launch_bounds__(kOrthBlock) void psgd_orth_kernel(float* __restrict__ A, int64_t n, int r,
+                                                              uint64_t seed) {
+  constexpr int kGram = R * (R + 1) / 2;
+  constexpr int kOrthRows = R <= 4 ? 4 : (R <= 8 ? 2 : 1);   // rows per thread held in registers
+  __shared__ double sh[kOrthBlock / kWave][kGram];
+  __shared__ double Rs[R][R];
+  __shared__ double Rinv[R];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int c = 0; c < r; ++c) {
-    double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) {
-      const double v = A[i * r + c];
-      s += v * v;
+  const bool single = n <= (int64_t)kOrthBlock * kOrthRows;
+  float a[kOrthRows][R];
+  auto load_chunk = [&](int64_t base) {
+#pragma unroll
+    for (int j = 0; j < kOrthRows; ++j) {
+      const int64_t i = base + threadIdx.x + (int64_t)j * kOrthBlock;
+      const bool rv = i < n;
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        float v;
+        if (DRAW) {
+          v = normal_at(seed, (uint64_t)(i * r + c));
+        } else {
+          const float t = A[(rv ? i : 0) * r + (c < r ? c : 0)];   // clamped, unconditional
+          v = t;
+        }
+        a[j][c] = (rv && c < r) ? v : 0.f;
+      }
     }
-    s = wave_sum(s);
-    if (lane == 0) sh[w][0] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int ww = 0; ww < 1024 / kWave; ++ww) t += sh[ww][0];
-      sres[0] = sqrtf((float)t);
+  };
+  double g[kGram];
+#pragma unroll
+  for (int e = 0; e < kGram; ++e) g[e] = 0.0;
+  for (int64_t base = 0; base < n; base += (int64_t)kOrthBlock * kOrthRows) {
+    load_chunk(base);
+#pragma unroll
+    for (int j = 0; j < kOrthRows; ++j) {
+      int e = 0;
+#pragma unroll
+      for (int c = 0; c < R; ++c)
+#pragma unroll
+        for (int c2 = c; c2 < R; ++c2, ++e) g[e] += (double)a[j][c] * (double)a[j][c2];
     }
-    __syncthreads();
-    const float norm = sres[0];
-    for (int64_t i = threadIdx.x; i < n; i += 1024) A[i * r + c] = A[i * r + c] / norm;
-    __syncthreads();
-    if (c + 1 < r) {
-      double d[kMaxRank];
-      for (int c2 = c + 1; c2 < r; ++c2) d[c2] = 0.0;
-      for (int64_t i = threadIdx.x; i < n; i += 1024) {
-        const double col = A[i * r + c];
-        for (int c2 = c + 1; c2 < r; ++c2) d[c2] += col * (double)A[i * r + c2];
+    if (DRAW && !single) {   // tall draw: store the draws, the solve pass re-reads them
+#pragma unroll
+      for (int j = 0; j < kOrthRows; ++j) {
+        const int64_t i = base + threadIdx.x + (int64_t)j * kOrthBlock;
+#pragma unroll
+        for (int c = 0; c < R; ++c)
+          if (i < n && c < r) A[i * r + c] = a[j][c];
       }
-      for (int c2 = c + 1; c2 < r; ++c2) {
-        const double t = wave_sum(d[c2]);
-        if (lane == 0) sh[w][c2] = t;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kGram; ++e) {
+    const double t = wave_sum(g[e]);
+    if (lane == 0) sh[w][e] = t;
+  }
+  __syncthreads();
+  __shared__ double Gs[kGram];
+  if (threadIdx.x < kGram) {
+    double t = 0.0;
+    for (int ww = 0; ww < kOrthBlock / kWave; ++ww) t += sh[ww][threadIdx.x];
+    Gs[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // packed upper-triangle index of (c, c2), c <= c2
+    auto gi = [](int c, int c2) { return c * R - c * (c - 1) / 2 + (c2 - c); };
+    for (int c = 0; c < R; ++c) {
+      double d = Gs[gi(c, c)];
+      for (int k = 0; k < c; ++k) d -= Rs[k][c] * Rs[k][c];
+      const double rcc = c < r ? sqrt(d) : 1.0;
+      const double inv = 1.0 / rcc;
+      Rs[c][c] = rcc;
+      Rinv[c] = inv;
+      for (int c2 = c + 1; c2 < R; ++c2) {
+        double t = Gs[gi(c, c2)];
+        for (int k = 0; k < c; ++k) t -= Rs[k][c] * Rs[k][c2];
+        Rs[c][c2] = c2 < r ? t * inv : 0.0;
       }
-      __syncthreads();
-      if (threadIdx.x < r && threadIdx.x > c) {
-        double t = 0.0;
-        for (int ww = 0; ww < 1024 / kWave; ++ww) t += sh[ww][threadIdx.x];
-        sres[threadIdx.x] = (float)t;
+    }
+  }
+  __syncthreads();
+  // A <- A R^-1, row-wise forward substitution
+  for (int64_t base = 0; base < n; base += (int64_t)kOrthBlock * kOrthRows) {
+    if (!single) load_chunk(base);   // single chunk: the rows are still in registers
+    if (DRAW && !single) {
+      // re-read what pass 1 stored (load_chunk would redraw the identical values; reading is cheaper)
+#pragma unroll
+      for (int j = 0; j < kOrthRows; ++j) {
+        const int64_t i = base + threadIdx.x + (int64_t)j * kOrthBlock;
+#pragma unroll
+        for (int c = 0; c < R; ++c) a[j][c] = (i < n && c < r) ? A[i * r + c] : 0.f;
       }
-      __syncthreads();
-      for (int64_t i = threadIdx.x; i < n; i += 1024) {
-        const float col = A[i * r + c];
-        for (int c2 = c + 1; c2 < r; ++c2) A[i * r + c2] = A[i * r + c2] - sres[c2] * col;
+    }
+#pragma unroll
+    for (int j = 0; j < kOrthRows; ++j) {
+      const int64_t i = base + threadIdx.x + (int64_t)j * kOrthBlock;
+      double x[R];
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        double t = (double)a[j][c];
+#pragma unroll
+        for (int k = 0; k < c; ++k) t -= x[k] * Rs[k][c];   // LDS broadcast reads
+        x[c] = t * Rinv[c];
       }
-      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < R; ++c)
+        if (i < n && c < r) A[i * r + c] = (float)x[c];
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // out = P Q^T (decompress, powersgd.py:58-65); optionally residual = M - out (PowerSGDMemory
-// update, memory/powersgd.py:32-37) in the same pass.  Thread = 4 consecutive columns of a row.
+// update, memory/powersgd.py:32-37) in the same pass.  A workgroup owns 1024 columns x kOuterRows
+// rows: each thread keeps Q[j .. j+3][0 .. r) in registers, P's rows for the band sit in LDS, and
+// the band is streamed with 16-B non-temporal stores (and loads of M for the residual).
+constexpr int kOuterRows = 16;
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void psgd_outer_kernel(const float* __restrict__ P, const float* __restrict__ Q,
                                                         int64_t n, int64_t m, int r, float* __restrict__ out,
                                                         const float* __restrict__ M, float* __restrict__ res) {
-  const int64_t m4 = (m + 3) / 4;
-  const int64_t total = n * m4;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int64_t i = t / m4;
-    const int64_t j = (t - i * m4) * 4;
-    float o[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < r; ++c) {
-      const float p = P[i * r + c];
+  __shared__ float sp[kOuterRows][kMaxRank];
+  const int64_t i0 = (int64_t)blockIdx.y * kOuterRows;
+  for (int e = threadIdx.x; e < kOuterRows * kMaxRank; e += 256) {
+    const int rr = e / kMaxRank, c = e % kMaxRank;
+    sp[rr][c] = (i0 + rr < n && c < r) ? P[(i0 + rr) * r + c] : 0.f;
+  }
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  float qr[4][kMaxRank];
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (j + s < m) o[s] = o[s] + p * Q[(j + s) * r + c];
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int c = 0; c < kMaxRank; ++c) qr[s][c] = (j + s < m && c < r) ? Q[(j + s) * r + c] : 0.f;
+  __syncthreads();
+  if (j >= m) return;
+  const int64_t rows = min((int64_t)kOuterRows, n - i0);
+  for (int rr = 0; rr < rows; ++rr) {
+    const int64_t i = i0 + rr;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < kMaxRank; ++c) {
+      if (c < r) {
+        const float p = sp[rr][c];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o[s] = o[s] + p * qr[s][c];
+      }
     }
     if (VEC && j + 3 < m) {
+#ifdef GRACE_OUTER_PLAIN
+      if (out) *reinterpret_cast<f32x4v*>(out + i * m + j) = f32x4v{o[0], o[1], o[2], o[3]};
+#else
       if (out) __builtin_nontemporal_store(f32x4v{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4v*>(out + i * m + j));
+#endif
       if (res) {
         const f32x4v mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + i * m + j));
         __builtin_nontemporal_store(f32x4v{mv.x - o[0], mv.y - o[1], mv.z - o[2], mv.w - o[3]},
@@ -219,66 +532,106 @@ __global__ __launch_bounds__(256) void psgd_outer_kernel(const float* __restrict
 
 // standard normal draws (Box-Muller on the counter-based generator), for q (powersgd.py:41)
 __global__ __launch_bounds__(256) void normal_kernel(float* __restrict__ x, int64_t n, uint64_t seed) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const uint64_t h = mix64(seed ^ mix64((uint64_t)i * 2 + 1));
-    const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);   // (0, 1]
-    const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
-    x[i] = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
-  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    x[i] = normal_at(seed, (uint64_t)i);
 }
 
 }  // namespace grace
 
 using namespace grace;
 
+namespace grace {
+template <bool DRAW>
+static void launch_orth(float* A, int64_t n, int32_t r, uint64_t seed, hipStream_t st) {
+  if (r <= 1) psgd_orth_kernel<1, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
+  else if (r <= 2) psgd_orth_kernel<2, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
+  else if (r <= 4) psgd_orth_kernel<4, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
+  else if (r <= 8) psgd_orth_kernel<8, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
+  else psgd_orth_kernel<16, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
+}
+}  // namespace grace
+
+
 extern "C" {
 
-grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
-                                void* stream) {
-  GRACE_REQUIRE(M && q && P && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank, "grace_powersgd_p: bad arguments");
-  const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
-  const unsigned grid = (unsigned)((n + 15) / 16);
-  if (vec) psgd_p_kernel<true><<<grid, kPBlock, 0, as_stream(stream)>>>(M, n, m, q, r, P);
-  else psgd_p_kernel<false><<<grid, kPBlock, 0, as_stream(stream)>>>(M, n, m, q, r, P);
-  GRACE_CHECK_LAUNCH("grace_powersgd_p");
-  return GRACE_OK;
+static int p_ksplit(int64_t n, int64_t m) {
+  const int64_t tiles = (n + kTileR - 1) / kTileR;
+  if (tiles > kTickets) return 1;
+#ifdef GRACE_P_KS
+  return (int)min((int64_t)GRACE_P_KS, (m + kTileC - 1) / kTileC);
+#endif
+  const int64_t nkt = (m + kTileC - 1) / kTileC;
+  int64_t ks = (2048 + tiles - 1) / tiles;                  // aim for >= 2048 workgroups
+  if (ks > nkt) ks = nkt;
+  if (ks > 64) ks = 64;
+  return ks < 1 ? 1 : (int)ks;
 }
 
-static int64_t qt_slabs(int64_t n, int64_t m) {
-  const int64_t cgroups = (m + 255) / 256;
-  int64_t s = 512 / cgroups;
-  if (s < 1) s = 1;
-  const int64_t maxs = (n + 3) / 4;
-  return s < maxs ? s : maxs;
+static int64_t qt_slab(int64_t n, int64_t m) {
+  const int64_t groups = (m + kTileC - 1) / kTileC;
+  if (groups * 64 > kTickets / 2) return n;
+#ifdef GRACE_QT_SLAB
+  return GRACE_QT_SLAB;
+#endif
+  const int64_t ns = (1024 + groups - 1) / groups;          // aim for >= 1024 workgroups
+  int64_t slab = (n + ns - 1) / ns;
+  slab = (slab + kTileR - 1) / kTileR * kTileR;
+  if (slab < 2 * kTileR) slab = 2 * kTileR;                 // keep the prefetch pipeline busy
+  while ((n + slab - 1) / slab > 64) slab *= 2;             // <= 64 slabs: two levels of kFan
+  return slab;
 }
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r) {
-  return sizeof(float) * (size_t)(qt_slabs(n, m) * m * r) + 256;
+  const size_t pp = sizeof(float) * (size_t)p_ksplit(n, m) * n * r;
+  const int64_t slab = qt_slab(n, m);
+  const int64_t nslab = (n + slab - 1) / slab;
+  const size_t qp = sizeof(float) * (size_t)(nslab + (nslab + kFan - 1) / kFan) * m * r;
+  return kTicketBytes + align256(pp > qp ? pp : qp);
+}
+
+grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
+                                void* ws, void* stream) {
+  GRACE_REQUIRE(M && q && P && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
+                "grace_powersgd_p: bad arguments");
+  const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
+  const dim3 grid((unsigned)p_ksplit(n, m), (unsigned)((n + kTileR - 1) / kTileR));
+  uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
+  float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
+  if (vec) psgd_p_kernel<true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  else psgd_p_kernel<false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  GRACE_CHECK_LAUNCH("grace_powersgd_p");
+  return GRACE_OK;
 }
 
 grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const float* P, int32_t r, float* Q,
                                  void* ws, void* stream) {
   GRACE_REQUIRE(M && P && Q && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
                 "grace_powersgd_qt: bad arguments");
-  const int64_t ns = qt_slabs(n, m);
-  int64_t slab = (n + ns - 1) / ns;
-  slab = (slab + 3) / 4 * 4;
+  const int64_t slab = qt_slab(n, m);
   const int64_t nslab = (n + slab - 1) / slab;
   const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
-  dim3 grid((unsigned)((m + 255) / 256), (unsigned)nslab);
-  float* part = reinterpret_cast<float*>(ws);
-  if (vec) psgd_qt_kernel<true><<<grid, kQBlock, 0, as_stream(stream)>>>(M, n, m, P, r, slab, part);
-  else psgd_qt_kernel<false><<<grid, kQBlock, 0, as_stream(stream)>>>(M, n, m, P, r, slab, part);
-  GRACE_CHECK_LAUNCH("grace_powersgd_qt");
-  psgd_qreduce_kernel<<<stream_grid(m * r, 256, 1024), 256, 0, as_stream(stream)>>>(part, nslab, m * r, Q);
+  const dim3 grid((unsigned)((m + kTileC - 1) / kTileC), (unsigned)nslab);
+  uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
+  float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
+  if (vec) psgd_qt_kernel<true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, P, r, slab, Q, part, tickets);
+  else psgd_qt_kernel<false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, P, r, slab, Q, part, tickets);
   GRACE_CHECK_LAUNCH("grace_powersgd_qt");
   return GRACE_OK;
 }
 
 grace_status_t grace_orthogonalize(float* A, int64_t n, int32_t r, void* stream) {
   GRACE_REQUIRE(A && n >= 1 && r >= 1 && r <= kMaxRank, "grace_orthogonalize: bad arguments");
-  psgd_orth_kernel<<<1, 1024, 0, as_stream(stream)>>>(A, n, r);
+  launch_orth<false>(A, n, r, 0, as_stream(stream));
   GRACE_CHECK_LAUNCH("grace_orthogonalize");
+  return GRACE_OK;
+}
+
+grace_status_t grace_normal_orthogonal(float* A, int64_t n, int32_t r, uint64_t seed, void* stream) {
+  GRACE_REQUIRE(A && n >= 1 && r >= 1 && r <= kMaxRank, "grace_normal_orthogonal: bad arguments");
+  launch_orth<true>(A, n, r, seed, as_stream(stream));
+  GRACE_CHECK_LAUNCH("grace_normal_orthogonal");
   return GRACE_OK;
 }
 
@@ -289,7 +642,7 @@ grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, i
   const bool vec = (m % 4 == 0) &&
                    (((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(M) |
                       reinterpret_cast<uintptr_t>(residual)) & 15u) == 0);
-  const unsigned grid = stream_grid(n * ((m + 3) / 4), 256, 4096);
+  const dim3 grid((unsigned)((m + 1023) / 1024), (unsigned)((n + kOuterRows - 1) / kOuterRows));
   if (vec) psgd_outer_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(P, Q, n, m, r, out, M, residual);
   else psgd_outer_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(P, Q, n, m, r, out, M, residual);
   GRACE_CHECK_LAUNCH("grace_powersgd_outer");

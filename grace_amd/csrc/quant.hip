@@ -17,6 +17,7 @@
 namespace grace {
 
 constexpr int kQBlock = 256;
+constexpr int kSegLds = 512;     // offset tables up to this many segments are staged in LDS
 
 // segment containing flat element / bucket index `x`: largest s with off[s] <= x
 __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t x) {
@@ -28,11 +29,63 @@ __device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t x)
   return lo;
 }
 
+// Offset tables (seg_off and the per-segment sub-block table) staged once per workgroup, so the
+// per-bucket / per-quad segment search runs on LDS instead of dependent global loads.
+struct SegTables {
+  int64_t seg[kSegLds + 1];
+  int64_t sub[kSegLds + 1];
+};
+
+struct SegView {
+  const int64_t* seg;
+  const int64_t* sub;
+};
+
+__device__ __forceinline__ SegView stage_tables(SegTables& t, const int64_t* seg, const int64_t* sub, int nseg) {
+  if (nseg <= kSegLds) {
+    for (int i = threadIdx.x; i <= nseg; i += blockDim.x) {
+      t.seg[i] = seg[i];
+      if (sub) t.sub[i] = sub[i];
+    }
+    __syncthreads();
+    return SegView{t.seg, sub ? t.sub : nullptr};
+  }
+  return SegView{seg, sub};
+}
+
+// advance a segment cursor monotonically: largest s' >= s with off[s'] <= x
+__device__ __forceinline__ int seg_advance(const int64_t* off, int nseg, int s, int64_t x) {
+  while (s + 1 < nseg && off[s + 1] <= x) ++s;
+  return s;
+}
+
+// contiguous per-workgroup range [lo, hi) of `total` items, in multiples of `step`
+__device__ __forceinline__ void block_range(int64_t total, int64_t step, int64_t& lo, int64_t& hi) {
+  int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  per = (per + step - 1) / step * step;
+  lo = min((int64_t)blockIdx.x * per, total);
+  hi = min(lo + per, total);
+}
+
 // float -> int16 exactly as torch CPU on x86 (cvttss2si to int32, low 16 bits): NaN / out of
 // int32 range -> 0x80000000 -> 0.  Used by QSGD's .type(torch.int16) (qsgd.py:36).
 __device__ __forceinline__ int32_t f2i16_x86(float v) {
   if (!(fabsf(v) < 2147483648.0f)) return 0;   // NaN, inf, |v| >= 2^31
   return (int32_t)(int16_t)(int32_t)v;
+}
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// 4 consecutive floats from p[e .. e+3], zero past `end`; one 16-B load when aligned and full
+__device__ __forceinline__ void load_quad(const float* __restrict__ p, int64_t e, int64_t end, bool aligned,
+                                          float (&v)[4]) {
+  if (aligned && e + 3 < end) {
+    const f4v q = *reinterpret_cast<const f4v*>(p + e);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = e + j < end ? p[e + j] : 0.f;
+  }
 }
 
 // ================================================================================================
@@ -41,81 +94,267 @@ __device__ __forceinline__ int32_t f2i16_x86(float v) {
 //   level    = (reciprocal(norm) * q) * |x|   -- Tensor.__rdiv__ is reciprocal() * q
 //   new      = floor(level) + (u < level - floor(level))
 //   code     = int16(new * sign(x)) -> int8 (q < 128) or fp16 (q >= 128)
-// One wave per group of buckets: each lane loads its slice of the bucket, the bucket norm is a
-// shuffle reduction, then the same lane encodes its elements.  Reads x once.
+// A half-wave (32 lanes x 4 elements) owns one bucket of up to 128: one 16-B load per lane, the
+// bucket norm is a 5-step xor-shuffle reduction, then the lane encodes the 4 values it holds and
+// stores them with one 4-B (int8) / 8-B (fp16) write.  x is read exactly once.  Buckets larger
+// than 128 loop over 128-element slices (two passes, the second hitting L2).
 // VARIANT 0: QSGDCompressor (qsgd.py:12-39).  VARIANT 1: QSGDCompressor_CUDA / qsgd_cuda.cu:320-388
 // (f64 norms over finite elements, level = q / norm * |x| by one division, NaN/Inf -> -128).
+template <typename CodeT, int VARIANT>
+__device__ __forceinline__ CodeT qsgd_code(float xv, float level, float ui, float norm) {
+  const float prev = floorf(level);
+  if constexpr (VARIANT == 0) {
+    const float nl = prev + ((ui < level - prev) ? 1.0f : 0.0f);
+    const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : (xv == 0.f ? 0.f : xv));   // torch.sign
+    const int32_t c16 = f2i16_x86(nl * sg);
+    if constexpr (sizeof(CodeT) == 1) return (CodeT)(int8_t)c16;
+    else return (CodeT)__float2half((float)(int16_t)c16);
+  } else {
+    int8_t c = -128;
+    if (isfinite(norm) && isfinite(xv)) {
+      const int8_t pl = (int8_t)prev;
+      c = (ui < level - prev) ? (int8_t)(pl + 1) : pl;
+      if (xv < 0.f) c = (int8_t)-c;
+    }
+    return (CodeT)c;
+  }
+}
+
+template <typename CodeT>
+__device__ __forceinline__ void store_codes4(CodeT* __restrict__ codes, int64_t e, int64_t end, bool aligned,
+                                             const CodeT (&c)[4]) {
+  if (aligned && e + 3 < end) {
+    if constexpr (sizeof(CodeT) == 1) {
+      const uint32_t w = (uint32_t)(uint8_t)c[0] | ((uint32_t)(uint8_t)c[1] << 8) |
+                         ((uint32_t)(uint8_t)c[2] << 16) | ((uint32_t)(uint8_t)c[3] << 24);
+      *reinterpret_cast<uint32_t*>(codes + e) = w;
+    } else {
+      uint2 w;
+      w.x = (uint32_t)__half_as_ushort(c[0]) | ((uint32_t)__half_as_ushort(c[1]) << 16);
+      w.y = (uint32_t)__half_as_ushort(c[2]) | ((uint32_t)__half_as_ushort(c[3]) << 16);
+      *reinterpret_cast<uint2*>(codes + e) = w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (e + j < end) codes[e + j] = c[j];
+  }
+}
+
 template <typename CodeT, int VARIANT>
 __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
     int nseg, int64_t nbuckets, int bucket, float qf, const float* __restrict__ u, uint64_t seed,
     const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * kQBlock + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * kQBlock) >> 6;
-  for (int64_t b = wave; b < nbuckets; b += nwaves) {
-    const int s = find_seg(bkt_off, nseg, b);
-    const int64_t base = seg_off[s] + (b - bkt_off[s]) * bucket;
-    const int64_t end = min(base + (int64_t)bucket, seg_off[s + 1]);
+  __shared__ SegTables tab;
+  const SegView sv = stage_tables(tab, seg_off, bkt_off, nseg);
+  const int l32 = threadIdx.x & 31;
+  constexpr int kHalves = kQBlock / 32;
+  int64_t blo, bhi;
+  block_range(nbuckets, kHalves, blo, bhi);
+  const int64_t b_first = blo + (threadIdx.x >> 5);
+  int s = b_first < bhi ? find_seg(sv.sub, nseg, b_first) : 0;
+  if (bucket <= 128) {
+    // two buckets per half-wave per iteration: both 16-B loads are in flight before either reduces
+    for (int64_t b = b_first; b < bhi; b += 2 * kHalves) {
+      int64_t bb[2], base[2], end[2];
+      bool ok[2], aligned[2];
+      float v[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bb[h] = b + h * kHalves;
+        ok[h] = bb[h] < bhi;
+        if (ok[h]) s = seg_advance(sv.sub, nseg, s, bb[h]);
+        base[h] = sv.seg[s] + (bb[h] - sv.sub[s]) * bucket;
+        end[h] = ok[h] ? min(base[h] + (int64_t)bucket, sv.seg[s + 1]) : base[h];
+        aligned[h] = (base[h] & 3) == 0;
+        load_quad(x, base[h] + 4 * l32, end[h], aligned[h], v[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!ok[h]) break;
+        const int64_t e = base[h] + 4 * l32;
+        float norm;
+        if (norms_in) {
+          norm = norms_in[bb[h]];
+        } else {
+          double acc = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (VARIANT == 0 || isfinite(v[h][j])) acc += (double)v[h][j] * (double)v[h][j];
+          acc = half_sum(acc);
+          norm = VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
+        }
+        if (l32 == 0) norms_out[bb[h]] = norm;
+        const float scale = VARIANT == 0 ? (1.0f / norm) * qf : qf / norm;
+        float uu[4];
+        if (u) {
+          load_quad(u, e, end[h], aligned[h], uu);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) uu[j] = uniform01(seed, (uint64_t)(e + j));
+        }
+        CodeT c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float level = VARIANT == 0 ? scale * fabsf(v[h][j]) : qf / norm * fabsf(v[h][j]);
+          c[j] = qsgd_code<CodeT, VARIANT>(v[h][j], level, uu[j], norm);
+        }
+        store_codes4(codes, e, end[h], aligned[h], c);
+      }
+    }
+    return;
+  }
+  for (int64_t b = b_first; b < bhi; b += kHalves) {
+    s = seg_advance(sv.sub, nseg, s, b);
+    const int64_t base = sv.seg[s] + (b - sv.sub[s]) * bucket;
+    const int64_t end = min(base + (int64_t)bucket, sv.seg[s + 1]);
     float norm;
     if (norms_in) {
       norm = norms_in[b];
     } else {
       double acc = 0.0;
-      for (int64_t i = base + lane; i < end; i += 64) {
-        const double v = (double)x[i];
-        if (VARIANT == 0 || isfinite(v)) acc += v * v;
+      for (int64_t i = base + l32; i < end; i += 32) {
+        const float v = x[i];
+        if (VARIANT == 0 || isfinite(v)) acc += (double)v * (double)v;
       }
-      acc = wave_sum(acc);
+      acc = half_sum(acc);
       norm = VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
     }
-    if (lane == 0) norms_out[b] = norm;
+    if (l32 == 0) norms_out[b] = norm;
     const float scale = VARIANT == 0 ? (1.0f / norm) * qf : qf / norm;
-    for (int64_t i = base + lane; i < end; i += 64) {
-      const float xv = x[i];
-      const float level = scale * fabsf(xv);
-      const float prev = floorf(level);
+    for (int64_t i = base + l32; i < end; i += 32) {
+      const float v = x[i];
       const float ui = u ? u[i] : uniform01(seed, (uint64_t)i);
-      const float nl = prev + ((ui < level - prev) ? 1.0f : 0.0f);
-      if constexpr (VARIANT == 0) {
-        const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : (xv == 0.f ? 0.f : xv));   // torch.sign
-        const int32_t c16 = f2i16_x86(nl * sg);
-        if constexpr (sizeof(CodeT) == 1) codes[i] = (CodeT)(int8_t)c16;
-        else codes[i] = (CodeT)__float2half((float)(int16_t)c16);
-      } else {
-        int8_t c = -128;
-        if (isfinite(norm) && isfinite(xv)) {
-          const int8_t pl = (int8_t)floorf(level);
-          c = (ui < level - prev) ? (int8_t)(pl + 1) : pl;
-          if (xv < 0.f) c = (int8_t)-c;
-        }
-        codes[i] = (CodeT)c;
-      }
+      const float level = VARIANT == 0 ? scale * fabsf(v) : qf / norm * fabsf(v);
+      codes[i] = qsgd_code<CodeT, VARIANT>(v, level, ui, norm);
     }
+  }
+}
+
+// 4 codes of one rank at p[0 .. 3] as floats (vec: one 4-B / 8-B load)
+template <typename CodeT>
+__device__ __forceinline__ void load_codes4(const CodeT* __restrict__ p, bool vec, float (&c)[4]) {
+  if constexpr (sizeof(CodeT) == 1) {
+    uint32_t wd;
+    if (vec) wd = *reinterpret_cast<const uint32_t*>(p);
+    else wd = (uint32_t)(uint8_t)p[0] | ((uint32_t)(uint8_t)p[1] << 8) | ((uint32_t)(uint8_t)p[2] << 16) |
+              ((uint32_t)(uint8_t)p[3] << 24);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = (float)(int8_t)(wd >> (8 * j));
+  } else {
+    uint2 wd;
+    if (vec) {
+      wd = *reinterpret_cast<const uint2*>(p);
+    } else {
+      wd.x = (uint32_t)__half_as_ushort(p[0]) | ((uint32_t)__half_as_ushort(p[1]) << 16);
+      wd.y = (uint32_t)__half_as_ushort(p[2]) | ((uint32_t)__half_as_ushort(p[3]) << 16);
+    }
+    c[0] = __half2float(__ushort_as_half((unsigned short)wd.x));
+    c[1] = __half2float(__ushort_as_half((unsigned short)(wd.x >> 16)));
+    c[2] = __half2float(__ushort_as_half((unsigned short)wd.y));
+    c[3] = __half2float(__ushort_as_half((unsigned short)(wd.y >> 16)));
+  }
+}
+
+template <typename CodeT>
+__device__ __forceinline__ float load_code1(const CodeT* __restrict__ p) {
+  if constexpr (sizeof(CodeT) == 1) return (float)(int8_t)*p;
+  else return __half2float(*p);
+}
+
+// Decoders: each workgroup walks a contiguous range in rounds of kDecRound elements; per round a
+// thread owns kDecQuads quads spaced one workgroup-width (1024 elements) apart, so every load and
+// 16-B store instruction of a wave is contiguous, and all of the round's loads are issued before
+// any of its results is needed.  The segment cursor only advances.
+constexpr int kDecQuads = 4;
+constexpr int64_t kDecRound = (int64_t)kQBlock * 4 * kDecQuads;
+
+// element-wise decode of [i0, i1) (quads that straddle a segment end; kept out of line so the
+// fast path's register budget stays small)
+template <typename CodeT, int VARIANT, bool B128>
+__device__ __attribute__((noinline)) void qsgd_decode_slow(
+    const CodeT* __restrict__ codes, const float* __restrict__ norms, int64_t code_stride, int64_t norm_stride,
+    int world, const int64_t* seg, const int64_t* sub, int nseg, int64_t i0, int64_t i1, int bucket, float qf,
+    float divisor, int aggregate, float* __restrict__ out) {
+  for (int64_t i = i0; i < i1; ++i) {
+    const int sj = find_seg(seg, nseg, i);
+    const uint32_t off = (uint32_t)(i - seg[sj]);
+    const int64_t bk = sub[sj] + (B128 ? (off >> 7) : off / (uint32_t)bucket);
+    float a = 0.f;
+    for (int w = 0; w < world; ++w) {
+      const float c = load_code1(codes + w * code_stride + i);
+      float d = (norms[w * norm_stride + bk] / qf) * c;
+      if (VARIANT == 1 && c == -128.0f) d = __int_as_float(0x7FC00000);
+      a = (aggregate || w > 0) ? a + d : d;
+    }
+    out[i] = divisor == 1.0f ? a : a / divisor;
   }
 }
 
 // decode (+ rank-ordered aggregate of W payloads): out = ((0 + d_0) + d_1 ...) / divisor with
 // d_w = (norm_w / q) * code_w  (qsgd.py:44-49).  W = 1, divisor = 1 is plain decompress.
-template <typename CodeT, int VARIANT>
+template <typename CodeT, int VARIANT, bool B128>
 __global__ __launch_bounds__(kQBlock) void qsgd_decode_kernel(
     const CodeT* __restrict__ codes, const float* __restrict__ norms, int64_t code_stride,
     int64_t norm_stride, int world, const int64_t* __restrict__ seg_off,
     const int64_t* __restrict__ bkt_off, int nseg, int64_t n, int bucket, float qf, float divisor,
-    int aggregate, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock) {
-    const int s = find_seg(seg_off, nseg, i);
-    const int64_t b = bkt_off[s] + (i - seg_off[s]) / bucket;
-    float acc = 0.f;
-    for (int w = 0; w < world; ++w) {
-      float c;
-      if constexpr (sizeof(CodeT) == 1) c = (float)(int8_t)codes[w * code_stride + i];
-      else c = __half2float(codes[w * code_stride + i]);
-      float d = (norms[w * norm_stride + b] / qf) * c;
-      if (VARIANT == 1 && c == -128.0f) d = __int_as_float(0x7FC00000);
-      acc = (aggregate || w > 0) ? acc + d : d;   // Python sum: 0 + d_0 + d_1 ...
+    int aggregate, int vec, float* __restrict__ out) {
+  __shared__ SegTables tab;
+  const SegView sv = stage_tables(tab, seg_off, bkt_off, nseg);
+  int64_t lo, hi;
+  block_range(n, kDecRound, lo, hi);
+  int s = lo < hi ? find_seg(sv.seg, nseg, lo + 4 * threadIdx.x < hi ? lo + 4 * threadIdx.x : lo) : 0;
+  for (int64_t r0 = lo; r0 < hi; r0 += kDecRound) {
+    int64_t e[kDecQuads], b0[kDecQuads];
+    int split[kDecQuads];
+    bool fast[kDecQuads];
+#pragma unroll
+    for (int k = 0; k < kDecQuads; ++k) {
+      e[k] = r0 + (int64_t)k * kQBlock * 4 + 4 * threadIdx.x;
+      const int64_t ec = e[k] < hi ? e[k] : hi - 1;
+      s = seg_advance(sv.seg, nseg, s, ec);
+      fast[k] = e[k] + 3 < hi && e[k] + 3 < sv.seg[s + 1] && bucket >= 4;
+      const uint32_t off = (uint32_t)(ec - sv.seg[s]);
+      const uint32_t bo = B128 ? (off >> 7) : off / (uint32_t)bucket;
+      const uint32_t in_b = B128 ? (off & 127u) : off - bo * (uint32_t)bucket;
+      split[k] = (int)min((uint32_t)bucket - in_b, 4u);
+      b0[k] = sv.sub[s] + bo;
     }
-    out[i] = divisor == 1.0f ? acc : acc / divisor;
+    float acc[kDecQuads][4] = {};
+    for (int w = 0; w < world; ++w) {
+      float c[kDecQuads][4], na[kDecQuads], nb[kDecQuads];
+#pragma unroll
+      for (int k = 0; k < kDecQuads; ++k) {
+        if (fast[k]) {
+          load_codes4(codes + w * code_stride + e[k], vec != 0, c[k]);
+          na[k] = norms[w * norm_stride + b0[k]];
+          nb[k] = split[k] < 4 ? norms[w * norm_stride + b0[k] + 1] : na[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kDecQuads; ++k) {
+        if (!fast[k]) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = ((j < split[k] ? na[k] : nb[k]) / qf) * c[k][j];
+          if (VARIANT == 1 && c[k][j] == -128.0f) d = __int_as_float(0x7FC00000);
+          acc[k][j] = (aggregate || w > 0) ? acc[k][j] + d : d;   // Python sum: 0 + d_0 + d_1 ...
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDecQuads; ++k) {
+      if (fast[k]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k][j] = divisor == 1.0f ? acc[k][j] : acc[k][j] / divisor;
+        __builtin_nontemporal_store(f4v{acc[k][0], acc[k][1], acc[k][2], acc[k][3]},
+                                    reinterpret_cast<f4v*>(out + e[k]));
+      } else {
+        qsgd_decode_slow<CodeT, VARIANT, B128>(codes, norms, code_stride, norm_stride, world, sv.seg, sv.sub, nseg,
+                                               e[k], min(e[k] + 4, hi), bucket, qf, divisor, aggregate, out);
+      }
+    }
   }
 }
 
@@ -125,29 +364,33 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_kernel(
 //   c      = f32(2.5 * (double)f32(std))       clamp bound as torch rounds the Python double
 //   scalar = max |clamp(x, -c, c)| = min(max|x|, c)
 //   code   = (u * scalar >= |clamp x|) ? 0 : sign(x)          int8 in {-1, 0, 1}
-// Stage 1 writes f64 partials per work unit; stage 2 (encode) reduces its segment's partials in
-// fixed order (deterministic), derives the scale and encodes its unit.
+// Stage 1 writes f64 partials per work unit (16384 elements); stage 2 (encode) reduces its
+// segment's partials with the whole workgroup in a fixed order (every unit of a segment derives
+// the identical scale), then encodes its unit.  Both stages move 16 B per lane.
 constexpr int kTernUnit = 16384;
 
 struct TernPartial { double sum, sq; float amax; uint32_t nan; };
 
-__global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __restrict__ x,
-                                                            const int64_t* __restrict__ seg_off,
-                                                            const int64_t* __restrict__ unit_off, int nseg,
-                                                            TernPartial* __restrict__ part) {
-  const int64_t unit = blockIdx.x;
-  const int s = find_seg(unit_off, nseg, unit);
-  const int64_t base = seg_off[s] + (unit - unit_off[s]) * kTernUnit;
-  const int64_t end = min(base + (int64_t)kTernUnit, seg_off[s + 1]);
-  double sum = 0.0, sq = 0.0;
-  float amax = 0.f;
-  uint32_t nan = 0;
-  for (int64_t i = base + threadIdx.x; i < end; i += kQBlock) {
-    const float v = x[i];
-    sum += (double)v;
-    sq += (double)v * (double)v;
-    if (v != v) nan = 1; else amax = fmaxf(amax, fabsf(v));
-  }
+// [base, end) split into a scalar head, 16-B aligned quads and a scalar tail
+struct QuadSplit {
+  int64_t a0, a1;   // aligned quad range [a0, a1), a0 % 4 == a1 % 4 == 0
+};
+__device__ __forceinline__ QuadSplit quad_split(int64_t base, int64_t end) {
+  int64_t a0 = (base + 3) & ~(int64_t)3;
+  if (a0 > end) a0 = end;
+  int64_t a1 = end & ~(int64_t)3;
+  if (a1 < a0) a1 = a0;
+  return QuadSplit{a0, a1};
+}
+
+__device__ __forceinline__ void tern_acc(float v, double& sum, double& sq, float& amax, uint32_t& nan) {
+  sum += (double)v;
+  sq += (double)v * (double)v;
+  if (v != v) nan = 1; else amax = fmaxf(amax, fabsf(v));
+}
+
+// workgroup reduction of a TernPartial in a fixed order (deterministic)
+__device__ __forceinline__ TernPartial block_tern_reduce(double sum, double sq, float amax, uint32_t nan) {
   __shared__ double sh_s[kQBlock / kWave], sh_q[kQBlock / kWave];
   __shared__ float sh_m[kQBlock / kWave];
   __shared__ uint32_t sh_n[kQBlock / kWave];
@@ -158,77 +401,141 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh_s[w] = sum; sh_q[w] = sq; sh_m[w] = amax; sh_n[w] = nan; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    TernPartial p{0.0, 0.0, 0.f, 0u};
-    for (int j = 0; j < kQBlock / kWave; ++j) {
-      p.sum += sh_s[j]; p.sq += sh_q[j]; p.amax = fmaxf(p.amax, sh_m[j]); p.nan |= sh_n[j];
-    }
-    part[unit] = p;
+  TernPartial p{0.0, 0.0, 0.f, 0u};
+  for (int j = 0; j < kQBlock / kWave; ++j) {
+    p.sum += sh_s[j]; p.sq += sh_q[j]; p.amax = fmaxf(p.amax, sh_m[j]); p.nan |= sh_n[j];
   }
+  return p;
 }
 
-__device__ __forceinline__ void tern_scale(const TernPartial* part, int64_t u0, int64_t u1, int64_t n,
-                                           const float* clip_in, int s, float* scalar) {
+__global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __restrict__ x,
+                                                            const int64_t* __restrict__ seg_off,
+                                                            const int64_t* __restrict__ unit_off, int nseg,
+                                                            TernPartial* __restrict__ part) {
+  __shared__ SegTables tab;
+  const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
+  const int64_t unit = blockIdx.x;
+  const int s = find_seg(sv.sub, nseg, unit);
+  const int64_t base = sv.seg[s] + (unit - sv.sub[s]) * kTernUnit;
+  const int64_t end = min(base + (int64_t)kTernUnit, sv.seg[s + 1]);
+  const QuadSplit qs = quad_split(base, end);
   double sum = 0.0, sq = 0.0;
   float amax = 0.f;
   uint32_t nan = 0;
-  for (int64_t j = u0; j < u1; ++j) {
-    sum += part[j].sum; sq += part[j].sq; amax = fmaxf(amax, part[j].amax); nan |= part[j].nan;
+  const int t = threadIdx.x;
+  if (base + t < qs.a0) tern_acc(x[base + t], sum, sq, amax, nan);
+  if (qs.a1 + t < end) tern_acc(x[qs.a1 + t], sum, sq, amax, nan);
+  const f4v* xq = reinterpret_cast<const f4v*>(x + qs.a0);
+  const int64_t nq = (qs.a1 - qs.a0) >> 2;
+#pragma unroll 4
+  for (int64_t j = t; j < nq; j += kQBlock) {
+    const f4v v = __builtin_nontemporal_load(xq + j);
+    tern_acc(v.x, sum, sq, amax, nan);
+    tern_acc(v.y, sum, sq, amax, nan);
+    tern_acc(v.z, sum, sq, amax, nan);
+    tern_acc(v.w, sum, sq, amax, nan);
   }
-  float c;
-  if (clip_in) {
-    c = clip_in[s];
-  } else {
-    const double mean = sum / (double)n;
-    double var = sq / (double)n - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float stdf = (float)sqrt(var);
-    c = (float)(2.5 * (double)stdf);
-  }
-  *scalar = nan ? __int_as_float(0x7FC00000) : fminf(amax, c);
+  const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
+  if (threadIdx.x == 0) part[unit] = p;
 }
 
 __global__ __launch_bounds__(kQBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
     int nseg, const TernPartial* __restrict__ part, const float* __restrict__ clip_in,
     const float* __restrict__ u, uint64_t seed, int8_t* __restrict__ codes, float* __restrict__ scalars) {
+  __shared__ SegTables tab;
+  const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
   const int64_t unit = blockIdx.x;
-  const int s = find_seg(unit_off, nseg, unit);
-  __shared__ float s_scalar, s_clip;
-  if (threadIdx.x == 0) {
-    float sc;
-    tern_scale(part, unit_off[s], unit_off[s + 1], seg_off[s + 1] - seg_off[s], clip_in, s, &sc);
-    s_scalar = sc;
-    if (unit == unit_off[s]) scalars[s] = sc;
-    // clamp bound: the injected / derived c (scalar = min(max|x|, c))
-    if (clip_in) {
-      s_clip = clip_in[s];
-    } else {
-      double sum = 0.0, sq = 0.0;
-      for (int64_t j = unit_off[s]; j < unit_off[s + 1]; ++j) { sum += part[j].sum; sq += part[j].sq; }
-      const double nn = (double)(seg_off[s + 1] - seg_off[s]);
-      const double mean = sum / nn;
-      double var = sq / nn - mean * mean;
-      if (var < 0.0) var = 0.0;
-      s_clip = (float)(2.5 * (double)(float)sqrt(var));
-    }
+  const int s = find_seg(sv.sub, nseg, unit);
+  const int64_t base = sv.seg[s] + (unit - sv.sub[s]) * kTernUnit;
+  const int64_t end = min(base + (int64_t)kTernUnit, sv.seg[s + 1]);
+  const QuadSplit qs = quad_split(base, end);
+  const int t = threadIdx.x;
+  const int64_t nq = (qs.a1 - qs.a0) >> 2;
+  // the unit's quads are loaded before the scale is known (their latency overlaps the reduction)
+  constexpr int kPer = kTernUnit / 4 / kQBlock;
+  f4v xv[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t j = t + (int64_t)k * kQBlock;
+    const int64_t jc = j < nq ? j : 0;
+    if (nq > 0) xv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + qs.a0) + jc);
   }
-  __syncthreads();
-  const float scalar = s_scalar, c = s_clip;
-  const int64_t base = seg_off[s] + (unit - unit_off[s]) * kTernUnit;
-  const int64_t end = min(base + (int64_t)kTernUnit, seg_off[s + 1]);
-  for (int64_t i = base + threadIdx.x; i < end; i += kQBlock) {
-    const float xv = x[i];
+  // the segment's statistics from its units' partials, in a fixed order
+  double sum = 0.0, sq = 0.0;
+  float amax = 0.f;
+  uint32_t nan = 0;
+  for (int64_t j = sv.sub[s] + threadIdx.x; j < sv.sub[s + 1]; j += kQBlock) {
+    const TernPartial pj = part[j];
+    sum += pj.sum; sq += pj.sq; amax = fmaxf(amax, pj.amax); nan |= pj.nan;
+  }
+  const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
+  float c;
+  if (clip_in) {
+    c = clip_in[s];
+  } else {
+    const double nn = (double)(sv.seg[s + 1] - sv.seg[s]);
+    const double mean = p.sum / nn;
+    double var = p.sq / nn - mean * mean;
+    if (var < 0.0) var = 0.0;
+    c = (float)(2.5 * (double)(float)sqrt(var));
+  }
+  const float scalar = p.nan ? __int_as_float(0x7FC00000) : fminf(p.amax, c);
+  if (threadIdx.x == 0 && unit == sv.sub[s]) scalars[s] = scalar;
+
+  auto enc = [&](float xv, float ui) -> int8_t {
     const float cl = fminf(fmaxf(xv, -c), c);
     const float ab = fabsf(cl);
-    const float ui = u ? u[i] : uniform01(seed, (uint64_t)i);
     const float rnd = ui * scalar;
     int8_t code = 0;
     if (!(rnd >= ab)) {
       const float sg = cl > 0.f ? scalar : (cl < 0.f ? -scalar : 0.f);
       code = sg > 0.f ? 1 : (sg < 0.f ? -1 : 0);
     }
-    codes[i] = code;
+    return code;
+  };
+  if (base + t < qs.a0) {
+    const int64_t i = base + t;
+    codes[i] = enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i));
+  }
+  if (qs.a1 + t < end) {
+    const int64_t i = qs.a1 + t;
+    codes[i] = enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i));
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t j = t + (int64_t)k * kQBlock;
+    if (j >= nq) break;
+    const int64_t i = qs.a0 + 4 * j;
+    const f4v v = xv[k];
+    f4v uu;
+    if (u) {
+      uu = *reinterpret_cast<const f4v*>(u + i);
+    } else {
+      uu.x = uniform01(seed, (uint64_t)i);
+      uu.y = uniform01(seed, (uint64_t)i + 1);
+      uu.z = uniform01(seed, (uint64_t)i + 2);
+      uu.w = uniform01(seed, (uint64_t)i + 3);
+    }
+    const uint32_t w = (uint32_t)(uint8_t)enc(v.x, uu.x) | ((uint32_t)(uint8_t)enc(v.y, uu.y) << 8) |
+                       ((uint32_t)(uint8_t)enc(v.z, uu.z) << 16) | ((uint32_t)(uint8_t)enc(v.w, uu.w) << 24);
+    *reinterpret_cast<uint32_t*>(codes + i) = w;
+  }
+}
+
+__device__ __attribute__((noinline)) void tern_decode_slow(const int8_t* __restrict__ codes,
+                                                           const float* __restrict__ scalars, int64_t code_stride,
+                                                           int64_t scal_stride, int world, const int64_t* seg,
+                                                           int nseg, int64_t i0, int64_t i1, float divisor,
+                                                           int aggregate, float* __restrict__ out) {
+  for (int64_t i = i0; i < i1; ++i) {
+    const int sj = find_seg(seg, nseg, i);
+    float a = 0.f;
+    for (int w = 0; w < world; ++w) {
+      const float d = (float)codes[w * code_stride + i] * scalars[w * scal_stride + sj];
+      a = (aggregate || w > 0) ? a + d : d;
+    }
+    out[i] = divisor == 1.0f ? a : a / divisor;
   }
 }
 
@@ -237,15 +544,55 @@ __global__ __launch_bounds__(kQBlock) void tern_decode_kernel(const int8_t* __re
                                                              int64_t code_stride, int64_t scal_stride,
                                                              int world, const int64_t* __restrict__ seg_off,
                                                              int nseg, int64_t n, float divisor, int aggregate,
-                                                             float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock) {
-    const int s = find_seg(seg_off, nseg, i);
-    float acc = 0.f;
-    for (int w = 0; w < world; ++w) {
-      const float d = (float)codes[w * code_stride + i] * scalars[w * scal_stride + s];
-      acc = (aggregate || w > 0) ? acc + d : d;
+                                                             int vec, float* __restrict__ out) {
+  __shared__ SegTables tab;
+  const SegView sv = stage_tables(tab, seg_off, nullptr, nseg);
+  int64_t lo, hi;
+  block_range(n, kDecRound, lo, hi);
+  int s = lo < hi ? find_seg(sv.seg, nseg, lo + 4 * threadIdx.x < hi ? lo + 4 * threadIdx.x : lo) : 0;
+  for (int64_t r0 = lo; r0 < hi; r0 += kDecRound) {
+    int64_t e[kDecQuads];
+    int sk[kDecQuads];
+    bool fast[kDecQuads];
+#pragma unroll
+    for (int k = 0; k < kDecQuads; ++k) {
+      e[k] = r0 + (int64_t)k * kQBlock * 4 + 4 * threadIdx.x;
+      s = seg_advance(sv.seg, nseg, s, e[k] < hi ? e[k] : hi - 1);
+      sk[k] = s;
+      fast[k] = e[k] + 3 < hi && e[k] + 3 < sv.seg[s + 1];
     }
-    out[i] = divisor == 1.0f ? acc : acc / divisor;
+    float acc[kDecQuads][4] = {};
+    for (int w = 0; w < world; ++w) {
+      float c[kDecQuads][4], sc[kDecQuads];
+#pragma unroll
+      for (int k = 0; k < kDecQuads; ++k) {
+        if (fast[k]) {
+          load_codes4(codes + w * code_stride + e[k], vec != 0, c[k]);
+          sc[k] = scalars[w * scal_stride + sk[k]];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kDecQuads; ++k) {
+        if (!fast[k]) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = c[k][j] * sc[k];
+          acc[k][j] = (aggregate || w > 0) ? acc[k][j] + d : d;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDecQuads; ++k) {
+      if (fast[k]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k][j] = divisor == 1.0f ? acc[k][j] : acc[k][j] / divisor;
+        __builtin_nontemporal_store(f4v{acc[k][0], acc[k][1], acc[k][2], acc[k][3]},
+                                    reinterpret_cast<f4v*>(out + e[k]));
+      } else {
+        tern_decode_slow(codes, scalars, code_stride, scal_stride, world, sv.seg, nseg, e[k], min(e[k] + 4, hi),
+                         divisor, aggregate, out);
+      }
+    }
   }
 }
 
@@ -343,7 +690,7 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
                 "grace_qsgd_compress: bad arguments");
   if (nbuckets == 0) return GRACE_OK;
   GRACE_REQUIRE(variant == 0 || (variant == 1 && quantum_num < 128), "grace_qsgd_compress: bad variant");
-  const unsigned grid = stream_grid(nbuckets, kQBlock / 64, 4096);
+  const unsigned grid = stream_grid(nbuckets, 2 * kQBlock / 32, 4096);
   hipStream_t st = as_stream(stream);
   if (variant == 1) {
     qsgd_encode_kernel<int8_t, 1><<<grid, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, nbuckets, bucket_size,
@@ -370,24 +717,25 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
   GRACE_REQUIRE(codes && norms && seg_off && bkt_off && out && world >= 1 && nseg >= 1 && n >= 0,
                 "grace_qsgd_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
-  const unsigned grid = stream_grid(n, kQBlock, 4096);
+  const unsigned grid = stream_grid((n + kDecRound - 1) / kDecRound, 1, 4096);
   hipStream_t st = as_stream(stream);
+  // 4 codes per load: one 4-B (int8) / 8-B (fp16) load when every rank's slice is aligned
+  const int64_t cbytes = variant == 0 && quantum_num >= 128 ? 2 : 1;
+  const int vec = (code_stride % 4 == 0) && ((uintptr_t)codes % (4 * cbytes) == 0);
+#define GRACE_QDEC(CT, V, B)                                                                         \
+  qsgd_decode_kernel<CT, V, B><<<grid, kQBlock, 0, st>>>(reinterpret_cast<const CT*>(codes), norms,  \
+                                                         code_stride, norm_stride, world, seg_off,   \
+                                                         bkt_off, nseg, n, bucket_size,              \
+                                                         (float)quantum_num, divisor, aggregate, vec, out)
+  const bool b128 = bucket_size == 128;
   if (variant == 1) {
-    qsgd_decode_kernel<int8_t, 1><<<grid, kQBlock, 0, st>>>(reinterpret_cast<const int8_t*>(codes), norms,
-                                                           code_stride, norm_stride, world, seg_off, bkt_off,
-                                                           nseg, n, bucket_size, (float)quantum_num, divisor,
-                                                           aggregate, out);
+    if (b128) GRACE_QDEC(int8_t, 1, true); else GRACE_QDEC(int8_t, 1, false);
   } else if (quantum_num < 128) {
-    qsgd_decode_kernel<int8_t, 0><<<grid, kQBlock, 0, st>>>(reinterpret_cast<const int8_t*>(codes), norms,
-                                                           code_stride, norm_stride, world, seg_off, bkt_off,
-                                                           nseg, n, bucket_size, (float)quantum_num, divisor,
-                                                           aggregate, out);
+    if (b128) GRACE_QDEC(int8_t, 0, true); else GRACE_QDEC(int8_t, 0, false);
   } else {
-    qsgd_decode_kernel<__half, 0><<<grid, kQBlock, 0, st>>>(reinterpret_cast<const __half*>(codes), norms,
-                                                           code_stride, norm_stride, world, seg_off, bkt_off,
-                                                           nseg, n, bucket_size, (float)quantum_num, divisor,
-                                                           aggregate, out);
+    if (b128) GRACE_QDEC(__half, 0, true); else GRACE_QDEC(__half, 0, false);
   }
+#undef GRACE_QDEC
   GRACE_CHECK_LAUNCH("grace_qsgd_decompress");
   return GRACE_OK;
 }
@@ -417,8 +765,9 @@ grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scala
   GRACE_REQUIRE(codes && scalars && seg_off && out && world >= 1 && nseg >= 1 && n >= 0,
                 "grace_terngrad_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
-  tern_decode_kernel<<<stream_grid(n, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      codes, scalars, code_stride, scal_stride, world, seg_off, nseg, n, divisor, aggregate, out);
+  const int vec = (code_stride % 4 == 0) && ((uintptr_t)codes % 4 == 0);
+  tern_decode_kernel<<<stream_grid((n + kDecRound - 1) / kDecRound, 1, 4096), kQBlock, 0, as_stream(stream)>>>(
+      codes, scalars, code_stride, scal_stride, world, seg_off, nseg, n, divisor, aggregate, vec, out);
   GRACE_CHECK_LAUNCH("grace_terngrad_decompress");
   return GRACE_OK;
 }

@@ -45,9 +45,12 @@ class PowerSGDCompressor(Compressor):
         r = min(n, m, self.rank)
         if self.use_memory and name in self.q_memory:
             q = self.q_memory[name]
-        else:
+        elif self.rng == "torch_cpu":
             q = self._normal(m, r, matrix.device, name)
             orthogonalize(q)
+        else:   # device draw + orthogonalisation fused in one launch
+            self._step += 1
+            q = ops.normal_orthogonal((m, r), ops.step_seed("powersgd-q", name, self._step), matrix.device)
         p = ops.powersgd_p(matrix, q)
         if self.world_size > 1 or (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
             dist.all_reduce(p)

@@ -427,7 +427,8 @@ def powersgd_p(M2d, q):
     n, m = M2d.shape
     r = q.shape[1]
     P = torch.empty(n, r, dtype=F32, device=M2d.device)
-    _lib.call("grace_powersgd_p", _p(M2d), n, m, _p(require_dev(q)), r, _p(P), _stream())
+    ws = workspace("powersgd", _lib.query("grace_powersgd_workspace_bytes", n, m, r), M2d.device)
+    _lib.call("grace_powersgd_p", _p(M2d), n, m, _p(require_dev(q)), r, _p(P), _p(ws), _stream())
     return P
 
 
@@ -443,6 +444,13 @@ def powersgd_qt(M2d, P):
 def orthogonalize_(A):
     A = require_dev(A)
     _lib.call("grace_orthogonalize", _p(A), A.shape[0], A.shape[1], _stream())
+    return A
+
+
+def normal_orthogonal(shape, seed, device):
+    """orthogonalize(normal draws of `shape`) in one launch (draws as ops.normal)."""
+    A = torch.empty(shape, dtype=F32, device=device)
+    _lib.call("grace_normal_orthogonal", _p(A), shape[0], shape[1], int(seed) & (2 ** 64 - 1), _stream())
     return A
 
 

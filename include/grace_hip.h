@@ -189,14 +189,17 @@ grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, 
 
 /* ---------------------------------------------------------------------------------- PowerSGD */
 /* PowerSGD (powersgd.py:30-65) on M[n x m] row-major, rank r <= 16, f32 MFMA contractions.
- * P = M q;  Q = M^T P (ws = grace_powersgd_workspace_bytes);  orthogonalize in place;
+ * P = M q and Q = M^T P share one workspace (grace_powersgd_workspace_bytes, zeroed once at
+ * allocation, left zeroed by every call);  orthogonalize in place (Cholesky-QR, f64);
  * out = P Q^T and/or residual = M - P Q^T (memory/powersgd.py:32-37) in one pass. */
 grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
-                                void* stream);
+                                void* ws, void* stream);
 size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r);
 grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const float* P, int32_t r, float* Q,
                                  void* ws, void* stream);
 grace_status_t grace_orthogonalize(float* A, int64_t n, int32_t r, void* stream);
+/* q = orthogonalize(normal draws) in one launch (powersgd.py:41-43); same draws as grace_normal_fill */
+grace_status_t grace_normal_orthogonal(float* A, int64_t n, int32_t r, uint64_t seed, void* stream);
 grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, int64_t m, int32_t r, float* out,
                                     const float* M, float* residual, void* stream);
 /* standard normal fill (q draws, powersgd.py:41 / memory/powersgd.py:27), device generator */

@@ -97,3 +97,22 @@ def test_one_dim_passthrough():
     x = _t(np.arange(10, dtype=np.float32))
     payload, ctx = comp.compress(x, "b")
     assert ctx is None and comp.decompress(payload, ctx) is x
+
+
+@pytest.mark.parametrize("n,r", [(4096, 4), (5000, 3), (100, 1), (9000, 8), (300, 16)])
+def test_orthogonalize_shapes_and_fused_draw(n, r):
+    """Register-resident (n <= 4096) and chunked (taller) orthogonalisation against a float64
+    MGS, and the fused draw == draw then orthogonalise."""
+    rng = np.random.default_rng(n + r)
+    a = rng.standard_normal((n, r)).astype(np.float32)
+    out = _np(ops.orthogonalize_(_t(a)))
+    exp = a.astype(np.float64)
+    for i in range(r):
+        exp[:, i] /= np.sqrt(np.sum(exp[:, i] ** 2))
+        if i + 1 < r:
+            exp[:, i + 1:] -= np.sum(exp[:, i:i + 1] * exp[:, i + 1:], axis=0) * exp[:, i:i + 1]
+    assert np.allclose(out, exp, rtol=1e-4, atol=1e-5)
+    fused = _np(ops.normal_orthogonal((n, r), 77, "cuda"))
+    ref = _np(ops.orthogonalize_(ops.normal((n, r), 77, "cuda")))
+    assert np.allclose(fused, ref, rtol=1e-5, atol=1e-6)
+    assert np.allclose(fused.T.astype(np.float64) @ fused, np.eye(r), atol=1e-4)

@@ -170,3 +170,40 @@ def test_allgather_world1_step(cls):
     # stochastic codecs are unbiased: the mean error is small against the spread of x
     bias = abs(float((out - x).mean()))
     assert bias < 0.1 * float(x.std())
+
+
+@pytest.mark.parametrize("q,bucket", [(127, 8), (127, 100), (127, 128), (255, 128), (127, 256), (200, 37)])
+def test_segmented_qsgd_bucket_and_code_variants(q, bucket):
+    """Segmented encode/decode at odd bucket sizes, fp16 codewords (q >= 128) and ragged segment
+    offsets (exercises the 16-element decode fast path, its bucket split and the slow path)."""
+    rng = np.random.default_rng(5)
+    sizes = [37, 1, 4099, 16, 15, 128 * 7 + 3, 2048, 1000]
+    xs = [(rng.standard_normal(n) * 0.01).astype(np.float32) for n in sizes]
+    flat = np.concatenate(xs)
+    u = rng.random(flat.size, dtype=np.float32)
+    codes, norms = ops.qsgd_compress(_t(flat), q, bucket, sizes=sizes, u=_t(u))
+    dec = _np(ops.qsgd_decompress(codes, norms, q, bucket, flat.size, sizes=sizes))
+    norms_np = _np(norms)
+    off = noff = 0
+    for n, x in zip(sizes, xs):
+        nb = -(-n // bucket)
+        exp_c, _ = O.qsgd_compress(x, u[off:off + n], q, bucket, norms=norms_np[noff:noff + nb])
+        assert same_bits(_np(codes[off:off + n]), exp_c), (n, q, bucket)
+        exp_d = O.qsgd_decode(exp_c, norms_np[noff:noff + nb], q, bucket, n)
+        assert same_bits(dec[off:off + n], exp_d), (n, q, bucket)
+        off += n
+        noff += nb
+
+
+def test_segmented_terngrad_decode_world3_ragged():
+    """W = 3 aggregate over ragged segments with a code stride that is not 16-B aligned."""
+    rng = np.random.default_rng(6)
+    sizes = [5, 33, 4096 + 7, 1, 300]
+    n = sum(sizes)
+    codes = rng.integers(-1, 2, size=3 * n, dtype=np.int8)
+    scal = rng.random(3 * len(sizes), dtype=np.float32)
+    out = _np(ops.terngrad_decompress(_t(codes), _t(scal), n, sizes=sizes, world=3, aggregate=True, divisor=3.0))
+    seg = np.repeat(np.arange(len(sizes)), sizes)
+    decs = [codes[w * n:(w + 1) * n].astype(np.float32) * scal[w * len(sizes) + seg] for w in range(3)]
+    exp = (O.python_sum(decs) / np.float32(3)).astype(np.float32)
+    assert same_bits(out, exp)
