@@ -17,6 +17,9 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   terngrad   TernGrad, same set (configs[2])
   topk_e2e   the headline step with the bucket arriving from pinned host memory (H2D) and the
              aggregated dense gradient returned to it (D2H): the PCIe-inclusive rate in DESIGN.md
+  topk_sharded  ONE 256 MiB bucket sharded over the N ranks, top-k 0.1 % + residual, exact global
+             selection (histogram exchange + boundary lists + payload allgather), replicated dense
+             decode (configs[4]); value = 4n / step time (strong scaling: the bucket is fixed)
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
 
 Launch: ``python bench.py`` (N=1) or
@@ -45,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
-                    choices=["topk", "topk_e2e", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
+                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -100,7 +103,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
     line = run(args, world, rank, dev)
     if rank == 0:
@@ -227,6 +230,38 @@ def bench_topk_e2e(args, world, rank, dev):
     line["config"] = {"workload": "pinned host bucket -> H2D -> Allgather(TopK 1%, ResidualMemory).step -> D2H",
                       "numel": n, "h2d_plus_d2h_ms": round(t_copy / args.steps * 1e3, 4)}
     line["roofline"] = None
+    return line
+
+
+def bench_topk_sharded(args, world, rank, dev):
+    from grace_amd.dist.sharded import ShardedTopK
+    n = args.numel
+    ratio = 0.001 if args.ratio == 0.01 else args.ratio
+    sizes = [n // world + (1 if r < n % world else 0) for r in range(world)]
+    m = sizes[rank]
+    eng = ShardedTopK(ratio)
+    gen = torch.Generator(device=dev)
+    shards = []
+    for j in range(args.buffers):
+        gen.manual_seed(1000 * rank + j + 1)
+        shards.append(torch.randn(m, device=dev, generator=gen))
+    for j in range(args.buffers):
+        eng.step(shards[j], f"b{j}")
+    elapsed = timed(lambda i: eng.step(shards[i % args.buffers], f"b{i % args.buffers}"), args.steps, args.warmup,
+                    world, dev)
+    t = elapsed / args.steps
+    k = max(1, int(n * ratio))
+    line = base_line(args, 1, elapsed, 4.0 * n,
+                     metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket sharded, top-k 0.1 %")
+    line["n_gpus"] = world
+    line["scaling"] = "strong"
+    line["config"] = {"workload": f"ShardedTopK(0.1 %) + residual, one {4 * n >> 20} MiB bucket over {world} "
+                                  "rank(s), replicated dense decode (BASELINE configs[4])",
+                      "numel": n, "k": k, "shard": m, "parallelism": f"{world} contiguous shards"}
+    per_gpu = 12.0 * m + 8.0 * k + 4.0 * n      # shard encode + replicated decode
+    line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_gpu": per_gpu}
     return line
 
 

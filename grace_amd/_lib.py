@@ -42,6 +42,15 @@ SIGNATURES = {
     "grace_topk_workspace_bytes": (SZ, [I64, I64]),
     "grace_topk_compress": (ST, [P, I64, I64, P, P, P, SZ, P]),
     "grace_topk_residual_step": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, SZ, P]),
+    "grace_topk_shard_xs_words": (SZ, []),
+    "grace_topk_shard_xh_words": (SZ, []),
+    "grace_topk_shard_sample": (ST, [P, P, I32, F32, F32, I64, I64, P, P]),
+    "grace_topk_shard_main": (ST, [P, P, I32, F32, F32, I64, I64, I64, I64, I64, P, P, P, SZ, P, P, P]),
+    "grace_topk_shard_route": (ST, [P, I64, I64, I64, I32, P, P, P, SZ, P, P]),
+    "grace_topk_shard_boundary": (ST, [P, I64, I64, I64, P, I32, I64, ctypes.c_uint32, P, P, I64, P, SZ, P]),
+    "grace_topk_shard_take": (ST, [P, P, I64, P, I64, I64, P, P, I64, P]),
+    "grace_topk_shard_read": (ST, [P, P, P]),
+    "grace_sparse_scatter_range": (ST, [P, P, I64, I64, I32, I64, I64, P, P]),
     "grace_sparse_decode": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_decode_i64": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),

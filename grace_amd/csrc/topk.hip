@@ -83,6 +83,7 @@ static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 #endif
 #define STAMP(ctlp, slot) STAMP_IF(blockIdx.x == 0, ctlp, slot)
 
+constexpr int kXcnt = 8;                                   // sharded exchange counters
 constexpr int kSampleMax = 131072;                         // stratified sample size
 constexpr int kSampleBlock = 1024;
 constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
@@ -100,6 +101,7 @@ struct TopkWs {
   int2* cand;
   int2* bnd;
   int64_t cap;
+  uint32_t* xcnt;      // sharded mode: [n_sure, n_cand] of this rank, exchanged after the main pass
 };
 
 static inline int64_t topk_cap(int64_t n, int64_t k) {
@@ -124,6 +126,7 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   w.cand = reinterpret_cast<int2*>(p);
   p += align256(sizeof(int2) * w.cap);
   w.bnd = reinterpret_cast<int2*>(p);
+  w.xcnt = nullptr;
   return w;
 }
 
@@ -241,6 +244,18 @@ __device__ __forceinline__ uint64_t comp_key(uint32_t key, uint32_t idx) {
   return ((uint64_t)key << 32) | (uint64_t)(0xFFFFFFFFu - idx);
 }
 
+// Boundary-list entries cross workgroups (and XCDs, whose L2s are not coherent with each other):
+// they are written with agent-scope (sc1, write-through) stores and read back with agent-scope
+// loads, so the arrival protocol needs no L2 writeback / invalidate fences.
+__device__ __forceinline__ void st_agent_i2(int2* p, int2 v) {
+  const uint64_t u = (uint64_t)(uint32_t)v.x | ((uint64_t)(uint32_t)v.y << 32);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int2 ld_agent_i2(const int2* p) {
+  const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_int2((int)(uint32_t)u, (int)(uint32_t)(u >> 32));
+}
+
 // Exact single-workgroup radix select: returns T such that exactly `need` items of src have
 // composite >= T (composites are unique).  6 passes of 11/11/11/11/11/9 bits.
 template <typename Src>
@@ -313,6 +328,7 @@ struct StepArgs {
   float* out;          // dense output (kDenseFused)
   int64_t sample_n;    // stratified sample size (<= kSampleMax)
   int64_t stratum;     // n / sample_n
+  int64_t idx_base;    // sharded mode: global index of this shard's element 0 (payload indices)
 };
 
 template <bool HAS_RES>
@@ -418,6 +434,7 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
   // re-zero the state the next kernels accumulate into
   for (int b = tid; b < kHistBins; b += kSelBlock) { w.hist[b * kHistStride] = 0; w.cursor[b * kCursorStride] = 0; }
   if (tid < (int)(sizeof(TopkCtl) / 4)) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
+  if (w.xcnt && tid < kXcnt) w.xcnt[tid] = 0u;
   __syncthreads();
   if (tid == 0) {
     // sure = key > hi: round up to the top of the bin (fewer sure); candidates start at the bottom
@@ -580,19 +597,19 @@ __device__ __forceinline__ void main_chunk(const StepArgs& a, const TopkWs& w, M
           const float tv = comp4(t[u], j);
           if ((msure >> b) & 1u) {
             if (ps < (uint32_t)kStage) {
-              sm.sure[ps] = make_int2((int)i, (int)f2u(tv));
+              sm.sure[ps] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
             } else {
               const uint32_t gp = gs0 + (ps - lim_s);
-              if (gp < (uint32_t)a.k) { a.vals[gp] = tv; a.idx[gp] = (int32_t)i; }
+              if (gp < (uint32_t)a.k) { a.vals[gp] = tv; a.idx[gp] = (int32_t)(i + a.idx_base); }
             }
             ++ps;
           }
           if ((mcand >> b) & 1u) {
             if (pc < (uint32_t)kStage) {
-              sm.cand[pc] = make_int2((int)i, (int)f2u(tv));
+              sm.cand[pc] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
             } else {
               const uint32_t gp = gc0 + (pc - lim_c);
-              if (gp < (uint32_t)w.cap) w.cand[gp] = make_int2((int)i, (int)f2u(tv));
+              if (gp < (uint32_t)w.cap) w.cand[gp] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
             }
             ++pc;
           }
@@ -622,6 +639,11 @@ __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   if (tid == 0) {
     sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
     sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+  }
+  if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
+    const uint32_t all = sm.cnt[0];
+    if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
+    if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
   }
   __syncthreads();
   for (uint32_t j = tid; j < ns; j += kMainBlock) {
@@ -714,7 +736,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
       int2 e = make_int2(0, 0);
       uint64_t me = 0;
       if (j < (int)nb) {
-        e = w.bnd[j];
+        e = ld_agent_i2(w.bnd + j);
         me = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
         s_comp[j] = me;
       }
@@ -728,14 +750,14 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
     }
     const int2* bnd = w.bnd;
     auto src = [bnd](int64_t j) {
-      const int2 e = bnd[j];
+      const int2 e = ld_agent_i2(bnd + j);
       return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
     };
     const uint64_t T = block_select_comp(src, nb, need, hist, s_w, s_res);
     if (threadIdx.x == 0) *s_pos = 0;
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += kSelBlock) {
-      const int2 e = bnd[j];
+      const int2 e = ld_agent_i2(bnd + j);
       if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) {
         const uint32_t p = atomicAdd(s_pos, 1u);
         emit<MODE>(a, pos0 + p, e.x, u2f((uint32_t)e.y));
@@ -836,25 +858,17 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
             if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
             ++ps;
           }
-          if ((fb >> u) & 1u) w.bnd[pb++] = e[u];
+          if ((fb >> u) & 1u) st_agent_i2(w.bnd + pb++, e[u]);
         }
       }
     }
   }
-  // arrival: every wave's stores complete, one release + ticket per workgroup; the last one
-  // acquires and finishes the boundary bin
+  // arrival: every wave's (write-through) boundary stores complete, then one ticket per
+  // workgroup; the last one finishes the boundary bin
   STAMP(w.ctl, 10);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
+  if (t == 0) s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
   STAMP_IF(true, w.ctl, 11);
@@ -929,6 +943,197 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_finalize");
   return GRACE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sharded top-k (BASELINE configs[4]): one bucket split into W contiguous shards,
+// one per rank; the union of the ranks' payloads is exactly the single-GPU top-k of the whole
+// bucket (same (|t| desc, global index asc) rule).  Per step, driven by grace_amd/dist/sharded.py:
+//   sample (local, into the exchange histogram xs) -> all_reduce(xs) -> select (global bracket)
+//   -> main (local RES pass, global indices, local histogram + counts into xh) -> all_gather(xh)
+//   -> host: boundary bin B, need, list capacities -> route (above-B to the payload, bin-B to a
+//   list) -> all_gather(lists) -> boundary (exact global selection of `need` in bin B; this
+//   rank's winners join its payload, payload padded with idx -1) -> all_gather(payloads) ->
+//   scatter-range decode.
+// The residual buffer holds t for every element after the main pass (RES mode), which is what
+// the exact fallback (bracket miss: all_gather t, single-GPU select) starts from.
+
+// route: local candidates above bin B -> payload (after the local sure entries), bin B -> bsend
+// list [count, pad, entries...]; the residual of every payload entry (sure + above) is zeroed.
+__global__ __launch_bounds__(kSelBlock) void topk_shard_route(StepArgs a, TopkWs w, int B, int64_t* bsend) {
+  const TopkCtl c = *w.ctl;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int64_t base = a.idx_base;
+  for (uint32_t j = blockIdx.x * kSelBlock + t; j < c.n_sure; j += gridDim.x * kSelBlock) {
+    const float v = a.vals[j];
+    a.r[a.idx[j] - base] = v - v;
+  }
+  int2* blist = reinterpret_cast<int2*>(bsend + 1);
+  for (uint32_t j0 = blockIdx.x * kSelBlock; j0 < c.n_cand; j0 += gridDim.x * kSelBlock) {
+    const uint32_t j = j0 + t;
+    int2 e = make_int2(0, 0);
+    int bin = -1;
+    if (j < c.n_cand) {
+      e = w.cand[j];
+      bin = (int)((abs_key(u2f((uint32_t)e.y)) - c.thr_lo) >> c.shift);
+    }
+    const uint64_t ma = __ballot(bin > B), mb = __ballot(bin == B);
+    uint32_t ba = 0, bb = 0;
+    if (lane == 0) {
+      if (ma) ba = atomicAdd(&w.ctl->n_sel, (uint32_t)__popcll(ma));
+      if (mb) bb = atomicAdd(&w.ctl->n_bacc, (uint32_t)__popcll(mb));
+    }
+    ba = __shfl(ba, 0, 64);
+    bb = __shfl(bb, 0, 64);
+    if (bin > B) {
+      const uint32_t pos = c.n_sure + ba + lane_rank(ma);
+      const float v = u2f((uint32_t)e.y);
+      a.vals[pos] = v;
+      a.idx[pos] = e.x;
+      a.r[e.x - base] = v - v;
+    } else if (bin == B) {
+      blist[bb + lane_rank(mb)] = e;
+    }
+  }
+  // the list count: written by the last workgroup to finish (ticket), after every entry
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t s_last;
+  if (t == 0) s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (s_last && t == 0) bsend[0] = (int64_t)__hip_atomic_load(&w.ctl->n_bacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// boundary: the W gathered bin-B lists (segment w at brecv + w * (cap_b + 1) int64 words: count,
+// then entries) hold every element of bin B; the `need` best by (|t| desc, index asc) are
+// selected exactly; this rank's winners are appended to its payload (residual zeroed), and the
+// payload [count, cap_p) is padded with idx -1.
+struct ShardList {
+  const int64_t* recv;
+  int64_t seg;          // words per rank segment
+  int world;
+  const uint32_t* off;  // LDS prefix offsets [world + 1]
+  __device__ int2 at(int64_t j) const {
+    int w = 0;
+    while (w + 1 < world && (int64_t)off[w + 1] <= j) ++w;
+    const int2* l = reinterpret_cast<const int2*>(recv + w * seg + 1);
+    return l[j - off[w]];
+  }
+};
+
+__global__ __launch_bounds__(kSelBlock) void topk_shard_boundary(StepArgs a, TopkWs w, const int64_t* brecv,
+                                                                int world, int64_t cap_b, uint32_t need,
+                                                                int64_t cap_p) {
+  __shared__ uint32_t s_off[65];
+  __shared__ uint64_t s_comp[kSelBlock];
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_pos;
+  const int t = threadIdx.x;
+  const int64_t seg = cap_b + 1;
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int q = 0; q < world; ++q) { s_off[q] = acc; acc += (uint32_t)brecv[q * seg]; }
+    s_off[world] = acc;
+    s_pos = w.ctl->n_sure + w.ctl->n_sel;
+  }
+  __syncthreads();
+  const uint32_t nb = s_off[world];
+  const ShardList L{brecv, seg, world, s_off};
+  const int64_t base = a.idx_base, m = a.n;
+  auto take = [&](int2 e) {
+    const int64_t gi = e.x;
+    if (gi >= base && gi < base + m) {
+      const uint32_t p = atomicAdd(&s_pos, 1u);
+      const float v = u2f((uint32_t)e.y);
+      a.vals[p] = v;
+      a.idx[p] = e.x;
+      a.r[gi - base] = v - v;
+    }
+  };
+  if (need > 0) {
+    if (nb <= (uint32_t)kSelBlock) {
+      int2 e = make_int2(0, 0);
+      uint64_t me = 0;
+      if (t < (int)nb) {
+        e = L.at(t);
+        me = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
+        s_comp[t] = me;
+      }
+      __syncthreads();
+      if (t < (int)nb) {
+        uint32_t rank = 0;
+        for (uint32_t q = 0; q < nb; ++q) rank += s_comp[q] > me;
+        if (rank < need) take(e);
+      }
+    } else {
+      auto src = [L](int64_t j) {
+        const int2 e = L.at(j);
+        return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
+      };
+      const uint64_t T = block_select_comp(src, nb, need, hist, s_w, s_res);
+      for (uint32_t j = t; j < nb; j += kSelBlock) {
+        const int2 e = L.at(j);
+        if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) take(e);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = s_pos;
+  for (int64_t j = cnt + t; j < cap_p; j += kSelBlock) {
+    a.vals[j] = 0.f;
+    a.idx[j] = -1;
+  }
+  if (t == 0) w.ctl->n_bnd = cnt;   // this rank's payload count (diagnostics)
+}
+
+// exact fallback: from the whole bucket's exact selection (vals_all / idx_all, k entries), take
+// this rank's entries in order into its payload, zero their residual, pad to cap_p with idx -1
+__global__ __launch_bounds__(kSelBlock) void topk_shard_take(const float* vals_all, const int32_t* idx_all,
+                                                            int64_t k, StepArgs a, int64_t cap_p) {
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  const int64_t base = a.idx_base, m = a.n;
+  uint32_t run = 0;
+  for (int64_t j0 = 0; j0 < k; j0 += kSelBlock) {
+    const int64_t j = j0 + threadIdx.x;
+    bool mine = false;
+    int32_t gi = 0;
+    float v = 0.f;
+    if (j < k) {
+      gi = idx_all[j];
+      v = vals_all[j];
+      mine = gi >= base && gi < base + m;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kSelBlock>(mine ? 1u : 0u, s_w, &tot);
+    if (mine && run + ex < (uint64_t)cap_p) {
+      a.vals[run + ex] = v;
+      a.idx[run + ex] = gi;
+      a.r[gi - base] = v - v;
+    }
+    run += tot;
+  }
+  for (int64_t j = run + threadIdx.x; j < cap_p; j += kSelBlock) {
+    a.vals[j] = 0.f;
+    a.idx[j] = -1;
+  }
+}
+
+// dense decode of gathered padded payloads (rank w's entries at vals/idx + w * stride, `per` of
+// them): out[idx - base] = 0 + v for base <= idx < base + len (idx -1 = padding); out must be
+// zero-filled first.  Indices are unique across ranks, so the order of the writes is irrelevant.
+__global__ void scatter_range_kernel(const float* __restrict__ vals, const int32_t* __restrict__ idx,
+                                     int64_t stride, int64_t per, int world, int64_t base, int64_t len,
+                                     float* __restrict__ out) {
+  const int64_t count = per * world;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < count;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = j / per, q = j - w * per;
+    const int64_t gi = idx[w * stride + q];
+    if (gi >= base && gi < base + len) out[gi - base] = 0.f + vals[w * stride + q];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1089,6 +1294,134 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
       GRACE_CHECK_LAUNCH("grace_sparse_aggregate");
     }
   }
+  return GRACE_OK;
+}
+
+
+size_t grace_topk_shard_xs_words(void) { return (size_t)kBracketBins; }
+size_t grace_topk_shard_xh_words(void) { return (size_t)(kHistBins + kXcnt); }
+
+static TopkWs shard_ws(void* ws, int64_t m, int64_t k, uint32_t* xs, uint32_t* xh) {
+  TopkWs w = carve(ws, m, k);
+  if (xs) w.shist = xs;
+  if (xh) {
+    w.hist = xh;
+    w.xcnt = xh + kHistBins;
+  }
+  return w;
+}
+
+grace_status_t grace_topk_shard_sample(const float* g, float* residual, int32_t has_residual, float beta,
+                                       float gamma, int64_t m, int64_t stratum, uint32_t* xs, void* stream) {
+  GRACE_REQUIRE(g && xs && m > 0 && stratum >= 1 && (!has_residual || residual),
+                "grace_topk_shard_sample: bad arguments");
+  StepArgs a{g, residual, beta, gamma, m, 1, nullptr, nullptr, nullptr};
+  a.stratum = stratum;
+  a.sample_n = m / stratum;
+  if (a.sample_n == 0) return GRACE_OK;
+  TopkWs w{};
+  w.shist = xs;
+  const unsigned grid = (unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock);
+  if (has_residual) topk_sample<true><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
+  else topk_sample<false><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
+  GRACE_CHECK_LAUNCH("grace_topk_shard_sample");
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t has_residual, float beta,
+                                     float gamma, int64_t m, int64_t idx_base, int64_t n_global, int64_t k,
+                                     int64_t sample_total, float* vals, int32_t* idx, void* ws, size_t ws_bytes_,
+                                     uint32_t* xs, uint32_t* xh, void* stream) {
+  GRACE_REQUIRE(g && residual && vals && idx && ws && xs && xh && m > 0 && k >= 1 && k <= n_global &&
+                    n_global < ((int64_t)1 << 31) && idx_base >= 0 && idx_base + m <= n_global &&
+                    sample_total >= 1,
+                "grace_topk_shard_main: bad arguments");
+  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_main: workspace too small");
+  hipStream_t s = as_stream(stream);
+  TopkWs w = shard_ws(ws, m, k, xs, xh);
+  StepArgs sel{g, residual, beta, gamma, n_global, k, vals, idx, nullptr};
+  sel.sample_n = sample_total;
+  topk_select<<<1, kSelBlock, 0, s>>>(sel, w);   // global bracket; re-zeroes xs, xh and the local state
+  GRACE_CHECK_LAUNCH("grace_topk_shard_main");
+  StepArgs a{g, residual, beta, gamma, m, k, vals, idx, nullptr};
+  a.idx_base = idx_base;
+  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual)) & 15u) == 0;
+  const unsigned nblk = (unsigned)((m + kMainChunk - 1) / kMainChunk);
+  {
+    TimerScope ts(s);
+    if (has_residual) {
+      if (vec) topk_main<true, kDenseRes, true><<<nblk, kMainBlock, 0, s>>>(a, w);
+      else topk_main<true, kDenseRes, false><<<nblk, kMainBlock, 0, s>>>(a, w);
+    } else {
+      if (vec) topk_main<false, kDenseRes, true><<<nblk, kMainBlock, 0, s>>>(a, w);
+      else topk_main<false, kDenseRes, false><<<nblk, kMainBlock, 0, s>>>(a, w);
+    }
+  }
+  GRACE_CHECK_LAUNCH("grace_topk_shard_main");
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_shard_route(float* residual, int64_t m, int64_t idx_base, int64_t k,
+                                      int32_t boundary_bin, float* vals, int32_t* idx, void* ws,
+                                      size_t ws_bytes_, int64_t* bsend, void* stream) {
+  GRACE_REQUIRE(residual && vals && idx && ws && bsend && m > 0 && k >= 1,
+                "grace_topk_shard_route: bad arguments");
+  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_route: workspace too small");
+  TopkWs w = carve(ws, m, k);
+  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
+  a.idx_base = idx_base;
+  topk_shard_route<<<kFinBlocks, kSelBlock, 0, as_stream(stream)>>>(a, w, boundary_bin, bsend);
+  GRACE_CHECK_LAUNCH("grace_topk_shard_route");
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_shard_boundary(float* residual, int64_t m, int64_t idx_base, int64_t k,
+                                         const int64_t* brecv, int32_t world, int64_t cap_b, uint32_t need,
+                                         float* vals, int32_t* idx, int64_t cap_p, void* ws, size_t ws_bytes_,
+                                         void* stream) {
+  GRACE_REQUIRE(residual && vals && idx && ws && brecv && m > 0 && world >= 1 && world <= 64 && cap_b >= 0 &&
+                    cap_p >= 0,
+                "grace_topk_shard_boundary: bad arguments");
+  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_boundary: workspace too small");
+  TopkWs w = carve(ws, m, k);
+  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
+  a.idx_base = idx_base;
+  topk_shard_boundary<<<1, kSelBlock, 0, as_stream(stream)>>>(a, w, brecv, world, cap_b, need, cap_p);
+  GRACE_CHECK_LAUNCH("grace_topk_shard_boundary");
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_shard_take(const float* vals_all, const int32_t* idx_all, int64_t k, float* residual,
+                                     int64_t m, int64_t idx_base, float* vals, int32_t* idx, int64_t cap_p,
+                                     void* stream) {
+  GRACE_REQUIRE(vals_all && idx_all && residual && vals && idx && k >= 1 && m > 0 && cap_p >= 0,
+                "grace_topk_shard_take: bad arguments");
+  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
+  a.idx_base = idx_base;
+  topk_shard_take<<<1, kSelBlock, 0, as_stream(stream)>>>(vals_all, idx_all, k, a, cap_p);
+  GRACE_CHECK_LAUNCH("grace_topk_shard_take");
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_shard_read(const void* ws, uint32_t* ctl_host, void* stream) {
+  GRACE_REQUIRE(ws && ctl_host, "grace_topk_shard_read: bad arguments");
+  hipError_t e = hipMemcpyAsync(ctl_host, ws, sizeof(TopkCtl), hipMemcpyDeviceToHost, as_stream(stream));
+  if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+  if (e != hipSuccess) {
+    set_error("grace_topk_shard_read", e);
+    return GRACE_ERR_HIP;
+  }
+  return GRACE_OK;
+}
+
+grace_status_t grace_sparse_scatter_range(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
+                                          int32_t world, int64_t base, int64_t len, float* out, void* stream) {
+  GRACE_REQUIRE(vals && idx && out && per >= 0 && world >= 1 && len >= 0,
+                "grace_sparse_scatter_range: bad arguments");
+  if (per == 0) return GRACE_OK;
+  scatter_range_kernel<<<stream_grid(per * world, 256, 2048), 256, 0, as_stream(stream)>>>(vals, idx, stride, per,
+                                                                                         world, base, len, out);
+  GRACE_CHECK_LAUNCH("grace_sparse_scatter_range");
   return GRACE_OK;
 }
 

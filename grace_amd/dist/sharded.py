@@ -1,0 +1,212 @@
+"""Sharded top-k with residual error feedback: ONE gradient bucket split into contiguous shards,
+one per rank (BASELINE configs[4]: 256 MiB bucket, k = 0.1 %, 8 x MI355X).
+
+The reference has no sharded mode -- its Allgather (grace_dl/dist/communicator/allgather.py:8-45)
+runs every rank on its own full bucket.  Here each rank owns n/W elements and the ranks together
+select exactly the single-GPU top-k of the whole bucket (TopKCompressor, topk.py:32-42, with the
+same tie rule as the single-GPU engine: larger |t| first, lower global index first), keep the
+residual of their own shard (ResidualMemory, residual.py:10-20) and decode the replicated dense
+bucket (or only their own slice, ``dense="shard"``).
+
+Per step (kernels: grace_amd/csrc/topk.hip, "Sharded top-k"):
+  1. sample this shard's |t| into the shared bracket histogram xs      -> all_reduce(xs)
+  2. global bracket + one streaming pass over the shard (t, r' = t, local candidates)
+                                                                       -> all_gather(xh)
+  3. host: boundary bin B, how many of it are still needed, exact list capacities (one 8 KB/rank
+     read -- the step's only host synchronisation)
+  4. route: sure + above-B entries to the local payload, bin-B entries to a list
+                                                                       -> all_gather(lists)
+  5. boundary: exact global ranking of bin B; winners join their owner's payload
+                                                                       -> all_gather(payloads)
+  6. scatter-range decode into the dense output.
+If the sampled bracket misses (degenerate data: heavy ties, mostly-zero buckets) every rank
+gathers t and runs the exact single-GPU selection instead (same result, slower).
+
+``kernels`` defaults to the native HIP set; the CPU tests inject an oracle-backed emulator of the
+same six calls to run the protocol on gloo.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from grace_amd import ops
+
+HIST_BINS = 2048
+
+
+class NativeShardKernels:
+    """The HIP kernels behind each protocol step (GPU tensors only)."""
+
+    def exchange_buffers(self, device):
+        return ops.shard_exchange_buffers(device)
+
+    def empty(self, n, dtype, device):
+        return torch.empty(n, dtype=dtype, device=device)
+
+    def cand_cap(self, m, k):
+        return min(m, 2 * k + 65536)   # topk.hip topk_cap
+
+    sample = staticmethod(ops.shard_sample)
+    main = staticmethod(ops.shard_main)
+    route = staticmethod(ops.shard_route)
+    boundary = staticmethod(ops.shard_boundary)
+    take = staticmethod(ops.shard_take)
+    scatter_range = staticmethod(ops.scatter_range)
+
+    def fill_zero(self, x):
+        return ops.fill(x, 0.0)
+
+    def select_all(self, t, k):
+        _, vals, idx = ops.topk_compress(t, k)
+        return vals, idx
+
+
+def plan_boundary(xh_all, k, world, cand_cap):
+    """Host step 3 from the gathered [W, 2048 + 8] exchange rows (hist, n_sure, n_cand, ...).
+
+    Returns (ok, B, need, cap_b, cap_p): B the boundary bin (2048 when no candidate is needed),
+    need the count still to take from bin B, cap_b the largest per-rank bin-B list, cap_p an upper
+    bound of any rank's payload count.  ok False = the bracket missed or a list overflowed."""
+    xh_all = np.asarray(xh_all, dtype=np.int64).reshape(world, -1)
+    hist_r = xh_all[:, :HIST_BINS]
+    n_sure_r = xh_all[:, HIST_BINS]
+    n_cand_r = xh_all[:, HIST_BINS + 1]
+    s = int(n_sure_r.sum())
+    c = int(n_cand_r.sum())
+    if s > k or s + c < k or bool((n_cand_r > cand_cap).any()):
+        return False, -1, 0, 0, 0
+    target = k - s
+    if target == 0:
+        return True, HIST_BINS, 0, 0, int(n_sure_r.max())
+    hist = hist_r.sum(axis=0)
+    above_incl = np.cumsum(hist[::-1])[::-1]          # count in bins >= b
+    above = above_incl - hist                          # count in bins > b
+    cand = np.nonzero((above < target) & (target <= above_incl))[0]
+    B = int(cand.max())
+    need = int(target - above[B])
+    cap_b = int(hist_r[:, B].max())
+    cap_p = int(min(k, (n_sure_r + (hist_r[:, B:].sum(axis=1))).max()))
+    return True, B, need, cap_b, cap_p
+
+
+class ShardedTopK:
+    """Top-k (ratio) + residual memory over one bucket sharded across the ranks of `group`."""
+
+    def __init__(self, compress_ratio, group=None, dense="replicated", kernels=None):
+        if dense not in ("replicated", "shard"):
+            raise ValueError("dense must be 'replicated' or 'shard'")
+        self.compress_ratio = compress_ratio
+        self.group = group
+        self.dense = dense
+        self.k_ops = kernels or NativeShardKernels()
+        self.residuals = {}
+        self._sizes = {}
+        self.last_payload = None      # (vals, idx) of this rank's entries of the last step
+        self.last_fallback = False
+
+    def _world(self):
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group), dist.get_rank(self.group)
+        return 1, 0
+
+    def _shard_sizes(self, name, m, device, world):
+        sizes = self._sizes.get(name)
+        if sizes is None or sizes[dist.get_rank(self.group) if world > 1 else 0] != m:
+            if world > 1:
+                mine = torch.tensor([m], dtype=torch.int64, device=device)
+                allm = self.k_ops.empty(world, torch.int64, device)
+                dist.all_gather_into_tensor(allm, mine, group=self.group)
+                sizes = [int(v) for v in allm.cpu().tolist()]
+            else:
+                sizes = [m]
+            self._sizes[name] = sizes
+        return sizes
+
+    def step(self, shard, name):
+        K = self.k_ops
+        world, rank = self._world()
+        g = shard.reshape(-1)
+        dev = g.device
+        m = g.numel()
+        sizes = self._shard_sizes(name, m, dev, world)
+        base = sum(sizes[:rank])
+        n = sum(sizes)
+        k = ops.ratio_k(n, self.compress_ratio)
+        res = self.residuals.get(name)
+        has_res = res is not None and res.numel() == m
+        if not has_res:
+            res = K.empty(m, torch.float32, dev)
+        self.residuals[name] = res
+        stratum = max(1, n // ops.SAMPLE_MAX)
+        sample_total = sum(sz // stratum for sz in sizes)
+        xs, xh = K.exchange_buffers(dev)
+        vals = K.empty(k, torch.float32, dev)
+        idx = K.empty(k, torch.int32, dev)
+
+        K.sample(g, res, has_res, stratum, xs)
+        if world > 1:
+            dist.all_reduce(xs, group=self.group)
+        K.main(g, res, has_res, base, n, k, sample_total, vals, idx, xs, xh)
+        if world > 1:
+            xh_all = K.empty(world * xh.numel(), torch.int32, dev)
+            dist.all_gather_into_tensor(xh_all, xh, group=self.group)
+        else:
+            xh_all = xh
+        ok, B, need, cap_b, cap_p = plan_boundary(xh_all.cpu().numpy(), k, world, K.cand_cap(m, k))
+        self.last_fallback = not ok
+        if not ok:
+            return self._fallback(res, base, n, k, sizes, world, vals, idx, dev)
+
+        bsend = K.empty(cap_b + 1, torch.int64, dev)
+        K.route(res, base, k, B, vals, idx, bsend)
+        if world > 1:
+            brecv = K.empty(world * (cap_b + 1), torch.int64, dev)
+            dist.all_gather_into_tensor(brecv, bsend, group=self.group)
+        else:
+            brecv = bsend
+        K.boundary(res, base, k, brecv, world, cap_b, need, vals, idx, cap_p)
+        self.last_payload = (vals[:cap_p], idx[:cap_p])
+        return self._decode(vals, idx, cap_p, base, n, m, world, dev)
+
+    def _decode(self, vals, idx, cap_p, base, n, m, world, dev):
+        K = self.k_ops
+        if self.dense == "shard":
+            out = K.fill_zero(K.empty(m, torch.float32, dev))
+            K.scatter_range(vals, idx, 0, cap_p, 1, base, out)
+            return out
+        out = K.fill_zero(K.empty(n, torch.float32, dev))
+        if world == 1:
+            K.scatter_range(vals, idx, 0, cap_p, 1, 0, out)
+            return out
+        send = K.empty(2 * cap_p, torch.float32, dev)
+        send[:cap_p].copy_(vals[:cap_p])
+        send[cap_p:].copy_(idx[:cap_p].view(torch.float32))
+        recv = K.empty(world * 2 * cap_p, torch.float32, dev)
+        dist.all_gather_into_tensor(recv, send, group=self.group)
+        K.scatter_range(recv, recv[cap_p:].view(torch.int32), 2 * cap_p, cap_p, world, 0, out)
+        return out
+
+    def _fallback(self, res, base, n, k, sizes, world, vals, idx, dev):
+        """Exact path: the residual buffer holds t for every element after the main pass."""
+        K = self.k_ops
+        if world > 1:
+            if len(set(sizes)) != 1:
+                parts = [K.empty(sz, torch.float32, dev) for sz in sizes]
+                dist.all_gather(parts, res, group=self.group)
+                t_all = torch.cat(parts)
+            else:
+                t_all = K.empty(n, torch.float32, dev)
+                dist.all_gather_into_tensor(t_all, res, group=self.group)
+        else:
+            t_all = res.clone()
+        vals_all, idx_all = K.select_all(t_all, k)
+        K.take(vals_all, idx_all, k, res, base, vals, idx, k)
+        self.last_payload = (vals, idx)
+        m = res.numel()
+        if self.dense == "shard":
+            out = K.fill_zero(K.empty(m, torch.float32, dev))
+            K.scatter_range(vals_all, idx_all, 0, k, 1, base, out)
+        else:
+            out = K.fill_zero(K.empty(n, torch.float32, dev))
+            K.scatter_range(vals_all, idx_all, 0, k, 1, 0, out)
+        return out

@@ -469,3 +469,56 @@ def normal(shape, seed, device):
     x = torch.empty(shape, dtype=F32, device=device)
     _lib.call("grace_normal_fill", _p(x), x.numel(), int(seed) & (2 ** 64 - 1), _stream())
     return x
+
+
+# ----------------------------------------------------------------------------- sharded top-k
+SAMPLE_MAX = 131072   # topk.hip kSampleMax: target size of the stratified bracket sample
+
+
+def shard_exchange_buffers(device):
+    """(xs, xh) int32 exchange buffers of the sharded top-k, zeroed once (re-zeroed by the kernels)."""
+    key = (str(device), "shard_x", torch.cuda.current_stream(device).cuda_stream)
+    hit = _ws.get(key)
+    if hit is None:
+        hit = (torch.zeros(_lib.query("grace_topk_shard_xs_words"), dtype=torch.int32, device=device),
+               torch.zeros(_lib.query("grace_topk_shard_xh_words"), dtype=torch.int32, device=device))
+        _ws[key] = hit
+    return hit
+
+
+def shard_sample(g, residual, has_residual, stratum, xs):
+    _lib.call("grace_topk_shard_sample", _p(g), _p(residual), 1 if has_residual else 0, 1.0, 1.0, g.numel(),
+              int(stratum), _p(xs), _stream())
+
+
+def shard_main(g, residual, has_residual, idx_base, n_global, k, sample_total, vals, idx, xs, xh):
+    m = g.numel()
+    ws = topk_workspace(m, k, g.device)
+    _lib.call("grace_topk_shard_main", _p(g), _p(residual), 1 if has_residual else 0, 1.0, 1.0, m, int(idx_base),
+              int(n_global), int(k), int(sample_total), _p(vals), _p(idx), _p(ws), ws.numel(), _p(xs), _p(xh),
+              _stream())
+
+
+def shard_route(residual, idx_base, k, boundary_bin, vals, idx, bsend):
+    m = residual.numel()
+    ws = topk_workspace(m, k, residual.device)
+    _lib.call("grace_topk_shard_route", _p(residual), m, int(idx_base), int(k), int(boundary_bin), _p(vals),
+              _p(idx), _p(ws), ws.numel(), _p(bsend), _stream())
+
+
+def shard_boundary(residual, idx_base, k, brecv, world, cap_b, need, vals, idx, cap_p):
+    m = residual.numel()
+    ws = topk_workspace(m, k, residual.device)
+    _lib.call("grace_topk_shard_boundary", _p(residual), m, int(idx_base), int(k), _p(brecv), int(world),
+              int(cap_b), int(need), _p(vals), _p(idx), int(cap_p), _p(ws), ws.numel(), _stream())
+
+
+def shard_take(vals_all, idx_all, k, residual, idx_base, vals, idx, cap_p):
+    _lib.call("grace_topk_shard_take", _p(vals_all), _p(idx_all), int(k), _p(residual), residual.numel(),
+              int(idx_base), _p(vals), _p(idx), int(cap_p), _stream())
+
+
+def scatter_range(vals, idx, stride, per, world, base, out):
+    """out[idx - base] = 0 + v over `world` padded payloads (idx -1 = padding); out pre-zeroed."""
+    _lib.call("grace_sparse_scatter_range", _p(vals), _p(idx), int(stride), int(per), int(world), int(base),
+              out.numel(), _p(out), _stream())

@@ -205,6 +205,44 @@ grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, i
 /* standard normal fill (q draws, powersgd.py:41 / memory/powersgd.py:27), device generator */
 grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* stream);
 
+/* ---- sharded top-k (BASELINE configs[4]) ------------------------------------
+ * One bucket of n_global elements split into contiguous shards, one per rank (this rank's shard:
+ * m elements starting at idx_base).  The union of the ranks' payloads equals the single-GPU
+ * grace_topk_residual_step selection on the whole bucket (same tie rule); the collectives between
+ * the calls are the caller's (grace_amd/dist/sharded.py):
+ *   shard_sample -> all_reduce(xs) -> shard_main -> all_gather(xh) -> [host: boundary bin, need]
+ *   -> shard_route -> all_gather(bsend) -> shard_boundary -> all_gather(payload) -> scatter_range
+ * xs: u32[grace_topk_shard_xs_words()] sample histogram, zero before the first step (shard_main
+ * re-zeroes it); xh: u32[grace_topk_shard_xh_words()] = candidate histogram [2048] + counters
+ * (n_sure, n_cand, ...).  vals/idx hold this rank's payload (capacity >= max(k, cap_p)); after
+ * shard_boundary entries [count, cap_p) are padding with idx -1.  ws as grace_topk_workspace_bytes(m, k).
+ * Replaces the single-process TopKCompressor.compress + ResidualMemory (topk.py:32-42,
+ * residual.py:10-20) for one bucket sharded over ranks. */
+size_t grace_topk_shard_xs_words(void);
+size_t grace_topk_shard_xh_words(void);
+grace_status_t grace_topk_shard_sample(const float* g, float* residual, int32_t has_residual, float beta,
+                                       float gamma, int64_t m, int64_t stratum, uint32_t* xs, void* stream);
+grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t has_residual, float beta,
+                                     float gamma, int64_t m, int64_t idx_base, int64_t n_global, int64_t k,
+                                     int64_t sample_total, float* vals, int32_t* idx, void* ws, size_t ws_bytes,
+                                     uint32_t* xs, uint32_t* xh, void* stream);
+grace_status_t grace_topk_shard_route(float* residual, int64_t m, int64_t idx_base, int64_t k,
+                                      int32_t boundary_bin, float* vals, int32_t* idx, void* ws,
+                                      size_t ws_bytes, int64_t* bsend, void* stream);
+grace_status_t grace_topk_shard_boundary(float* residual, int64_t m, int64_t idx_base, int64_t k,
+                                         const int64_t* brecv, int32_t world, int64_t cap_b, uint32_t need,
+                                         float* vals, int32_t* idx, int64_t cap_p, void* ws, size_t ws_bytes,
+                                         void* stream);
+/* exact fallback (bracket miss): this rank's entries of the whole bucket's selection */
+grace_status_t grace_topk_shard_take(const float* vals_all, const int32_t* idx_all, int64_t k, float* residual,
+                                     int64_t m, int64_t idx_base, float* vals, int32_t* idx, int64_t cap_p,
+                                     void* stream);
+/* diagnostic: copy the 64-byte control block to the host (synchronises the stream) */
+grace_status_t grace_topk_shard_read(const void* ws, uint32_t* ctl_host, void* stream);
+/* out[idx - base] = 0 + v for gathered padded payloads (rank w at + w * stride, `per` entries) */
+grace_status_t grace_sparse_scatter_range(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
+                                          int32_t world, int64_t base, int64_t len, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
