@@ -51,6 +51,15 @@ SIGNATURES = {
     "grace_topk_shard_take": (ST, [P, P, I64, P, I64, I64, P, P, I64, P]),
     "grace_topk_shard_read": (ST, [P, P, P]),
     "grace_sparse_scatter_range": (ST, [P, P, I64, I64, I32, I64, I64, P, P]),
+    "grace_dgc_workspace_bytes": (SZ, [I64]),
+    "grace_dgc_sample": (ST, [P, I64, P, U64, I64, P, P]),
+    "grace_dgc_threshold": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),
+    "grace_dgc_write": (ST, [P, I64, P, P, P, P]),
+    "grace_dgc_compensate": (ST, [P, P, P, I32, F32, I64, P]),
+    "grace_dgc_mask_update": (ST, [P, P, P, I64, P, P]),
+    "grace_sumsq_workspace_bytes": (SZ, []),
+    "grace_sumsq": (ST, [P, I64, P, P, P]),
+    "grace_clip_by_sumsq": (ST, [P, P, F32, P, I64, P]),
     "grace_sparse_decode": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_decode_i64": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),

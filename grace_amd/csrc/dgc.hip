@@ -1,0 +1,456 @@
+// Deep Gradient Compression (DGC) for CDNA4: sampled threshold + error-feedback memory with
+// momentum correction.
+//
+// Reference semantics (sands-lab/grace):
+//   DgcCompressor.compress  grace_dl/dist/compressor/dgc.py:12-43
+//     sample 1 % of the elements (uniform indices, with replacement), thr = the k_s-th largest
+//     |sample| (k_s = max(1, int(numel * ratio * 0.01))); mask = |t| >= thr; then up to 10 times:
+//     selected > 1.3 numel ratio -> thr *= 1.3, selected < 0.7 numel ratio -> thr *= 0.7, else stop;
+//     payload = (t[where(mask)], where(mask)) in ascending index order, int64 indices.
+//   DgcMemory.compensate / update  grace_dl/dist/memory/dgc.py:15-39
+//     r = momentum r + g (first step r = g);  a = a + r (first step a = g);  t = a;
+//     after compress: r = r * ~mask, a = a * ~mask (a multiply: masked entries become +-0 / NaN).
+//
+// The reference re-scans the whole tensor once per threshold adjustment (up to 11 times).  Here
+// every threshold the loop could ever visit is known up front -- thr0 * 1.3^a * 0.7^b along the
+// 2^10 paths of the loop, computed with the same f32 multiplications in the same order -- so ONE
+// pass histograms |t| against that sorted table (binary search in LDS, only for the few elements
+// above its smallest entry), a single thread replays the loop on exact counts, and two more
+// passes produce the ordered payload (per-chunk counts, then the compaction).
+#include <math.h>
+
+#include "common.h"
+
+namespace grace {
+
+constexpr int kDBlock = 256;
+constexpr int kDChunk = 4096;          // elements per compaction chunk
+constexpr int kDepth = 10;              // dgc.py:26 range(10)
+constexpr int kNodes = (1 << (kDepth + 1)) - 1;   // 2047 thresholds the loop can visit
+constexpr int kTab = 2048;              // sorted table (padded with +inf)
+
+struct DgcMeta {
+  uint32_t thr0;      // bits of the sampled threshold
+  uint32_t thr;       // bits of the final threshold
+  uint32_t total;     // selected count at the final threshold
+  uint32_t nan0;      // thr0 is NaN
+  uint32_t pad[12];
+};
+
+struct DgcWs {
+  DgcMeta* meta;
+  float* tab;         // [kTab] ascending
+  uint32_t* hist;     // [kTab + 1]
+  uint32_t* part;     // [nchunks] counts
+  uint32_t* offs;     // [nchunks] exclusive offsets
+};
+
+static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static DgcWs dgc_carve(void* ws, int64_t n) {
+  const int64_t nch = (n + kDChunk - 1) / kDChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  DgcWs w;
+  w.meta = reinterpret_cast<DgcMeta*>(p);
+  p += 256;
+  w.tab = reinterpret_cast<float*>(p);
+  p += al256(sizeof(float) * kTab);
+  w.hist = reinterpret_cast<uint32_t*>(p);
+  p += al256(sizeof(uint32_t) * (kTab + 1));
+  w.part = reinterpret_cast<uint32_t*>(p);
+  p += al256(sizeof(uint32_t) * nch);
+  w.offs = reinterpret_cast<uint32_t*>(p);
+  return w;
+}
+
+static size_t dgc_ws_bytes(int64_t n) {
+  const int64_t nch = (n + kDChunk - 1) / kDChunk;
+  return 256 + al256(sizeof(float) * kTab) + al256(sizeof(uint32_t) * (kTab + 1)) +
+         2 * al256(sizeof(uint32_t) * nch);
+}
+
+// ------------------------------------------------------------------------------------------------
+// sample: |t[idx_j]|, idx from the caller (parity: torch's CPU uniform_(0, numel).long()) or the
+// counter-based generator (uniform integer in [0, numel))
+__global__ __launch_bounds__(kDBlock) void dgc_sample_kernel(const float* __restrict__ t, int64_t n,
+                                                            const int64_t* __restrict__ sidx, uint64_t seed,
+                                                            int64_t ns, float* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * kDBlock + threadIdx.x; j < ns; j += (int64_t)gridDim.x * kDBlock) {
+    int64_t i;
+    if (sidx) {
+      i = sidx[j];
+    } else {
+      const uint64_t h = ((uint64_t)rand32(seed, (uint64_t)j) << 32) | rand32(seed ^ 0xD6E8FEB86659FD93ull, (uint64_t)j);
+      i = (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
+    }
+    out[j] = fabsf(t[i]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// table: thr0 = min of the top-k_s sampled magnitudes (torch.min propagates NaN), then every
+// threshold of the adjustment tree (node = path bits from the root, 1 -> *1.3, 0 -> *0.7, the
+// multiplications in loop order), bitonic-sorted ascending; the counts are zeroed.
+__global__ __launch_bounds__(1024) void dgc_table_kernel(const float* __restrict__ topv, int64_t ks, DgcWs w) {
+  __shared__ float s[kTab];
+  __shared__ float s_min;
+  __shared__ uint32_t s_nan;
+  const int t = threadIdx.x;
+  float mn = INFINITY;
+  uint32_t nan = 0;
+  for (int64_t j = t; j < ks; j += 1024) {
+    const float v = topv[j];
+    if (v != v) nan = 1; else mn = fminf(mn, v);
+  }
+  // block reduce
+  __shared__ float sm[1024 / kWave];
+  __shared__ uint32_t sn[1024 / kWave];
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+  nan = __ballot(nan != 0) != 0;
+  if ((t & 63) == 0) { sm[t >> 6] = mn; sn[t >> 6] = nan; }
+  __syncthreads();
+  if (t == 0) {
+    float m = INFINITY;
+    uint32_t nn = 0;
+    for (int j = 0; j < 1024 / kWave; ++j) { m = fminf(m, sm[j]); nn |= sn[j]; }
+    s_min = m;
+    s_nan = nn;
+    w.meta->thr0 = nn ? 0x7FC00000u : __float_as_uint(m);
+    w.meta->nan0 = nn;
+  }
+  __syncthreads();
+  const float thr0 = s_min;
+  const float up = 1.3f, down = 0.7f;   // the Python floats as the f32 operands torch multiplies by
+  for (int node = t; node < kTab; node += 1024) {
+    float x = INFINITY;
+    if (node < kNodes) {
+      // node in heap order: depth d = floor(log2(node + 1)), path = the d bits below the leading 1
+      const uint32_t id = (uint32_t)node + 1u;
+      const int d = 31 - __clz(id);
+      x = thr0;
+      for (int b = d - 1; b >= 0; --b) x = ((id >> b) & 1u) ? x * up : x * down;
+    }
+    s[node] = x;
+  }
+  __syncthreads();
+  // bitonic sort ascending (kTab = 2048 = 2 x 1024 threads)
+  for (int size = 2; size <= kTab; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = t; e < kTab / 2; e += 1024) {
+        const int lo = 2 * e - (e & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const float a = s[lo], b = s[hi];
+        if ((a > b) == asc) { s[lo] = b; s[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int e = t; e < kTab; e += 1024) w.tab[e] = s[e];
+  for (int e = t; e <= kTab; e += 1024) w.hist[e] = 0u;
+}
+
+// number of table entries <= key (upper bound); NaN compares false -> 0
+__device__ __forceinline__ int tab_bin(const float* tab, float key) {
+  if (!(key >= tab[0])) return 0;
+  int lo = 1, hi = kTab;            // answer in [1, kTab]
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;   // is tab[mid] <= key ?
+    if (key >= tab[mid]) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// one pass: histogram of |t| over the table (elements below the smallest entry skip the search)
+__global__ __launch_bounds__(kDBlock) void dgc_count_kernel(const float* __restrict__ t, int64_t n, DgcWs w) {
+  __shared__ float tab[kTab];
+  __shared__ uint32_t h[kTab + 1];
+  for (int e = threadIdx.x; e < kTab; e += kDBlock) tab[e] = w.tab[e];
+  for (int e = threadIdx.x; e <= kTab; e += kDBlock) h[e] = 0u;
+  __syncthreads();
+  const float t0 = tab[0];
+  const int64_t n4 = n >> 2;
+  const bool vec = (reinterpret_cast<uintptr_t>(t) & 15u) == 0;
+  const int64_t stride = (int64_t)gridDim.x * kDBlock;
+  if (vec) {
+    for (int64_t q = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q < n4; q += stride) {
+      const float4 v = reinterpret_cast<const float4*>(t)[q];
+      const float a[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (a[j] >= t0) atomicAdd(&h[tab_bin(tab, a[j])], 1u);
+    }
+  }
+  for (int64_t i = (vec ? n4 * 4 : 0) + (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += stride) {
+    const float a = fabsf(t[i]);
+    if (a >= t0) atomicAdd(&h[tab_bin(tab, a)], 1u);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e <= kTab; e += kDBlock)
+    if (h[e]) atomicAdd(&w.hist[e], h[e]);
+}
+
+// replay dgc.py:23-36 on the exact counts (one thread): count(|t| >= x) for a table value x at
+// lower-bound position p is the number of elements whose bin is > p
+__global__ void dgc_replay_kernel(int64_t n, double ratio, DgcWs w) {
+  __shared__ uint32_t suf[kTab + 2];
+  if (threadIdx.x != 0) return;
+  uint32_t acc = 0;
+  suf[kTab + 1] = 0;
+  for (int b = kTab; b >= 0; --b) { acc += w.hist[b]; suf[b] = acc; }
+  // torch compares the int64 count tensor with the Python float (1.3 * numel * ratio, a double)
+  // in the default dtype, f32
+  const float hi = (float)(1.3 * (double)n * ratio);
+  const float lo = (float)(0.7 * (double)n * ratio);
+  auto count_ge = [&](float x) -> uint32_t {
+    if (x != x) return 0u;
+    int a = 0, b = kTab;            // first index with tab >= x
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (w.tab[mid] < x) a = mid + 1; else b = mid;
+    }
+    return suf[a + 1];
+  };
+  float thr = __uint_as_float(w.meta->thr0);
+  uint32_t sel = count_ge(thr);
+  for (int it = 0; it < kDepth; ++it) {
+    if ((float)sel > hi) thr = 1.3f * thr;
+    else if ((float)sel < lo) thr = 0.7f * thr;
+    else break;
+    sel = count_ge(thr);
+  }
+  w.meta->thr = __float_as_uint(thr);
+  w.meta->total = sel;
+}
+
+// per-chunk counts at the final threshold, then exclusive offsets (one workgroup)
+__global__ __launch_bounds__(kDBlock) void dgc_chunk_kernel(const float* __restrict__ t, int64_t n, DgcWs w) {
+  const float thr = __uint_as_float(w.meta->thr);
+  const int64_t base = (int64_t)blockIdx.x * kDChunk;
+  const int64_t end = min(base + (int64_t)kDChunk, n);
+  uint32_t c = 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += kDBlock) c += fabsf(t[i]) >= thr;
+  c = wave_sum(c);
+  __shared__ uint32_t sc[kDBlock / kWave];
+  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int j = 0; j < kDBlock / kWave; ++j) s += sc[j];
+    w.part[blockIdx.x] = s;
+  }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ uint32_t dgc_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+  constexpr int NW = BLOCK / kWave;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < NW; ++i) { const uint32_t x = s_w[i]; s_w[i] = acc; acc += x; }
+    s_w[NW] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = s_w[wv] + inc - v;
+  if (total) *total = s_w[NW];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(1024) void dgc_offsets_kernel(int64_t nch, DgcWs w) {
+  __shared__ uint32_t s_w[1024 / kWave + 1];
+  uint32_t run = 0;
+  for (int64_t j0 = 0; j0 < nch; j0 += 1024) {
+    const int64_t j = j0 + threadIdx.x;
+    const uint32_t c = j < nch ? w.part[j] : 0u;
+    uint32_t tot;
+    const uint32_t ex = dgc_excl_scan<1024>(c, s_w, &tot);
+    if (j < nch) w.offs[j] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) w.meta->total = run;
+}
+
+// ordered compaction of |t| >= thr: values f32, indices int64 (torch.where order)
+__global__ __launch_bounds__(kDBlock) void dgc_write_kernel(const float* __restrict__ t, int64_t n, DgcWs w,
+                                                           float* __restrict__ vals, int64_t* __restrict__ idx) {
+  __shared__ uint32_t s_w[kDBlock / kWave + 1];
+  const float thr = __uint_as_float(w.meta->thr);
+  const int64_t base = (int64_t)blockIdx.x * kDChunk;
+  const int64_t end = min(base + (int64_t)kDChunk, n);
+  uint32_t run = w.offs[blockIdx.x];
+  for (int64_t j0 = base; j0 < end; j0 += kDBlock) {
+    const int64_t i = j0 + threadIdx.x;
+    float v = 0.f;
+    bool sel = false;
+    if (i < end) { v = t[i]; sel = fabsf(v) >= thr; }
+    uint32_t tot;
+    const uint32_t ex = dgc_excl_scan<kDBlock>(sel ? 1u : 0u, s_w, &tot);
+    if (sel) { vals[run + ex] = v; idx[run + ex] = i; }
+    run += tot;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// memory
+// compensate: r = m r + g (r = g first), a = a + r (a = g first); returns a in `acc`
+__global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __restrict__ g, float* __restrict__ r,
+                                                                float* __restrict__ a, int has_state,
+                                                                float momentum, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock) {
+    const float gv = g[i];
+    if (has_state) {
+      const float rv = momentum * r[i] + gv;
+      r[i] = rv;
+      a[i] = a[i] + rv;
+    } else {
+      r[i] = gv;
+      a[i] = gv;
+    }
+  }
+}
+
+// update: keep = !(|t| >= thr) as in mask = tensor.abs() >= thr; r = r * keep, a = a * keep
+// (t is the compensated tensor the mask came from; it may alias a)
+__global__ __launch_bounds__(kDBlock) void dgc_mask_kernel(const float* t, float* r, float* a, int64_t n,
+                                                          const DgcMeta* __restrict__ meta) {
+  const float thr = __uint_as_float(meta->thr);
+  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock) {
+    const float keep = fabsf(t[i]) >= thr ? 0.f : 1.f;
+    const float av = t == a ? t[i] : a[i];
+    r[i] = r[i] * keep;
+    a[i] = av * keep;
+  }
+}
+
+// gradient clipping (memory/dgc.py:16-19): sum of squares (f64 accumulate) of one tensor
+__global__ __launch_bounds__(kDBlock) void sumsq_kernel(const float* __restrict__ x, int64_t n,
+                                                       double* __restrict__ part) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock) {
+    const double v = x[i];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  __shared__ double sw[kDBlock / kWave];
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int j = 0; j < kDBlock / kWave; ++j) a += sw[j];
+    part[blockIdx.x] = a;
+  }
+}
+
+__global__ void sumsq_finish_kernel(const double* __restrict__ part, int nb, float* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int j = 0; j < nb; ++j) a += part[j];
+    *out = (float)a;
+  }
+}
+
+// clamp(x, -c, c) with c = sqrt(s / world) read from the device (after the caller's all_reduce)
+__global__ __launch_bounds__(kDBlock) void clip_kernel(const float* __restrict__ x, const float* __restrict__ s,
+                                                      float world, float* __restrict__ out, int64_t n) {
+  const float c = sqrtf(*s / world);
+  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock)
+    out[i] = fminf(fmaxf(x[i], -c), c);
+}
+
+}  // namespace grace
+
+using namespace grace;
+
+extern "C" {
+
+size_t grace_dgc_workspace_bytes(int64_t n) { return dgc_ws_bytes(n < 1 ? 1 : n); }
+
+grace_status_t grace_dgc_sample(const float* t, int64_t n, const int64_t* sample_idx, uint64_t seed, int64_t ns,
+                                float* sample_abs, void* stream) {
+  GRACE_REQUIRE(t && sample_abs && n >= 1 && ns >= 1, "grace_dgc_sample: bad arguments");
+  dgc_sample_kernel<<<stream_grid(ns, kDBlock, 1024), kDBlock, 0, as_stream(stream)>>>(t, n, sample_idx, seed, ns,
+                                                                                      sample_abs);
+  GRACE_CHECK_LAUNCH("grace_dgc_sample");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_threshold(const float* t, int64_t n, const float* top_vals, int64_t ks, double ratio,
+                                   void* ws, void* stream) {
+  GRACE_REQUIRE(t && top_vals && ws && n >= 1 && ks >= 1, "grace_dgc_threshold: bad arguments");
+  hipStream_t s = as_stream(stream);
+  DgcWs w = dgc_carve(ws, n);
+  const int64_t nch = (n + kDChunk - 1) / kDChunk;
+  dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_threshold");
+  dgc_count_kernel<<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_threshold");
+  dgc_replay_kernel<<<1, 64, 0, s>>>(n, ratio, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_threshold");
+  dgc_chunk_kernel<<<(unsigned)nch, kDBlock, 0, s>>>(t, n, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_threshold");
+  dgc_offsets_kernel<<<1, 1024, 0, s>>>(nch, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_threshold");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_write(const float* t, int64_t n, const void* ws, float* vals, int64_t* idx, void* stream) {
+  GRACE_REQUIRE(t && ws && n >= 1, "grace_dgc_write: bad arguments");
+  DgcWs w = dgc_carve(const_cast<void*>(ws), n);
+  const int64_t nch = (n + kDChunk - 1) / kDChunk;
+  dgc_write_kernel<<<(unsigned)nch, kDBlock, 0, as_stream(stream)>>>(t, n, w, vals, idx);
+  GRACE_CHECK_LAUNCH("grace_dgc_write");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accum, int32_t has_state,
+                                    float momentum, int64_t n, void* stream) {
+  GRACE_REQUIRE(g && residual && accum && n >= 0, "grace_dgc_compensate: bad arguments");
+  if (n == 0) return GRACE_OK;
+  dgc_compensate_kernel<<<stream_grid(n, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(g, residual, accum,
+                                                                                         has_state, momentum, n);
+  GRACE_CHECK_LAUNCH("grace_dgc_compensate");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_mask_update(const float* t, float* residual, float* accum, int64_t n, const void* ws,
+                                     void* stream) {
+  GRACE_REQUIRE(t && residual && accum && ws && n >= 0, "grace_dgc_mask_update: bad arguments");
+  if (n == 0) return GRACE_OK;
+  dgc_mask_kernel<<<stream_grid(n, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(
+      t, residual, accum, n, reinterpret_cast<const DgcMeta*>(ws));
+  GRACE_CHECK_LAUNCH("grace_dgc_mask_update");
+  return GRACE_OK;
+}
+
+size_t grace_sumsq_workspace_bytes(void) { return sizeof(double) * 1024; }
+
+grace_status_t grace_sumsq(const float* x, int64_t n, void* ws, float* out, void* stream) {
+  GRACE_REQUIRE(x && ws && out && n >= 0, "grace_sumsq: bad arguments");
+  const unsigned nb = n ? stream_grid(n, kDBlock, 1024) : 1;
+  hipStream_t s = as_stream(stream);
+  sumsq_kernel<<<nb, kDBlock, 0, s>>>(x, n, reinterpret_cast<double*>(ws));
+  GRACE_CHECK_LAUNCH("grace_sumsq");
+  sumsq_finish_kernel<<<1, 64, 0, s>>>(reinterpret_cast<const double*>(ws), (int)nb, out);
+  GRACE_CHECK_LAUNCH("grace_sumsq");
+  return GRACE_OK;
+}
+
+grace_status_t grace_clip_by_sumsq(const float* x, const float* sumsq_dev, float world, float* out, int64_t n,
+                                   void* stream) {
+  GRACE_REQUIRE(x && sumsq_dev && out && n >= 0 && world > 0.f, "grace_clip_by_sumsq: bad arguments");
+  if (n == 0) return GRACE_OK;
+  clip_kernel<<<stream_grid(n, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(x, sumsq_dev, world, out, n);
+  GRACE_CHECK_LAUNCH("grace_clip_by_sumsq");
+  return GRACE_OK;
+}
+
+}  // extern "C"

@@ -963,38 +963,43 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
 __global__ __launch_bounds__(kSelBlock) void topk_shard_route(StepArgs a, TopkWs w, int B, int64_t* bsend) {
   const TopkCtl c = *w.ctl;
   const int t = threadIdx.x;
-  const int lane = t & 63;
   const int64_t base = a.idx_base;
   for (uint32_t j = blockIdx.x * kSelBlock + t; j < c.n_sure; j += gridDim.x * kSelBlock) {
     const float v = a.vals[j];
     a.r[a.idx[j] - base] = v - v;
   }
   int2* blist = reinterpret_cast<int2*>(bsend + 1);
-  for (uint32_t j0 = blockIdx.x * kSelBlock; j0 < c.n_cand; j0 += gridDim.x * kSelBlock) {
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  __shared__ uint32_t s_base[2];
+  // contiguous slice per workgroup; one block scan places the round, one atomic per list reserves
+  const uint32_t per = (c.n_cand + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * per, b1 = min(c.n_cand, b0 + per);
+  for (uint32_t j0 = b0; j0 < b1; j0 += kSelBlock) {
     const uint32_t j = j0 + t;
     int2 e = make_int2(0, 0);
     int bin = -1;
-    if (j < c.n_cand) {
+    if (j < b1) {
       e = w.cand[j];
       bin = (int)((abs_key(u2f((uint32_t)e.y)) - c.thr_lo) >> c.shift);
     }
-    const uint64_t ma = __ballot(bin > B), mb = __ballot(bin == B);
-    uint32_t ba = 0, bb = 0;
-    if (lane == 0) {
-      if (ma) ba = atomicAdd(&w.ctl->n_sel, (uint32_t)__popcll(ma));
-      if (mb) bb = atomicAdd(&w.ctl->n_bacc, (uint32_t)__popcll(mb));
+    const uint32_t packed = (bin > B ? 1u : 0u) | ((bin == B ? 1u : 0u) << 16);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kSelBlock>(packed, s_w, &tot);
+    if (t == 0) {
+      s_base[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
+      s_base[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
     }
-    ba = __shfl(ba, 0, 64);
-    bb = __shfl(bb, 0, 64);
+    __syncthreads();
     if (bin > B) {
-      const uint32_t pos = c.n_sure + ba + lane_rank(ma);
+      const uint32_t pos = c.n_sure + s_base[0] + (ex & 0xFFFFu);
       const float v = u2f((uint32_t)e.y);
       a.vals[pos] = v;
       a.idx[pos] = e.x;
       a.r[e.x - base] = v - v;
     } else if (bin == B) {
-      blist[bb + lane_rank(mb)] = e;
+      blist[s_base[1] + (ex >> 16)] = e;
     }
+    __syncthreads();
   }
   // the list count: written by the last workgroup to finish (ticket), after every entry
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -152,10 +152,16 @@ class ShardedTopK:
             dist.all_gather_into_tensor(xh_all, xh, group=self.group)
         else:
             xh_all = xh
-        ok, B, need, cap_b, cap_p = plan_boundary(xh_all.cpu().numpy(), k, world, K.cand_cap(m, k))
+        # the exchange rows go to the host asynchronously; the dense output's zero-fill is queued
+        # behind them, so it runs on the GPU while the host plans the boundary
+        host = self._host_rows(xh_all)
+        out_len = m if self.dense == "shard" else n
+        out = K.fill_zero(K.empty(out_len, torch.float32, dev))
+        self._wait_host()
+        ok, B, need, cap_b, cap_p = plan_boundary(host.numpy(), k, world, K.cand_cap(m, k))
         self.last_fallback = not ok
         if not ok:
-            return self._fallback(res, base, n, k, sizes, world, vals, idx, dev)
+            return self._fallback(res, base, n, k, sizes, world, vals, idx, dev, out)
 
         bsend = K.empty(cap_b + 1, torch.int64, dev)
         K.route(res, base, k, B, vals, idx, bsend)
@@ -166,15 +172,31 @@ class ShardedTopK:
             brecv = bsend
         K.boundary(res, base, k, brecv, world, cap_b, need, vals, idx, cap_p)
         self.last_payload = (vals[:cap_p], idx[:cap_p])
-        return self._decode(vals, idx, cap_p, base, n, m, world, dev)
+        return self._decode(vals, idx, cap_p, base, n, m, world, dev, out)
 
-    def _decode(self, vals, idx, cap_p, base, n, m, world, dev):
+    def _host_rows(self, xh_all):
+        """Start the device->host copy of the exchange rows (pinned, non-blocking)."""
+        if not xh_all.is_cuda:
+            self._evt = None
+            return xh_all
+        buf = getattr(self, "_pinned", None)
+        if buf is None or buf.numel() != xh_all.numel():
+            buf = torch.empty(xh_all.numel(), dtype=xh_all.dtype, pin_memory=True)
+            self._pinned = buf
+        buf.copy_(xh_all, non_blocking=True)
+        self._evt = torch.cuda.Event()
+        self._evt.record()
+        return buf
+
+    def _wait_host(self):
+        if self._evt is not None:
+            self._evt.synchronize()
+
+    def _decode(self, vals, idx, cap_p, base, n, m, world, dev, out):
         K = self.k_ops
         if self.dense == "shard":
-            out = K.fill_zero(K.empty(m, torch.float32, dev))
             K.scatter_range(vals, idx, 0, cap_p, 1, base, out)
             return out
-        out = K.fill_zero(K.empty(n, torch.float32, dev))
         if world == 1:
             K.scatter_range(vals, idx, 0, cap_p, 1, 0, out)
             return out
@@ -186,7 +208,7 @@ class ShardedTopK:
         K.scatter_range(recv, recv[cap_p:].view(torch.int32), 2 * cap_p, cap_p, world, 0, out)
         return out
 
-    def _fallback(self, res, base, n, k, sizes, world, vals, idx, dev):
+    def _fallback(self, res, base, n, k, sizes, world, vals, idx, dev, out):
         """Exact path: the residual buffer holds t for every element after the main pass."""
         K = self.k_ops
         if world > 1:
@@ -202,11 +224,5 @@ class ShardedTopK:
         vals_all, idx_all = K.select_all(t_all, k)
         K.take(vals_all, idx_all, k, res, base, vals, idx, k)
         self.last_payload = (vals, idx)
-        m = res.numel()
-        if self.dense == "shard":
-            out = K.fill_zero(K.empty(m, torch.float32, dev))
-            K.scatter_range(vals_all, idx_all, 0, k, 1, base, out)
-        else:
-            out = K.fill_zero(K.empty(n, torch.float32, dev))
-            K.scatter_range(vals_all, idx_all, 0, k, 1, 0, out)
+        K.scatter_range(vals_all, idx_all, 0, k, 1, base if self.dense == "shard" else 0, out)
         return out

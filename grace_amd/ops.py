@@ -522,3 +522,50 @@ def scatter_range(vals, idx, stride, per, world, base, out):
     """out[idx - base] = 0 + v over `world` padded payloads (idx -1 = padding); out pre-zeroed."""
     _lib.call("grace_sparse_scatter_range", _p(vals), _p(idx), int(stride), int(per), int(world), int(base),
               out.numel(), _p(out), _stream())
+
+
+# ----------------------------------------------------------------------------- DGC
+def dgc_compress(t, ratio, sample_idx=None, seed=0):
+    """DgcCompressor.compress (dgc.py:12-43) of flat t: (values f32, indices int64, meta) where
+    meta (16 B, device) holds the final threshold for dgc_mask_update.  sample_idx: int64 device
+    indices (the reference's CPU uniform_ stream) or None for the device generator."""
+    t = dev_f32(t)
+    n = t.numel()
+    ns = max(1, int(n * 0.01))
+    ks = max(1, int(n * ratio * 0.01))
+    sample = torch.empty(ns, dtype=F32, device=t.device)
+    _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
+    _, top, _ = topk_compress(sample, min(ks, ns))
+    ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
+    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    meta = ws[:16].clone()
+    count = int(meta[8:12].view(torch.int32).item())          # host sync: the payload size
+    vals = torch.empty(count, dtype=F32, device=t.device)
+    idx = torch.empty(count, dtype=torch.int64, device=t.device)
+    if count:
+        _lib.call("grace_dgc_write", _p(t), n, _p(ws), _p(vals), _p(idx), _stream())
+    return vals, idx, meta
+
+
+def dgc_compensate(g, residual, accum, has_state, momentum):
+    _lib.call("grace_dgc_compensate", _p(dev_f32(g)), _p(residual), _p(accum), 1 if has_state else 0,
+              float(momentum), g.numel(), _stream())
+
+
+def dgc_mask_update(t, residual, accum, meta):
+    _lib.call("grace_dgc_mask_update", _p(dev_f32(t)), _p(residual), _p(accum), t.numel(), _p(meta), _stream())
+
+
+def sumsq(x):
+    x = dev_f32(x)
+    out = torch.empty(1, dtype=F32, device=x.device)
+    ws = workspace("sumsq", _lib.query("grace_sumsq_workspace_bytes"), x.device)
+    _lib.call("grace_sumsq", _p(x), x.numel(), _p(ws), _p(out), _stream())
+    return out
+
+
+def clip_by_sumsq(x, s, world):
+    x = dev_f32(x)
+    out = torch.empty_like(x)
+    _lib.call("grace_clip_by_sumsq", _p(x), _p(s), float(world), _p(out), x.numel(), _stream())
+    return out

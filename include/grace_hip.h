@@ -243,6 +243,32 @@ grace_status_t grace_topk_shard_read(const void* ws, uint32_t* ctl_host, void* s
 grace_status_t grace_sparse_scatter_range(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
                                           int32_t world, int64_t base, int64_t len, float* out, void* stream);
 
+/* ---- DGC (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39) -------------------------
+ * compress: grace_dgc_sample (|t| at the sampled indices: sample_idx from the caller = torch's
+ * CPU uniform_(0, numel).long() stream, or NULL = device generator) -> the k_s largest of the
+ * sample (grace_topk_compress) -> grace_dgc_threshold (sampled threshold, the 10-step adjustment
+ * replayed on exact counts, ordered-compaction offsets; the selected count is at ws + 8, u32)
+ * -> grace_dgc_write (values f32, indices int64, ascending).  The final threshold's bits are at
+ * ws + 4 (u32); grace_dgc_mask_update reads them from the first 16 bytes of `meta`. */
+size_t grace_dgc_workspace_bytes(int64_t n);
+grace_status_t grace_dgc_sample(const float* t, int64_t n, const int64_t* sample_idx, uint64_t seed, int64_t ns,
+                                float* sample_abs, void* stream);
+grace_status_t grace_dgc_threshold(const float* t, int64_t n, const float* top_vals, int64_t ks, double ratio,
+                                   void* ws, void* stream);
+grace_status_t grace_dgc_write(const float* t, int64_t n, const void* ws, float* vals, int64_t* idx, void* stream);
+/* memory: r = m r + g, a = a + r (has_state 0: r = a = g);  update: r *= keep, a *= keep with
+ * keep = !(|t| >= thr) (t may alias a) */
+grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accum, int32_t has_state,
+                                    float momentum, int64_t n, void* stream);
+grace_status_t grace_dgc_mask_update(const float* t, float* residual, float* accum, int64_t n, const void* meta,
+                                     void* stream);
+/* gradient clipping (memory/dgc.py:16-19): s = sum(x*x) (f64 accumulate) into out_dev; after the
+ * caller's all_reduce of s: out = clamp(x, -c, c), c = sqrt(s / world) */
+size_t grace_sumsq_workspace_bytes(void);
+grace_status_t grace_sumsq(const float* x, int64_t n, void* ws, float* out_dev, void* stream);
+grace_status_t grace_clip_by_sumsq(const float* x, const float* sumsq_dev, float world, float* out, int64_t n,
+                                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

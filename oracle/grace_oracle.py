@@ -387,3 +387,54 @@ def bucket_gbps(numel, seconds):
 
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["math"]
+
+
+# ------------------------------------------------------------------------------------------ DGC
+def dgc_compress(x, sample_idx, ratio):
+    """DgcCompressor.compress (grace_dl/dist/compressor/dgc.py:12-43) given the sampled indices
+    (torch.empty(ns).uniform_(0, numel).long()).  Returns (values f32, indices int64, mask, thr).
+    thr0 = min of the k_s largest |sample| (torch.topk puts NaN first; torch.min propagates NaN);
+    each adjustment is f32(1.3) * thr / f32(0.7) * thr, and the count is compared with the
+    Python double 1.3 * numel * ratio in f32 (torch promotes the int64 count with a float
+    scalar to the default dtype)."""
+    t = _f32(x).ravel()
+    numel = t.size
+    s = np.abs(t[np.asarray(sample_idx, dtype=np.int64)]).astype(F32)
+    k = max(1, int(numel * ratio * 0.01))
+    key = np.where(np.isnan(s), np.inf, s)
+    order = np.argsort(-key, kind="stable")
+    top = s[order[:k]]
+    thr = F32(np.min(top)) if not np.isnan(top).any() else F32(np.nan)
+    a = np.abs(t)
+    hi = F32(1.3 * numel * ratio)
+    lo = F32(0.7 * numel * ratio)
+    mask = a >= thr
+    sel = F32(mask.sum())
+    for _ in range(10):
+        if sel > hi:
+            thr = F32(F32(1.3) * thr)
+        elif sel < lo:
+            thr = F32(F32(0.7) * thr)
+        else:
+            break
+        mask = a >= thr
+        sel = F32(mask.sum())
+    idx = np.nonzero(mask)[0].astype(np.int64)
+    return t[idx].copy(), idx, mask, thr
+
+
+def dgc_memory_compensate(g, residual, accum, momentum):
+    """DgcMemory.compensate without clipping (memory/dgc.py:20-29): r = m r + g; a = a + r
+    (first step r = a = g).  Returns (t, r, a)."""
+    g = _f32(g).ravel()
+    if residual is None:
+        return g.copy(), g.copy(), g.copy()
+    r = (F32(momentum) * _f32(residual) + g).astype(F32)
+    a = (_f32(accum) + r).astype(F32)
+    return a.copy(), r, a
+
+
+def dgc_memory_update(residual, accum, mask):
+    """DgcMemory.update (memory/dgc.py:31-39): r * ~mask, a * ~mask (f32 multiply by 0/1)."""
+    keep = (~np.asarray(mask, dtype=bool)).astype(F32)
+    return (_f32(residual) * keep).astype(F32), (_f32(accum) * keep).astype(F32)

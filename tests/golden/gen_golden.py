@@ -399,6 +399,62 @@ def _rank2_worker(rank, path, outdir):
     d.destroy_process_group()
 
 
+def gen_dgc():
+    """DGC (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39).  The sample indices come
+    from torch's global CPU generator: seeded per case and re-drawn here for the fixture."""
+    from grace_dl.dist.compressor.dgc import DgcCompressor
+    from grace_dl.dist.memory.dgc import DgcMemory
+
+    init_world1()
+    st = Store("dgc")
+    inputs = [(f"n{n}", g_randn(n, 900 + n)) for n in (1, 129, 4099, 16411, 100003)]
+    inputs += [("ties", tied_vec(4099, 41)), ("s64x33", g_randn((64, 33), 42)),
+               ("nan", torch.cat([g_randn(3000, 43), torch.tensor([float("nan"), float("inf"), -float("inf")])])),
+               ("zeros", torch.zeros(2000))]
+    for case, x in inputs:
+        for ratio in (0.01, 0.1, 0.5):
+            seed = 1234 + len(st.cases)
+            numel = x.numel()
+            torch.manual_seed(seed)
+            sidx = torch.empty([max(1, int(numel * 0.01))]).uniform_(0, numel).type(torch.long)
+            comp = DgcCompressor(ratio)
+            torch.manual_seed(seed)
+            (vals, idx), ctx = comp.compress(x, "w")
+            dec = comp.decompress([vals, idx], ctx)
+            st.add(f"dgc_{case}_r{ratio}", {"codec": "dgc", "ratio": ratio, "seed": seed, "shape": list(x.shape)},
+                   x=x, sample_idx=sidx, vals=vals, idx=idx, mask=ctx[1].to(torch.uint8), dec=dec)
+    # DgcMemory(momentum 0.9, no clipping) + compressor, three steps (world 1)
+    for n, ratio in ((4099, 0.01), (16411, 0.05)):
+        comp, mem = DgcCompressor(ratio), DgcMemory(0.9, False, 1)
+        seq = {}
+        for s in range(3):
+            g = g_randn(n, 950 + s)
+            seed = 4321 + s
+            seq[f"g{s}"] = g.clone()
+            t = mem.compensate(g, "w")
+            seq[f"t{s}"] = t.clone()
+            numel = t.numel()
+            torch.manual_seed(seed)
+            seq[f"sidx{s}"] = torch.empty([max(1, int(numel * 0.01))]).uniform_(0, numel).type(torch.long)
+            torch.manual_seed(seed)
+            (vals, idx), ctx = comp.compress(t, "w")
+            mem.update(t, "w", comp, (vals, idx), ctx)
+            seq[f"vals{s}"], seq[f"idx{s}"] = vals, idx
+            seq[f"res{s}"] = mem.residuals["w"].clone()
+            seq[f"grad{s}"] = mem.gradients["w"].clone()
+            seq[f"seed{s}"] = torch.tensor([seed])
+        st.add(f"dgc_memory_n{n}_r{ratio}", {"codec": "dgc_memory", "ratio": ratio, "momentum": 0.9, "n": n,
+                                             "steps": 3}, **seq)
+    # gradient_clipping=True: dist.all_reduce returns None, so the reference raises (memory/dgc.py:17-18)
+    try:
+        DgcMemory(0.9, True, 1).compensate(g_randn(10, 1), "w")
+        clip_raises = False
+    except TypeError:
+        clip_raises = True
+    st.add("dgc_clipping_quirk", {"codec": "dgc_clip", "raises_type_error": clip_raises}, flag=np.array([clip_raises]))
+    st.save()
+
+
 def gen_world2():
     import torch.multiprocessing as mp
     st = Store("world2")
@@ -413,12 +469,16 @@ def gen_world2():
 
 if __name__ == "__main__":
     torch.manual_seed(0)
-    gen_sign()
-    gen_sparse()
-    gen_quant()
-    gen_powersgd()
-    gen_world2()
-    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+    only = sys.argv[1:]          # e.g. "dgc": regenerate just those fixtures
+    mpath = os.path.join(OUT, "manifest.json")
+    if only and os.path.exists(mpath):
+        with open(mpath) as f:
+            MANIFEST.update(json.load(f))
+    for name, fn in (("sign", gen_sign), ("sparse", gen_sparse), ("quant", gen_quant),
+                     ("powersgd", gen_powersgd), ("world2", gen_world2), ("dgc", gen_dgc)):
+        if not only or name in only:
+            fn()
+    with open(mpath, "w") as f:
         json.dump(MANIFEST, f, indent=1, sort_keys=True)
     if dist.is_initialized():
         dist.destroy_process_group()

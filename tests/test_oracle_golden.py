@@ -296,3 +296,28 @@ def test_world2_randomk_allreduce(golden):
     vals = ((r0["randk_g"].ravel()[idx] + r1["randk_g"].ravel()[idx]) / np.float32(2)).astype(np.float32)
     out = O.randomk_decode(vals, idx, 4099)
     assert same_bits(out, r0["randk_out"].ravel())
+
+
+def test_dgc_oracle_vs_reference(golden):
+    cases = golden.cases("dgc", codec="dgc")
+    assert cases
+    for c in cases:
+        vals, idx, mask, _ = O.dgc_compress(c["x"], c["sample_idx"], c.meta["ratio"])
+        assert np.array_equal(idx, c["idx"]), c.name
+        assert same_bits(vals, c["vals"]), c.name
+        assert np.array_equal(mask.astype(np.uint8), c["mask"].ravel()), c.name
+        assert same_bits(O.sparse_decode(vals, idx, c["x"].size), c["dec"].ravel()), c.name
+
+
+def test_dgc_memory_oracle_vs_reference(golden):
+    for c in golden.cases("dgc", codec="dgc_memory"):
+        r = a = None
+        for s in range(c.meta["steps"]):
+            t, r, a = O.dgc_memory_compensate(c[f"g{s}"], r, a, c.meta["momentum"])
+            assert same_bits(t, c[f"t{s}"]), (c.name, s)
+            vals, idx, mask, _ = O.dgc_compress(t, c[f"sidx{s}"], c.meta["ratio"])
+            assert np.array_equal(idx, c[f"idx{s}"]) and same_bits(vals, c[f"vals{s}"]), (c.name, s)
+            r, a = O.dgc_memory_update(r, a, mask)
+            assert same_bits(r, c[f"res{s}"]) and same_bits(a, c[f"grad{s}"]), (c.name, s)
+    quirk = golden.case("dgc", "dgc_clipping_quirk")
+    assert bool(quirk["flag"][0])   # the reference's gradient_clipping=True raises TypeError

@@ -29,6 +29,9 @@ def child():
     P = ops.powersgd_p(Ms[0], q)
     Q = ops.powersgd_qt(Ms[0], P)
     it = iter(range(10 ** 9))
+    A64 = torch.randn(64, 4, device="cuda")
+    A16k = torch.randn(16384, 4, device="cuda")
+    E = torch.empty(64, device="cuda")
     res = {
         "p": timeit(lambda: ops.powersgd_p(Ms[next(it) % 3], q)),
         "qt": timeit(lambda: ops.powersgd_qt(Ms[next(it) % 3], P)),
@@ -36,6 +39,9 @@ def child():
         "outer": timeit(lambda: ops.powersgd_outer(P, Q)),
         "qdraw": timeit(lambda: ops.normal_orthogonal((4096, 4), 5, "cuda")),
         "copy": timeit(lambda: Ms[1].copy_(Ms[next(it) % 2 * 2])),
+        "orth64": timeit(lambda: ops.orthogonalize_(A64)),
+        "orth16k": timeit(lambda: ops.orthogonalize_(A16k)),
+        "empty": timeit(lambda: ops.fill(E, 0.0)),
     }
     print(os.environ.get("GRACE_HIP_LIB", "default"), " ".join(f"{k}={v:.1f}us" for k, v in res.items()), flush=True)
 
