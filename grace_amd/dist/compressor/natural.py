@@ -41,6 +41,20 @@ class NaturalCompressor(Compressor):
                                       divisor=world_size if self.average else 1.0).view(shape)
 
 
+    # AllToAll hooks (grace_amd/dist/communicator/all_to_all.py): one launch per phase
+    def a2a_decode_sum(self, gathered, chunk, world_size):
+        codes, = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.natural_decompress(codes, chunk, self.flavour, world=world_size, aggregate=True)
+
+    def a2a_decode_concat(self, gathered, chunk, world_size):
+        codes, = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.natural_decompress(codes, world_size * chunk, self.flavour)
+
+
 class NaturalCompressor_CUDA(NaturalCompressor):
     flavour = 1
 

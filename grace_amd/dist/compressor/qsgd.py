@@ -53,6 +53,22 @@ class _QSGDBase(Compressor):
                                    divisor=world_size if self.average else 1.0).view(shape)
 
 
+    # AllToAll hooks (grace_amd/dist/communicator/all_to_all.py): one launch per phase
+    def a2a_decode_sum(self, gathered, chunk, world_size):
+        codes, norms = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.qsgd_decompress(codes, norms, self.quantum_num, self.bucket_size, chunk, variant=self.variant,
+                                   world=world_size, aggregate=True)
+
+    def a2a_decode_concat(self, gathered, chunk, world_size):
+        codes, norms = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.qsgd_decompress(codes, norms, self.quantum_num, self.bucket_size, world_size * chunk,
+                                   variant=self.variant)
+
+
 class QSGDCompressor(_QSGDBase):
     variant = 0
 

@@ -38,3 +38,16 @@ class TernGradCompressor(Compressor):
             return None
         return ops.terngrad_decompress(codes, scalars, shape.numel(), world=world_size, aggregate=True,
                                        divisor=world_size if self.average else 1.0).view(shape)
+
+    # AllToAll hooks (grace_amd/dist/communicator/all_to_all.py): one launch per phase
+    def a2a_decode_sum(self, gathered, chunk, world_size):
+        codes, scalars = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.terngrad_decompress(codes, scalars, chunk, world=world_size, aggregate=True)
+
+    def a2a_decode_concat(self, gathered, chunk, world_size):
+        codes, scalars = gathered
+        if not codes.is_cuda:
+            return None
+        return ops.terngrad_decompress(codes, scalars, world_size * chunk, sizes=[chunk] * world_size)

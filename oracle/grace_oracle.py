@@ -438,3 +438,49 @@ def dgc_memory_update(residual, accum, mask):
     """DgcMemory.update (memory/dgc.py:31-39): r * ~mask, a * ~mask (f32 multiply by 0/1)."""
     keep = (~np.asarray(mask, dtype=bool)).astype(F32)
     return (_f32(residual) * keep).astype(F32), (_f32(accum) * keep).astype(F32)
+
+
+# ------------------------------------------------------------------------------------------ AllToAll
+def alltoall_two_phase(grads, kind, u1, u2, quantum_num=127, bucket_size=128, average=True):
+    """AllToAll.send_receive (grace_dl/dist/communicator/all_to_all.py:29-124) for all W ranks at
+    once, with ZERO padding (the reference pads with torch.empty: uninitialised, see
+    grace_amd/dist/communicator/all_to_all.py).  grads[r]: rank r's gradient; u1[r] / u2[r]: the
+    uniforms of rank r's compress of its whole tensor and of its aggregated chunk.
+    kind 'qsgd' | 'terngrad'.  Returns the per-rank outputs (identical on every rank).
+    Parity of the communicator is unpinned (gloo has no list all_to_all, so the reference cannot
+    run here); the codecs it composes are pinned by their own golden vectors."""
+    W = len(grads)
+    n = _f32(grads[0]).size
+    unit = W * bucket_size if kind == "qsgd" else W
+    n_pad = -(-n // unit) * unit
+    chunk = n_pad // W
+
+    def compress(x, u):
+        if kind == "qsgd":
+            return qsgd_compress(x, u, quantum_num, bucket_size)
+        return terngrad_compress(x, u)
+
+    def decode(payload, numel):
+        if kind == "qsgd":
+            return qsgd_decode(payload[0], payload[1], quantum_num, bucket_size, numel)
+        return terngrad_decode(payload[0], payload[1])
+
+    pay = [compress(grads[r], u1[r]) for r in range(W)]
+    codes_p = [np.concatenate([p[0], np.zeros(n_pad - n, dtype=p[0].dtype)]) for p in pay]
+    agg = []
+    for r in range(W):       # rank r's chunk
+        decs = []
+        for w in range(W):
+            c = codes_p[w][r * chunk:(r + 1) * chunk]
+            if kind == "qsgd":
+                nb = chunk // bucket_size
+                norms = np.concatenate([pay[w][1], np.zeros(n_pad // bucket_size - pay[w][1].size, F32)])
+                decs.append(qsgd_decode(c, norms[r * nb:(r + 1) * nb], quantum_num, bucket_size, chunk))
+            else:
+                decs.append(terngrad_decode(c, pay[w][1]))
+        agg.append(python_sum(decs))
+    pay2 = [compress(agg[r], u2[r]) for r in range(W)]
+    full = np.concatenate([decode(pay2[r], chunk) for r in range(W)])[:n]
+    if average:
+        full = (full / F32(W)).astype(F32)
+    return full
