@@ -60,6 +60,14 @@ SIGNATURES = {
     "grace_sumsq_workspace_bytes": (SZ, []),
     "grace_sumsq": (ST, [P, I64, P, P, P]),
     "grace_clip_by_sumsq": (ST, [P, P, F32, P, I64, P]),
+    "grace_pack_bits": (ST, [P, I64, P, P]),
+    "grace_unpack_bits": (ST, [P, I64, P, P]),
+    "grace_sign_majority_bits": (ST, [P, I64, I32, I64, P, P]),
+    "grace_pack2_bytes": (I64, [I64]),
+    "grace_pack2": (ST, [P, I64, P, P]),
+    "grace_unpack2": (ST, [P, I64, P, P]),
+    "grace_tern_pack": (ST, [P, I64, P, P]),
+    "grace_tern_unpack": (ST, [P, I64, P, P]),
     "grace_sparse_decode": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_decode_i64": (ST, [P, P, I64, P, I64, P]),
     "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),

@@ -25,6 +25,8 @@ from grace_amd.dist._util import divide
 
 
 def _kind(compressor):
+    if getattr(compressor, "wire", "int8") not in ("int8", "u8"):
+        raise NotImplementedError("AllToAll chunks the element-wise codes: use the default wire format")
     kind = getattr(compressor, "a2a_kind", None)
     if kind:
         return kind

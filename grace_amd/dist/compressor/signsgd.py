@@ -1,5 +1,9 @@
 """signSGD (grace_dl/dist/compressor/signsgd.py:6-30): u8 codeword (x >= 0), decode 2c-1,
-majority-vote aggregate.  average=False as in the reference."""
+majority-vote aggregate.  average=False as in the reference.
+
+``wire='bits'`` sends the same codewords packed 1 bit per element (8x fewer bytes on the wire;
+grace_amd/csrc/wire.hip), and the Allgather majority vote runs on the packed payloads directly.
+The default ``wire='u8'`` is the reference's payload."""
 import torch
 
 from grace_amd import ops
@@ -8,14 +12,22 @@ from grace_amd.dist import Compressor
 
 class SignSGDCompressor(Compressor):
 
-    def __init__(self):
+    def __init__(self, wire="u8"):
         super().__init__(average=False)
+        if wire not in ("u8", "bits"):
+            raise ValueError("wire must be 'u8' or 'bits'")
+        self.wire = wire
 
     def compress(self, tensor, name):
-        return [ops.sign_encode(tensor)], tensor.size()
+        codes = ops.sign_encode(tensor)
+        if self.wire == "bits":
+            return [ops.pack_bits(codes)], tensor.size()
+        return [codes], tensor.size()
 
     def decompress(self, tensors, shape):
         sign_encode, = tensors
+        if self.wire == "bits":
+            sign_encode = ops.unpack_bits(sign_encode, shape.numel())
         return ops.sign_decode(sign_encode).view(shape)
 
     def aggregate(self, tensors):
@@ -31,6 +43,8 @@ class SignSGDCompressor(Compressor):
         if not codes.is_cuda:
             return None
         n = shape.numel()
+        if self.wire == "bits":
+            return ops.sign_majority_bits(codes, world_size, n).view(shape)
         return ops.sign_majority(codes, world_size, n).view(shape)
 
     def fused_step(self, communicator, tensor, name):

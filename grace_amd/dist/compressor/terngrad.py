@@ -4,6 +4,9 @@ Payload (codes int8[n] in {-1,0,1}, scalar f32[1]).  The std / max reductions ru
 device (the reference's f32 CPU reduction order is not reproducible on a GPU; the scalar agrees
 within a few ulp and codewords are bit-exact given the same clamp bound and uniforms, see
 tests/test_gpu_quant.py).  ``rng`` as for QSGD.
+``wire='2bit'`` sends the codes as code + 1 in the 2-bit byte layout of
+grace_dl/tensorflow/compressor/packing.py (4x fewer bytes); the default ``wire='int8'`` is the
+reference's payload.
 """
 import torch
 
@@ -13,9 +16,12 @@ from grace_amd.dist import Compressor
 
 class TernGradCompressor(Compressor):
 
-    def __init__(self, rng="device"):
+    def __init__(self, rng="device", wire="int8"):
         super().__init__()
+        if wire not in ("int8", "2bit"):
+            raise ValueError("wire must be 'int8' or '2bit'")
         self.rng = rng
+        self.wire = wire
         self._step = 0
 
     def compress(self, tensor, name):
@@ -26,15 +32,19 @@ class TernGradCompressor(Compressor):
         else:
             u, seed = None, ops.step_seed("terngrad", ops.rank_of_process(), name, self._step)
         codes, scalar = ops.terngrad_compress(flat, u=u, seed=seed)
+        if self.wire == "2bit":
+            codes = ops.tern_pack(codes)
         return (codes, scalar), tensor.size()
 
     def decompress(self, tensor_compressed, ctx):
         codes, scalar = tensor_compressed
+        if self.wire == "2bit":
+            codes = ops.tern_unpack(codes, ctx.numel())
         return ops.terngrad_decompress(codes, scalar, ctx.numel()).view(ctx)
 
     def decode_aggregate_gathered(self, gathered, shape, world_size):
         codes, scalars = gathered
-        if not codes.is_cuda:
+        if not codes.is_cuda or self.wire == "2bit":
             return None
         return ops.terngrad_decompress(codes, scalars, shape.numel(), world=world_size, aggregate=True,
                                        divisor=world_size if self.average else 1.0).view(shape)

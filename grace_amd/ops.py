@@ -569,3 +569,57 @@ def clip_by_sumsq(x, s, world):
     out = torch.empty_like(x)
     _lib.call("grace_clip_by_sumsq", _p(x), _p(s), float(world), _p(out), x.numel(), _stream())
     return out
+
+
+# ----------------------------------------------------------------------------- packed wire formats
+def pack_bits(codes):
+    """u8 {0,1} codes -> int32 words, bit i = code i (LSB first)."""
+    codes = require_dev(codes, "codes")
+    n = codes.numel()
+    words = torch.empty((n + 31) // 32, dtype=torch.int32, device=codes.device)
+    _lib.call("grace_pack_bits", _p(codes), n, _p(words), _stream())
+    return words
+
+
+def unpack_bits(words, n):
+    words = require_dev(words, "words")
+    codes = torch.empty(n, dtype=torch.uint8, device=words.device)
+    _lib.call("grace_unpack_bits", _p(words), n, _p(codes), _stream())
+    return codes
+
+
+def sign_majority_bits(words_wn, world, n):
+    words_wn = require_dev(words_wn, "words")
+    out = torch.empty(n, dtype=F32, device=words_wn.device)
+    _lib.call("grace_sign_majority_bits", _p(words_wn), (n + 31) // 32, int(world), n, _p(out), _stream())
+    return out
+
+
+def pack2(values):
+    values = require_dev(values, "values")
+    n = values.numel()
+    out = torch.empty(_lib.query("grace_pack2_bytes", n), dtype=torch.uint8, device=values.device)
+    _lib.call("grace_pack2", _p(values), n, _p(out), _stream())
+    return out
+
+
+def unpack2(packed, n):
+    packed = require_dev(packed, "packed")
+    out = torch.empty(n, dtype=torch.uint8, device=packed.device)
+    _lib.call("grace_unpack2", _p(packed), n, _p(out), _stream())
+    return out
+
+
+def tern_pack(codes):
+    codes = require_dev(codes, "codes")
+    n = codes.numel()
+    out = torch.empty(_lib.query("grace_pack2_bytes", n), dtype=torch.uint8, device=codes.device)
+    _lib.call("grace_tern_pack", _p(codes), n, _p(out), _stream())
+    return out
+
+
+def tern_unpack(packed, n):
+    packed = require_dev(packed, "packed")
+    out = torch.empty(n, dtype=torch.int8, device=packed.device)
+    _lib.call("grace_tern_unpack", _p(packed), n, _p(out), _stream())
+    return out

@@ -269,6 +269,21 @@ grace_status_t grace_sumsq(const float* x, int64_t n, void* ws, float* out_dev, 
 grace_status_t grace_clip_by_sumsq(const float* x, const float* sumsq_dev, float world, float* out, int64_t n,
                                    void* stream);
 
+/* ---- packed wire formats ------------------------------------------------
+ * 1-bit: sign codes u8 {0,1} <-> u32 words, bit i of the stream = code i (LSB first);
+ * majority decode (signsgd.py:24-30) straight from W packed payloads (rank w at + w * stride).
+ * 2-bit: grace_dl/tensorflow/compressor/packing.py:4-29 byte layout (planar quarters, pad values
+ * range(0, 4 - n % 4)); grace_pack2_bytes(n) output bytes.  TernGrad codes travel as code + 1. */
+grace_status_t grace_pack_bits(const uint8_t* codes, int64_t n, uint32_t* words, void* stream);
+grace_status_t grace_unpack_bits(const uint32_t* words, int64_t n, uint8_t* codes, void* stream);
+grace_status_t grace_sign_majority_bits(const uint32_t* words, int64_t stride_words, int32_t world, int64_t n,
+                                        float* out, void* stream);
+int64_t grace_pack2_bytes(int64_t n);
+grace_status_t grace_pack2(const uint8_t* values, int64_t n, uint8_t* packed, void* stream);
+grace_status_t grace_unpack2(const uint8_t* packed, int64_t n, uint8_t* values, void* stream);
+grace_status_t grace_tern_pack(const int8_t* codes, int64_t n, uint8_t* packed, void* stream);
+grace_status_t grace_tern_unpack(const uint8_t* packed, int64_t n, int8_t* codes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

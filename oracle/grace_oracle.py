@@ -484,3 +484,23 @@ def alltoall_two_phase(grads, kind, u1, u2, quantum_num=127, bucket_size=128, av
     if average:
         full = (full / F32(W)).astype(F32)
     return full
+
+
+# ------------------------------------------------------------------------------------------ wire formats
+def pack2_encode(values):
+    """grace_dl/tensorflow/compressor/packing.py:4-17 encode_byte: pad with range(0, 4 - n % 4)
+    (4 values when n % 4 == 0), split into 4 planar quarters, byte = a1 + 4 a2 + 16 a3 + 64 a4.
+    TensorFlow is absent here: restated from source, parity unpinned."""
+    a = np.asarray(values, dtype=np.int64).ravel()
+    pad = 4 - a.size % 4
+    a = np.concatenate([a, np.arange(pad, dtype=np.int64)])
+    q = a.size // 4
+    s = a[:q] + a[q:2 * q] * 4 + a[2 * q:3 * q] * 16 + a[3 * q:] * 64
+    return s.astype(np.uint8)
+
+
+def pack2_decode(encoded, real_size):
+    """packing.py:20-29 decode_byte."""
+    a = np.asarray(encoded, dtype=np.int64)
+    parts = [a % 4, (a // 4) % 4, (a // 16) % 4, (a // 64) % 4]
+    return np.concatenate(parts)[:real_size].astype(np.int32)
