@@ -20,6 +20,9 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   topk_sharded  ONE 256 MiB bucket sharded over the N ranks, top-k 0.1 % + residual, exact global
              selection (histogram exchange + boundary lists + payload allgather), replicated dense
              decode (configs[4]); value = 4n / step time (strong scaling: the bucket is fixed)
+  ddp_params / ddp_bucket  the DDP loopback harness (grace_amd/harness.py) on ResNet-50's 161
+             gradient tensors, top-k 1 % + residual: per-parameter grc.step loop
+             (examples/dist/CIFAR10-dawndist/core.py:204-208) vs one flat bucket
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
 
 Launch: ``python bench.py`` (N=1) or
@@ -48,7 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
-                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd"])
+                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd",
+                             "ddp_params", "ddp_bucket"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -103,7 +107,8 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
+           "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
     line = run(args, world, rank, dev)
     if rank == 0:
@@ -262,6 +267,30 @@ def bench_topk_sharded(args, world, rank, dev):
     line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                         "algorithmic_bytes_per_gpu": per_gpu}
+    return line
+
+
+def bench_ddp(args, world, rank, dev):
+    from grace_amd.dist.helper import grace_from_params
+    from grace_amd.harness import GradBucket, ShapeModel, step_bucketed, step_parameters
+    model = ShapeModel(resnet50_shapes(), dev)
+    bucket = GradBucket(model)
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
+                             "communicator": "allgather", "world_size": world})
+    bucket.flat.normal_()
+    if args.workload == "ddp_params":
+        fn = lambda i: step_parameters(model, grc)   # noqa: E731
+    else:
+        fn = lambda i: step_bucketed(bucket, grc)    # noqa: E731
+    fn(0)
+    elapsed = timed(fn, args.steps, args.warmup, world, dev)
+    total = bucket.flat.numel()
+    line = base_line(args, world, elapsed, 4.0 * total,
+                     metric=f"grad-codec GB/s, ResNet-50 gradients through the DDP loopback harness ({args.workload})")
+    line["config"] = {"workload": f"{'per-parameter grc.step loop' if args.workload == 'ddp_params' else 'one flat bucket'}"
+                                  f", Allgather(TopK 1 %, Residual), 161 ResNet-50 tensors", "numel": total,
+                      "tensors": len(bucket.params)}
+    line["roofline"] = None
     return line
 
 

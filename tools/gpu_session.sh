@@ -29,7 +29,7 @@ for step in "$@"; do
     pytopk) run pytest_topk 900 python3 -m pytest tests/test_gpu_topk.py -x -q ;;
     pytestall) run pytest_gpu_all 1200 python3 -m pytest tests -m gpu -q ;;
     bench)  run bench 600 python3 bench.py ;;
-    benchall) for wl in ${BENCH_WL:-sign sign256 qsgd terngrad powersgd topk_e2e topk_sharded}; do run "bench_$wl" 300 python3 bench.py --workload $wl; done ;;
+    benchall) for wl in ${BENCH_WL:-sign sign256 qsgd terngrad powersgd topk_e2e topk_sharded ddp_params ddp_bucket}; do run "bench_$wl" 300 python3 bench.py --workload $wl; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$ROOT/gpurun_out/prof_$TAG" -o bench -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
     profwl) for wl in ${PROF_WL:-sign qsgd terngrad powersgd}; do
