@@ -39,8 +39,14 @@ namespace grace {
 // dense outputs written by a top-k launch
 enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2 };
 
-constexpr int kMainBlock = 256;
-constexpr int kMainVec = 16;                               // float4 per thread
+#ifndef GRACE_MAIN_BLOCK
+#define GRACE_MAIN_BLOCK 256
+#endif
+#ifndef GRACE_MAIN_VEC
+#define GRACE_MAIN_VEC 16
+#endif
+constexpr int kMainBlock = GRACE_MAIN_BLOCK;
+constexpr int kMainVec = GRACE_MAIN_VEC;                   // float4 per thread
 constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 16384 elements per workgroup
 constexpr int kHistBins = 2048;                            // candidate histogram
 constexpr int kStage = 512;                                // LDS staging entries per list
@@ -352,24 +358,38 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 
+#ifndef GRACE_SAMPLE_PER
+#define GRACE_SAMPLE_PER 1
+#endif
+constexpr int kSamplePer = GRACE_SAMPLE_PER;               // samples per thread: 1 is fastest --
+                                                           // the strided samples are latency-bound
+                                                           // random loads that want many waves
+
 template <bool HAS_RES>
 __global__ __launch_bounds__(kSampleBlock) void topk_sample(StepArgs a, TopkWs w) {
   __shared__ uint32_t lh[kBracketBins];
   const int tid = threadIdx.x;
   STAMP(w.ctl, 0);
-  // issue the sample load first: its latency hides the LDS clear
-  const int64_t sidx = (int64_t)blockIdx.x * kSampleBlock + tid;
-  const bool valid = sidx < a.sample_n;
-  float t = 0.f;
-  if (valid) {
-    const uint32_t st = (uint32_t)a.stratum;
-    const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
-    t = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+  // issue every sample load first: their latency hides the LDS clear
+  const uint32_t st = (uint32_t)a.stratum;
+  float t[kSamplePer];
+  bool valid[kSamplePer];
+#pragma unroll
+  for (int p = 0; p < kSamplePer; ++p) {
+    const int64_t sidx = ((int64_t)blockIdx.x * kSamplePer + p) * kSampleBlock + tid;
+    valid[p] = sidx < a.sample_n;
+    t[p] = 0.f;
+    if (valid[p]) {
+      const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+      t[p] = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+    }
   }
   for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
   __syncthreads();
   STAMP(w.ctl, 1);
-  if (valid) atomicAdd(&lh[abs_key(t) >> 16], 1u);
+#pragma unroll
+  for (int p = 0; p < kSamplePer; ++p)
+    if (valid[p]) atomicAdd(&lh[abs_key(t[p]) >> 16], 1u);
   __syncthreads();
   for (int b = tid; b < kBracketBins; b += kSampleBlock)
     if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
@@ -462,7 +482,10 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
 // per lane).  Per group every lane counts its sure / candidate elements, one wave-wide prefix
 // scan (packed 16|16 bits) places them, and ONE LDS atomic per wave per group reserves staging
 // space; the staged entries leave with one global atomic per workgroup at the end.
-constexpr int kGroup = 4;
+#ifndef GRACE_MAIN_GROUP
+#define GRACE_MAIN_GROUP 4
+#endif
+constexpr int kGroup = GRACE_MAIN_GROUP;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
@@ -927,7 +950,8 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
   a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
   a.stratum = a.n / a.sample_n;
-  topk_sample<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
+  topk_sample<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock * kSamplePer - 1) / (kSampleBlock * kSamplePer)),
+                         kSampleBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_sample");
   topk_select<<<1, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_select");
@@ -1326,7 +1350,7 @@ grace_status_t grace_topk_shard_sample(const float* g, float* residual, int32_t 
   if (a.sample_n == 0) return GRACE_OK;
   TopkWs w{};
   w.shist = xs;
-  const unsigned grid = (unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock);
+  const unsigned grid = (unsigned)((a.sample_n + kSampleBlock * kSamplePer - 1) / (kSampleBlock * kSamplePer));
   if (has_residual) topk_sample<true><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
   else topk_sample<false><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
   GRACE_CHECK_LAUNCH("grace_topk_shard_sample");
