@@ -176,15 +176,14 @@ struct SignStepOp {
   const float* x; uint8_t* c; float* o;
   __device__ void vec(int64_t i) const {
     float4 v = reinterpret_cast<const float4*>(x)[i];
-    uint32_t w = pack_ge0(v);
-    reinterpret_cast<uint32_t*>(c)[i] = w;
+    if (c) reinterpret_cast<uint32_t*>(c)[i] = pack_ge0(v);   // codes optional (W=1 step)
     reinterpret_cast<float4*>(o)[i] =
         make_float4(v.x >= 0.f ? 1.f : -1.f, v.y >= 0.f ? 1.f : -1.f, v.z >= 0.f ? 1.f : -1.f,
                     v.w >= 0.f ? 1.f : -1.f);
   }
   __device__ void one(int64_t i) const {
     bool p = x[i] >= 0.f;
-    c[i] = (uint8_t)p;
+    if (c) c[i] = (uint8_t)p;
     o[i] = p ? 1.f : -1.f;
   }
 };
@@ -368,9 +367,9 @@ grace_status_t grace_signum_encode(const float* g, float* momentum, int32_t has_
 }
 
 grace_status_t grace_sign_step_w1(const float* x, uint8_t* codes, float* out, int64_t n, void* stream) {
-  GRACE_REQUIRE(n >= 0 && x && codes && out, "grace_sign_step_w1: bad arguments");
+  GRACE_REQUIRE(n >= 0 && x && out, "grace_sign_step_w1: bad arguments");
   return launch_stream("grace_sign_step_w1", SignStepOp{x, codes, out}, n,
-                       aligned16(x) && aligned4(codes) && aligned16(out), stream);
+                       aligned16(x) && (!codes || aligned4(codes)) && aligned16(out), stream);
 }
 
 size_t grace_reduce_workspace_bytes(int64_t n) {

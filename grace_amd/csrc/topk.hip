@@ -538,12 +538,12 @@ struct MainShared {
 
 template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void main_chunk(const StepArgs& a, const TopkWs& w, MainShared& sm,
-                                           uint32_t lo, uint32_t hi, uint32_t sh) {
+                                           uint32_t lo, uint32_t hi, uint32_t sh, int64_t chunk) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int64_t n = a.n;
   constexpr int NG = kMainVec / kGroup;
-  const int64_t cbase = (int64_t)blockIdx.x * kMainChunk + (int64_t)tid * 4;
+  const int64_t cbase = chunk * kMainChunk + (int64_t)tid * 4;
   float4 rc[kGroup], gc[kGroup];
   load_group<HAS_RES, FAST>(a, cbase, rc, gc);
 #pragma unroll 1
@@ -649,37 +649,43 @@ __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   __shared__ MainShared sm;
   const int tid = threadIdx.x;
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
-  if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
-  __syncthreads();
-  if (VEC && (int64_t)(blockIdx.x + 1) * kMainChunk <= a.n)
-    main_chunk<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh);
-  else
-    main_chunk<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh);
-  __syncthreads();
-  const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
-  const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
-  if (tid == 0) {
-    sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
-    sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
-  }
-  if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
-    const uint32_t all = sm.cnt[0];
-    if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
-    if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
-  }
-  __syncthreads();
-  for (uint32_t j = tid; j < ns; j += kMainBlock) {
-    const uint32_t gp = sm.cnt[1] + j;
-    if (gp < (uint32_t)a.k) {
-      const int2 e = sm.sure[j];
-      a.vals[gp] = u2f((uint32_t)e.y);
-      a.idx[gp] = e.x;
+  const int64_t nchunks = (a.n + kMainChunk - 1) / kMainChunk;
+  // grid-stride over chunks (gridDim.x == nchunks unless GRACE_MAIN_PERSIST caps the grid);
+  // the staged lists leave after every chunk (packed 16|16 counts), the histogram once at the end
+  for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    if (tid < 4) sm.cnt[tid] = 0;
+    __syncthreads();
+    if (VEC && (chunk + 1) * kMainChunk <= a.n)
+      main_chunk<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, chunk);
+    else
+      main_chunk<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, chunk);
+    __syncthreads();
+    const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
+    const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
+    if (tid == 0) {
+      sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
+      sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
     }
-  }
-  for (uint32_t j = tid; j < nc; j += kMainBlock) {
-    const uint32_t gp = sm.cnt[2] + j;
-    if (gp < (uint32_t)w.cap) w.cand[gp] = sm.cand[j];
+    if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
+      const uint32_t all = sm.cnt[0];
+      if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
+      if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < ns; j += kMainBlock) {
+      const uint32_t gp = sm.cnt[1] + j;
+      if (gp < (uint32_t)a.k) {
+        const int2 e = sm.sure[j];
+        a.vals[gp] = u2f((uint32_t)e.y);
+        a.idx[gp] = e.x;
+      }
+    }
+    for (uint32_t j = tid; j < nc; j += kMainBlock) {
+      const uint32_t gp = sm.cnt[2] + j;
+      if (gp < (uint32_t)w.cap) w.cand[gp] = sm.cand[j];
+    }
+    __syncthreads();
   }
   for (int b = tid; b < kHistBins; b += kMainBlock) {
     const uint32_t h = sm.hist[b];
@@ -955,7 +961,10 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   GRACE_CHECK_LAUNCH("topk_sample");
   topk_select<<<1, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_select");
-  const unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
+  unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
+#ifdef GRACE_MAIN_PERSIST
+  if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
+#endif
   {
     TimerScope ts(s);
     if (vec)
@@ -1186,11 +1195,20 @@ __global__ void scatter_add_tag_kernel(const float* vals, const int32_t* idx, in
     tags[i] = w;
   }
 }
-__global__ void tag_divide_kernel(const int32_t* idx, int64_t count, int32_t w, float divisor,
+// every aggregated element is divided exactly once: by the entry of the last rank that touched it
+// (tags[i] holds that rank after the ordered scatters).  One launch over all W payloads; the
+// per-rank prefix counts travel in the kernel arguments.
+constexpr int kMaxAggWorld = 64;
+struct AggCum { int64_t v[kMaxAggWorld + 1]; };
+
+__global__ void tag_divide_kernel(const int32_t* idx, int64_t stride, AggCum cum, int32_t world, float divisor,
                                   float* out, const int32_t* tags) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < count;
+  const int64_t total = cum.v[world];
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total;
        j += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t i = idx[j];
+    int w = 0;
+    while (w + 1 < world && cum.v[w + 1] <= j) ++w;
+    const int32_t i = idx[w * stride + (j - cum.v[w])];
     if (tags[i] == w) out[i] = out[i] / divisor;
   }
 }
@@ -1299,14 +1317,12 @@ grace_status_t grace_sparse_decode_i64(const float* vals, const int64_t* idx, in
   return GRACE_OK;
 }
 
-grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int64_t stride,
-                                      const int64_t* counts_host, int32_t world, float divisor,
-                                      float* out, int32_t* tags, int64_t n, void* stream) {
-  GRACE_REQUIRE(vals && idx && counts_host && out && tags && world >= 1 && n >= 0,
-                "grace_sparse_aggregate: bad arguments");
+grace_status_t grace_sparse_aggregate_into(const float* vals, const int32_t* idx, int64_t stride,
+                                           const int64_t* counts_host, int32_t world, float divisor,
+                                           float* out, int32_t* tags, int64_t n, void* stream) {
+  GRACE_REQUIRE(vals && idx && counts_host && out && tags && world >= 1 && world <= kMaxAggWorld && n >= 0,
+                "grace_sparse_aggregate: bad arguments (1 <= world <= 64)");
   hipStream_t s = as_stream(stream);
-  grace_status_t st = grace_fill(out, 0.f, n, stream);
-  if (st != GRACE_OK) return st;
   for (int w = 0; w < world; ++w) {
     const int64_t c = counts_host[w];
     if (c <= 0) continue;
@@ -1315,15 +1331,37 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
     GRACE_CHECK_LAUNCH("grace_sparse_aggregate");
   }
   if (divisor != 1.0f) {
-    for (int w = 0; w < world; ++w) {
-      const int64_t c = counts_host[w];
-      if (c <= 0) continue;
-      tag_divide_kernel<<<stream_grid(c, 256, 1024), 256, 0, s>>>(idx + w * stride, c, w, divisor, out,
-                                                                  tags);
+    for (int w0 = 0; w0 < world; w0 += kMaxAggWorld) {   // one launch per 64 ranks
+      const int nw = min(kMaxAggWorld, world - w0);
+      AggCum cum;
+      int64_t total = 0;
+      for (int w = 0; w < nw; ++w) {
+        cum.v[w] = total;
+        total += counts_host[w0 + w] > 0 ? counts_host[w0 + w] : 0;
+      }
+      cum.v[nw] = total;
+      if (total == 0) continue;
+      // tags hold absolute ranks: shift the tag base by w0 through the idx/tags comparison below
+      tag_divide_kernel<<<stream_grid(total, 256, 2048), 256, 0, s>>>(idx + w0 * stride, stride, cum, nw, divisor,
+                                                                       out, tags);
       GRACE_CHECK_LAUNCH("grace_sparse_aggregate");
+      if (w0 + nw < world) {
+        set_error_msg("grace_sparse_aggregate: more than 64 ranks per divide launch is not supported");
+        return GRACE_ERR_ARG;
+      }
     }
   }
   return GRACE_OK;
+}
+
+grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int64_t stride,
+                                      const int64_t* counts_host, int32_t world, float divisor,
+                                      float* out, int32_t* tags, int64_t n, void* stream) {
+  GRACE_REQUIRE(vals && idx && counts_host && out && tags && world >= 1 && n >= 0,
+                "grace_sparse_aggregate: bad arguments");
+  grace_status_t st = grace_fill(out, 0.f, n, stream);
+  if (st != GRACE_OK) return st;
+  return grace_sparse_aggregate_into(vals, idx, stride, counts_host, world, divisor, out, tags, n, stream);
 }
 
 
@@ -1375,7 +1413,10 @@ grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t ha
   StepArgs a{g, residual, beta, gamma, m, k, vals, idx, nullptr};
   a.idx_base = idx_base;
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual)) & 15u) == 0;
-  const unsigned nblk = (unsigned)((m + kMainChunk - 1) / kMainChunk);
+  unsigned nblk = (unsigned)((m + kMainChunk - 1) / kMainChunk);
+#ifdef GRACE_MAIN_PERSIST
+  if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
+#endif
   {
     TimerScope ts(s);
     if (has_residual) {

@@ -67,9 +67,11 @@ class TopKCompressor(Compressor):
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
         buf, _, _ = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None)
         mem.residuals[name] = res
+        # sort the local payload by index, exchange, then decode all W payloads in one pass over the
+        # output (grace_amd/csrc/payload.hip) instead of W random scatters
+        sbuf = ops.sort_payload(buf, k, n)
         gathered = torch.empty(world * 2 * k, dtype=torch.float32, device=g.device)
-        dist.all_gather_into_tensor(gathered, buf)
+        dist.all_gather_into_tensor(gathered, sbuf)
         divisor = world if self.average else 1
-        out = ops.sparse_aggregate(gathered, gathered[k:].view(torch.int32), 2 * k, [k] * world, world,
-                                   n, divisor)
+        out = ops.sparse_aggregate_sorted(gathered, k, world, n, divisor)
         return out.view(tensor.shape)

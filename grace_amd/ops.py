@@ -128,9 +128,9 @@ def signum_encode(g, momentum_buf, has_prev, momentum):
     return codes
 
 
-def sign_step_w1(x):
+def sign_step_w1(x, want_codes=True):
     x = dev_f32(x)
-    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device) if want_codes else None
     out = torch.empty_like(x)
     _lib.call("grace_sign_step_w1", _p(x), _p(codes), _p(out), x.numel(), _stream())
     return codes, out
@@ -221,18 +221,39 @@ def sparse_decode(vals, idx, n):
 _tags = {}
 
 
-def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor):
-    """Rank-ordered decode+aggregate of W sparse payloads laid out rank-major with `stride`."""
+def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out=None):
+    """Rank-ordered decode+aggregate of W sparse payloads laid out rank-major with `stride`.
+    With `out` given it must already be zero-filled (e.g. by a fill that overlapped the gather)."""
     dev = vals_base.device
     tags = _tags.get(str(dev))
     if tags is None or tags.numel() < n:
         tags = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         _tags[str(dev)] = tags
-    out = torch.empty(n, dtype=F32, device=dev)
+    prefilled = out is not None
+    if out is None:
+        out = torch.empty(n, dtype=F32, device=dev)
     import ctypes
     arr = (ctypes.c_int64 * world)(*[int(c) for c in counts])
-    _lib.call("grace_sparse_aggregate", _p(vals_base), _p(idx_base), int(stride), ctypes.addressof(arr),
-              int(world), float(divisor), _p(out), _p(tags), n, _stream())
+    _lib.call("grace_sparse_aggregate_into" if prefilled else "grace_sparse_aggregate", _p(vals_base), _p(idx_base),
+              int(stride), ctypes.addressof(arr), int(world), float(divisor), _p(out), _p(tags), n, _stream())
+    return out
+
+
+def sort_payload(buf, k, n):
+    """Packed payload [vals f32[k] | idx i32[k]] -> a new packed payload sorted by index."""
+    out = torch.empty_like(buf)
+    ws = workspace("sortpay", _lib.query("grace_sort_payload_workspace_bytes", k, n), buf.device)
+    _lib.call("grace_sort_payload", _p(buf), _p(buf[k:]), int(k), int(n), _p(out), _p(out[k:]), _p(ws), ws.numel(),
+              _stream())
+    return out
+
+
+def sparse_aggregate_sorted(gathered, k, world, n, divisor):
+    """Rank-ordered aggregate of W index-sorted packed payloads (rank-major, stride 2k)."""
+    out = torch.empty(n, dtype=F32, device=gathered.device)
+    ws = workspace("sortagg", _lib.query("grace_sorted_aggregate_workspace_bytes", n, world), gathered.device)
+    _lib.call("grace_sparse_aggregate_sorted", _p(gathered), _p(gathered[k:]), 2 * k, int(k), int(world),
+              float(divisor), _p(out), int(n), _p(ws), _stream())
     return out
 
 

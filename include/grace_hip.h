@@ -79,6 +79,7 @@ grace_status_t grace_sign_majority(const uint8_t* codes_wn, int32_t world, float
 grace_status_t grace_signum_encode(const float* g, float* momentum, int32_t has_prev, float coef_g,
                                    float coef_m, uint8_t* codes, int64_t n, void* stream);
 /* Fused signSGD step at world 1: codes = (x>=0), out = 2 c - 1 (aggregate of a single decode). */
+/* codes may be NULL (the world-1 step needs only the decoded output) */
 grace_status_t grace_sign_step_w1(const float* x, uint8_t* codes, float* out, int64_t n, void* stream);
 
 /* ------------------------------------------------------------------------------- reductions */
@@ -118,6 +119,24 @@ grace_status_t grace_sparse_decode_i64(const float* vals, const int64_t* idx, in
 /* Decode + aggregate of W gathered sparse payloads, exactly ((0 + d_0) + d_1 + ...) / divisor in
  * rank order (allgather.py:40-45).  vals/idx are rank-major [world][stride]; counts_host[w] is
  * rank w's payload length.  tags is an int32[n] scratch array (no initialisation needed). */
+/* world > 1 decode via chunk-grouped payloads (grace_amd/csrc/payload.hip): each rank groups its
+ * own payload by 8192-element output chunk before the exchange (grace_sort_payload: counting sort
+ * by chunk, n <= 2^28; ws = grace_sort_payload_workspace_bytes), then grace_sparse_aggregate_sorted writes
+ * out = (((0 + d_0) + d_1) + ...) / divisor densely in one pass over the output (no zero-fill,
+ * no per-rank scatter); ws = grace_sorted_aggregate_workspace_bytes(n, world).  Indices must be
+ * unique within each payload. */
+size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n);
+grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t k, int64_t n, float* vals_out,
+                                  int32_t* idx_out, void* ws, size_t ws_bytes, void* stream);
+size_t grace_sorted_aggregate_workspace_bytes(int64_t n, int32_t world);
+grace_status_t grace_sparse_aggregate_sorted(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
+                                             int32_t world, float divisor, float* out, int64_t n, void* ws,
+                                             void* stream);
+/* as grace_sparse_aggregate with `out` already zero-filled by the caller (lets the fill overlap
+ * the payload exchange); 1 <= world <= 64 */
+grace_status_t grace_sparse_aggregate_into(const float* vals, const int32_t* idx, int64_t stride,
+                                           const int64_t* counts_host, int32_t world, float divisor,
+                                           float* out, int32_t* tags, int64_t n, void* stream);
 grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int64_t stride,
                                       const int64_t* counts_host, int32_t world, float divisor,
                                       float* out, int32_t* tags, int64_t n, void* stream);

@@ -99,3 +99,43 @@ def test_threshold_allgather_world1_variable_path():
     assert same_bits(out, exp)
     res = _np(comm.memory.residuals["w"])
     assert same_bits(res, O.residual_update(x, O.sparse_decode(ov, oi, x.size)))
+
+
+@pytest.mark.parametrize("world,n,k", [(1, 4099, 40), (2, 100003, 1000), (3, (1 << 20) + 17, 20000),
+                                       (8, 5_000_000, 50000)])
+def test_sparse_aggregate_rank_ordered(world, n, k):
+    """Allgather decode + aggregate of W top-k payloads (allgather.py:40-45): bit-exact with the
+    Python sum of the dense decodes in rank order, divided by W -- with overlapping selections,
+    -0.0 and NaN values, and an output length that is not a multiple of the 4096-element chunk."""
+    from grace_amd import ops as G
+    rng = np.random.default_rng(world * 7 + k)
+    shared = rng.choice(n, k // 2, replace=False)          # indices every rank selects
+    vals_l, idx_l, decs = [], [], []
+    for w in range(world):
+        own = rng.choice(np.setdiff1d(np.arange(n), shared), k - shared.size, replace=False)
+        idx = rng.permutation(np.concatenate([shared, own])).astype(np.int32)
+        v = rng.standard_normal(k).astype(np.float32)
+        v[:5] = np.float32(-0.0)
+        v[5] = np.nan
+        vals_l.append(v)
+        idx_l.append(idx)
+        decs.append(O.sparse_decode(v, idx, n))
+    payload = np.concatenate([np.concatenate([v, i.view(np.float32)]) for v, i in zip(vals_l, idx_l)])
+    buf = _t(payload)
+    # chunk-grouped payloads (grace_sort_payload) for the one-pass aggregate
+    sorted_buf = torch.cat([G.sort_payload(buf[w * 2 * k:(w + 1) * 2 * k], k, n) for w in range(world)])
+    for w in range(world):
+        idx_s = _np(sorted_buf[w * 2 * k + k:(w + 1) * 2 * k].view(torch.int32))
+        vals_s = _np(sorted_buf[w * 2 * k:w * 2 * k + k])
+        assert np.all(np.diff(idx_s >> 13) >= 0)                       # grouped by 8192-chunk
+        order = np.argsort(idx_s)
+        assert np.array_equal(idx_s[order], np.sort(idx_l[w]))        # same entries
+        assert same_bits(vals_s[order], vals_l[w][np.argsort(idx_l[w])])
+    for divisor in (world, 1):
+        out = _np(G.sparse_aggregate(buf, buf[k:].view(torch.int32), 2 * k, [k] * world, world, n, divisor))
+        exp = O.python_sum(decs)
+        if divisor != 1:
+            exp = (exp / np.float32(divisor)).astype(np.float32)
+        assert same_bits(out, exp), (world, divisor)
+        out2 = _np(G.sparse_aggregate_sorted(sorted_buf, k, world, n, divisor))
+        assert same_bits(out2, exp), ("sorted", world, divisor)
