@@ -18,14 +18,22 @@ constexpr int kPChunkLog = 13;
 constexpr int kPChunk = 1 << kPChunkLog;
 constexpr int kPBlock = 256;
 
-constexpr int kGroupBlock = 1024;
-constexpr int kGroupPer = 16;                          // payload entries per thread
+#ifndef GRACE_GROUP_BLOCK
+#define GRACE_GROUP_BLOCK 256
+#endif
+constexpr int kGroupBlock = GRACE_GROUP_BLOCK;         // more, smaller workgroups: the payload is
+constexpr int kGroupPer = 16;                          // only ~0.7M entries; entries per thread
 constexpr int kMaxGroupChunks = 32768;                 // LDS histogram bins (128 KB): n <= 2^28
 
-// pass 1: per-workgroup LDS histogram of chunk ids, flushed with one atomic per non-zero bin
+// pass 1: per-workgroup LDS histogram of chunk ids, flushed with one atomic per non-zero bin; the
+// last workgroup to finish (ticket; agent-scope atomics, no L2 fences) scans the counts in place
+__device__ void scan_counts_block(uint32_t* counts, int64_t nchunks);
+
 __global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const int32_t* __restrict__ idx, int64_t k,
-                                                                int64_t nchunks, uint32_t* __restrict__ counts) {
+                                                                int64_t nchunks, uint32_t* __restrict__ counts,
+                                                                uint32_t* __restrict__ ticket) {
   extern __shared__ uint32_t h[];
+  __shared__ uint32_t s_last;
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kGroupBlock * kGroupPer;
@@ -37,17 +45,33 @@ __global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const int32_t* 
   __syncthreads();
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock)
     if (h[c]) atomicAdd(&counts[c], h[c]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_last) scan_counts_block(counts, nchunks);
 }
 
-// exclusive scan of the chunk counts in place (one workgroup)
-__global__ __launch_bounds__(1024) void group_scan_kernel(uint32_t* __restrict__ counts, int64_t nchunks) {
-  __shared__ uint32_t s_w[1024 / kWave + 1];
+// exclusive scan of the chunk counts in place by one workgroup (kScanPer counts per thread per
+// round); the counts were produced by device-scope atomics, so they are read with agent loads
+constexpr int kScanPer = 8;
+__device__ void scan_counts_block(uint32_t* counts, int64_t nchunks) {
+  constexpr int NT = kGroupBlock;
+  __shared__ uint32_t s_w[NT / kWave + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t run = 0;
-  for (int64_t c0 = 0; c0 < nchunks; c0 += 1024) {
-    const int64_t c = c0 + threadIdx.x;
-    const uint32_t v = c < nchunks ? counts[c] : 0u;
-    uint32_t inc = v;
+  for (int64_t c0 = 0; c0 < nchunks; c0 += NT * kScanPer) {
+    const int64_t cb = c0 + (int64_t)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+      v[e] = cb + e < nchunks ? __hip_atomic_load(counts + cb + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      sum += v[e];
+    }
+    uint32_t inc = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t t = __shfl_up(inc, o, 64);
@@ -57,12 +81,17 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(uint32_t* __restrict__
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t acc = 0;
-      for (int i = 0; i < 1024 / kWave; ++i) { const uint32_t t = s_w[i]; s_w[i] = acc; acc += t; }
-      s_w[1024 / kWave] = acc;
+      for (int i = 0; i < NT / kWave; ++i) { const uint32_t t = s_w[i]; s_w[i] = acc; acc += t; }
+      s_w[NT / kWave] = acc;
     }
     __syncthreads();
-    if (c < nchunks) counts[c] = run + s_w[w] + inc - v;
-    run += s_w[1024 / kWave];
+    uint32_t ex = run + s_w[w] + inc - sum;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+      if (cb + e < nchunks) counts[cb + e] = ex;
+      ex += v[e];
+    }
+    run += s_w[NT / kWave];
     __syncthreads();
   }
 }
@@ -162,7 +191,7 @@ extern "C" {
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
   (void)k;
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  return sizeof(uint32_t) * (size_t)nchunks + 256;
+  return sizeof(uint32_t) * (size_t)nchunks + 256 + 256;   // counts, then the ticket (zero between calls)
 }
 
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is
@@ -171,18 +200,18 @@ grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t
                                   int32_t* idx_out, void* ws, size_t ws_bytes, void* stream) {
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
   GRACE_REQUIRE(vals && idx && vals_out && idx_out && ws && k >= 0 && k < ((int64_t)1 << 31) && n >= 1 &&
-                    nchunks <= kMaxGroupChunks && ws_bytes >= sizeof(uint32_t) * (size_t)nchunks,
+                    nchunks <= kMaxGroupChunks && ws_bytes >= grace_sort_payload_workspace_bytes(k, n),
                 "grace_sort_payload: bad arguments (n <= 2^28)");
   if (k == 0) return GRACE_OK;
   hipStream_t s = as_stream(stream);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) +
+                                                 ((sizeof(uint32_t) * nchunks + 255) & ~(size_t)255));
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
   if (e != hipSuccess) { set_error("grace_sort_payload", e); return GRACE_ERR_HIP; }
   const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
   const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
-  group_hist_kernel<<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts);
-  GRACE_CHECK_LAUNCH("grace_sort_payload");
-  group_scan_kernel<<<1, 1024, 0, s>>>(counts, nchunks);
+  group_hist_kernel<<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
   GRACE_CHECK_LAUNCH("grace_sort_payload");
   group_scatter_kernel<<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, idx_out);
   GRACE_CHECK_LAUNCH("grace_sort_payload");
