@@ -32,6 +32,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 
 namespace grace {
@@ -55,7 +57,10 @@ constexpr int kSmallN = 32768;                             // single-workgroup p
 constexpr int kSampleRunLen = 16;
 constexpr int kSampleRuns = 2048;
 constexpr int kSample = kSampleRuns * kSampleRunLen;       // 32768 keys, 32 per thread
-constexpr int kFinBlocks = 64;
+#ifndef GRACE_FIN_BLOCKS
+#define GRACE_FIN_BLOCKS 64
+#endif
+constexpr int kFinBlocks = GRACE_FIN_BLOCKS;
 constexpr int kFinPer = 8;                                 // candidates per thread per round
 
 struct TopkCtl {
@@ -71,7 +76,8 @@ struct TopkCtl {
   uint32_t need;
   uint32_t ticket;     // finalize kernel arrival counter
   uint32_t n_bacc;     // boundary-list fill counter
-  uint32_t pad[4];
+  uint32_t bticket;    // bracket kernel arrival counter (reset by its last workgroup)
+  uint32_t pad[3];
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 
@@ -90,7 +96,10 @@ static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 #define STAMP(ctlp, slot) STAMP_IF(blockIdx.x == 0, ctlp, slot)
 
 constexpr int kXcnt = 8;                                   // sharded exchange counters
-constexpr int kSampleMax = 131072;                         // stratified sample size
+#ifndef GRACE_SAMPLE_MAX
+#define GRACE_SAMPLE_MAX 131072
+#endif
+constexpr int kSampleMax = GRACE_SAMPLE_MAX;               // stratified sample size
 constexpr int kSampleBlock = 1024;
 constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
 constexpr int kCursorStride = 32;                          // one placement cursor per 128-B line
@@ -151,19 +160,19 @@ static hipEvent_t g_ev[2 * kMaxEv];
 static int g_ev_created = 0;
 static int g_ev_used = 0;
 
-struct TimerScope {
-  hipStream_t s;
-  int slot = -1;
-  explicit TimerScope(hipStream_t st) : s(st) {
-    if (g_timer_on && g_ev_used < kMaxEv) {
-      slot = g_ev_used++;
-      hipEventRecord(g_ev[2 * slot], s);
-    }
+// With the timer on, the dominant kernel is launched with hipExtLaunchKernelGGL, whose start / stop
+// events ride on the kernel's own dispatch packet: no separate marker packets, so no extra
+// system-scope release (an L2 writeback of every XCD, ~6 us per hipEventRecord on gfx950) is
+// inserted between the step's kernels and the timed step is the untimed one.
+template <typename... KArgs, typename... Args>
+static void launch_timed(void (*kern)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
+  if (g_timer_on && g_ev_used < kMaxEv) {
+    const int slot = g_ev_used++;
+    hipExtLaunchKernelGGL(kern, grid, block, 0, s, g_ev[2 * slot], g_ev[2 * slot + 1], 0, args...);
+  } else {
+    kern<<<grid, block, 0, s>>>(args...);
   }
-  ~TimerScope() {
-    if (slot >= 0) hipEventRecord(g_ev[2 * slot + 1], s);
-  }
-};
+}
 
 // ------------------------------------------------------------------------------------------------
 // block-wide exclusive scan of one uint32 per thread (BLOCK threads, wave64)
@@ -407,23 +416,12 @@ __device__ __forceinline__ uint32_t chunk_sum_rot(const uint32_t* h, int t) {
   return s;
 }
 
-__global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
+// select body: lh = the whole sample histogram in LDS (kSelBlock threads)
+__device__ void bracket_select(const StepArgs& a, const TopkWs& w, uint32_t* lh) {
   constexpr int PER = kBracketBins / kSelBlock;   // 32
-  __shared__ uint32_t lh[kBracketBins];
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];
   __shared__ uint32_t s_res[4];
   const int tid = threadIdx.x;
-  STAMP(w.ctl, 3);
-  // coalesced copy of the global sample histogram into LDS, re-zeroing it behind us
-  const uint4* gh = reinterpret_cast<const uint4*>(w.shist);
-  uint4* lh4 = reinterpret_cast<uint4*>(lh);
-#pragma unroll
-  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) lh4[tid + j * kSelBlock] = gh[tid + j * kSelBlock];
-  __syncthreads();
-  uint4* gz = reinterpret_cast<uint4*>(w.shist);
-#pragma unroll
-  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
-  STAMP(w.ctl, 4);
   const int64_t S = a.sample_n;
   // sample ranks (descending, 0-based) bracketing the k-th largest with ~6 sigma
   const double p = (double)a.k / (double)a.n;
@@ -436,18 +434,27 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
   // descending scan: thread t owns the chunk of bins [PER*(NT-1-t), PER*(NT-1-t)+PER)
   const int chunk = kSelBlock - 1 - tid;
   const uint32_t sum = chunk_sum_rot<kSelBlock, kBracketBins>(lh, chunk);
-  if (tid < 4) s_res[tid] = 0;
+  __shared__ uint32_t s_fc[4];   // owning chunk and the count above it, per target rank
+  if (tid < 4) { s_res[tid] = 0; s_fc[tid] = 0; }
   const uint32_t ex = block_excl_scan<kSelBlock>(sum, s_w, nullptr);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (ex < r1[q] && r1[q] <= ex + sum) {
-      uint32_t acc = ex;
-      for (int j = PER - 1; j >= 0; --j) {
-        const uint32_t h = lh[chunk * PER + j];
-        if (acc + h >= r1[q]) { s_res[q] = (uint32_t)(chunk * PER + j); break; }
-        acc += h;
-      }
+  for (int q = 0; q < 2; ++q)
+    if (ex < r1[q] && r1[q] <= ex + sum) { s_fc[2 * q] = (uint32_t)chunk; s_fc[2 * q + 1] = ex; }
+  __syncthreads();
+  // the bin inside the owning chunk: one half-wave per target, inclusive scan of its 32 bins
+  // (descending) and the first lane whose running count reaches the rank
+  static_assert(PER == 32, "one half-wave per chunk");
+  if (tid < 64) {
+    const int q = tid >> 5, j = tid & 31;
+    const uint32_t bin = s_fc[2 * q] * PER + (PER - 1 - j);
+    uint32_t v = lh[bin];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t t = __shfl_up(v, o, 32);
+      if (j >= o) v += t;
     }
+    const uint32_t hm = (uint32_t)(__ballot(s_fc[2 * q + 1] + v >= r1[q]) >> (32 * q));
+    if (j == __ffs(hm) - 1) s_res[q] = bin;
   }
   __syncthreads();
   const uint32_t d0 = s_res[0], d1 = s_res[1];
@@ -471,7 +478,74 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
     w.ctl->thr_hi = hi;
     w.ctl->shift = sh;
   }
+}
+
+__global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
+  __shared__ uint32_t lh[kBracketBins];
+  const int tid = threadIdx.x;
+  STAMP(w.ctl, 3);
+  // coalesced copy of the global sample histogram into LDS, re-zeroing it behind us
+  const uint4* gh = reinterpret_cast<const uint4*>(w.shist);
+  uint4* lh4 = reinterpret_cast<uint4*>(lh);
+#pragma unroll
+  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) lh4[tid + j * kSelBlock] = gh[tid + j * kSelBlock];
+  __syncthreads();
+  uint4* gz = reinterpret_cast<uint4*>(w.shist);
+#pragma unroll
+  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
+  STAMP(w.ctl, 4);
+  bracket_select(a, w, lh);
   STAMP(w.ctl, 5);
+}
+
+// sample + select in ONE launch: the sample workgroups flush their LDS histograms with global
+// atomics, wait for them (vmcnt(0)) and take a ticket; the last to arrive reads the merged
+// histogram back with agent-scope loads (the other XCDs' atomics are not in its L2) and runs
+// the select.  Saves a launch and the inter-kernel drain of the two-kernel bracket.
+template <bool HAS_RES>
+__global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs w) {
+  __shared__ uint32_t lh[kBracketBins];
+  __shared__ uint32_t s_last;
+  const int tid = threadIdx.x;
+  STAMP(w.ctl, 0);
+  const uint32_t st = (uint32_t)a.stratum;
+  const int64_t sidx = (int64_t)blockIdx.x * kSampleBlock + tid;
+  const bool valid = sidx < a.sample_n;
+  float t = 0.f;
+  if (valid) {
+    const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+    t = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+  }
+  for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
+  __syncthreads();
+  STAMP(w.ctl, 1);
+  if (valid) atomicAdd(&lh[abs_key(t) >> 16], 1u);
+  __syncthreads();
+  for (int b = tid; b < kBracketBins; b += kSampleBlock)
+    if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
+  STAMP(w.ctl, 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&w.ctl->bticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  STAMP_IF(true, w.ctl, 3);
+  constexpr int kW64 = kBracketBins / 2 / kSelBlock;   // 16 x 8 B per thread
+  uint64_t* lh8 = reinterpret_cast<uint64_t*>(lh);
+  const uint64_t* gh8 = reinterpret_cast<const uint64_t*>(w.shist);
+  uint64_t v[kW64];
+#pragma unroll
+  for (int j = 0; j < kW64; ++j)
+    v[j] = __hip_atomic_load(gh8 + tid + j * kSelBlock, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int j = 0; j < kW64; ++j) lh8[tid + j * kSelBlock] = v[j];
+  __syncthreads();
+  uint4* gz = reinterpret_cast<uint4*>(w.shist);
+#pragma unroll
+  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
+  STAMP_IF(true, w.ctl, 4);
+  bracket_select(a, w, lh);   // zeroes the whole ctl block, bticket included
+  STAMP_IF(true, w.ctl, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -753,27 +827,35 @@ __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, u
 // over the whole bucket (slow, rare, same result).
 template <int MODE>
 __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint32_t need, uint32_t nb,
-                              uint32_t* hist, uint64_t* s_comp, uint32_t* s_w, uint32_t* s_res,
-                              uint32_t* s_pos) {
+                              uint32_t* hist, uint64_t* s_comp, int2* s_ent, uint32_t* s_w,
+                              uint32_t* s_res, uint32_t* s_pos) {
   const uint32_t k = (uint32_t)a.k;
   if (ok) {
     if (need == 0) return;
     const uint32_t pos0 = k - need;
     if (nb <= (uint32_t)kSelBlock) {
-      // rank by pairwise comparison of unique composites
+      // rank by pairwise comparison of unique composites; G adjacent lanes share one entry's
+      // comparisons (G = 4 at nb = 256) and combine their counts with xor-shuffles
       const int j = threadIdx.x;
-      int2 e = make_int2(0, 0);
-      uint64_t me = 0;
-      if (j < (int)nb) {
-        e = ld_agent_i2(w.bnd + j);
-        me = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
-        s_comp[j] = me;
+      const int nbi = (int)nb;
+      if (j < nbi) {
+        const int2 e = ld_agent_i2(w.bnd + j);
+        s_ent[j] = e;
+        s_comp[j] = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
       }
+      int G = 1;
+      while (G < 16 && nbi * (G * 2) <= kSelBlock) G *= 2;
       __syncthreads();
-      if (j < (int)nb) {
+      const int el = j / G, part = j % G;
+      if (el < nbi) {
+        const uint64_t me = s_comp[el];
         uint32_t rank = 0;
-        for (uint32_t q = 0; q < nb; ++q) rank += s_comp[q] > me;
-        if (rank < need) emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
+        for (int q = part; q < nbi; q += G) rank += s_comp[q] > me;
+        for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
+        if (part == 0 && rank < need) {
+          const int2 e = s_ent[el];
+          emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
+        }
       }
       return;
     }
@@ -809,6 +891,7 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
   __shared__ uint32_t s_base[kHistBins];
   __shared__ uint32_t hist[2048];
   __shared__ uint64_t s_comp[kSelBlock];
+  __shared__ int2 s_ent[kSelBlock];
   __shared__ uint32_t s_res[2];
   __shared__ int s_B;
   __shared__ uint32_t s_need, s_pos, s_last;
@@ -901,7 +984,7 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
   __syncthreads();
   if (!s_last) return;
   STAMP_IF(true, w.ctl, 11);
-  boundary_work<MODE>(a, w, ok, need, nb, hist, s_comp, s_w, s_res, &s_pos);
+  boundary_work<MODE>(a, w, ok, need, nb, hist, s_comp, s_ent, s_w, s_res, &s_pos);
   __syncthreads();
   STAMP_IF(true, w.ctl, 12);
 }
@@ -956,22 +1039,16 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
   a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
   a.stratum = a.n / a.sample_n;
-  topk_sample<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock * kSamplePer - 1) / (kSampleBlock * kSamplePer)),
-                         kSampleBlock, 0, s>>>(a, w);
-  GRACE_CHECK_LAUNCH("topk_sample");
-  topk_select<<<1, kSelBlock, 0, s>>>(a, w);
-  GRACE_CHECK_LAUNCH("topk_select");
+  topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
+  GRACE_CHECK_LAUNCH("topk_bracket");
   unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
 #ifdef GRACE_MAIN_PERSIST
   if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
 #endif
-  {
-    TimerScope ts(s);
-    if (vec)
-      topk_main<HAS_RES, MODE, true><<<nblk, kMainBlock, 0, s>>>(a, w);
-    else
-      topk_main<HAS_RES, MODE, false><<<nblk, kMainBlock, 0, s>>>(a, w);
-  }
+  if (vec)
+    launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
+  else
+    launch_timed(topk_main<HAS_RES, MODE, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
   GRACE_CHECK_LAUNCH("topk_main");
   topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_finalize");
@@ -1235,7 +1312,7 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
 grace_status_t grace_timer_enable(int enable) {
   if (enable && !g_ev_created) {
     for (int i = 0; i < 2 * kMaxEv; ++i) {
-      hipError_t e = hipEventCreate(&g_ev[i]);
+      hipError_t e = hipEventCreateWithFlags(&g_ev[i], hipEventDisableSystemFence);
       if (e != hipSuccess) {
         set_error("grace_timer_enable", e);
         return GRACE_ERR_HIP;
@@ -1417,15 +1494,12 @@ grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t ha
 #ifdef GRACE_MAIN_PERSIST
   if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
 #endif
-  {
-    TimerScope ts(s);
-    if (has_residual) {
-      if (vec) topk_main<true, kDenseRes, true><<<nblk, kMainBlock, 0, s>>>(a, w);
-      else topk_main<true, kDenseRes, false><<<nblk, kMainBlock, 0, s>>>(a, w);
-    } else {
-      if (vec) topk_main<false, kDenseRes, true><<<nblk, kMainBlock, 0, s>>>(a, w);
-      else topk_main<false, kDenseRes, false><<<nblk, kMainBlock, 0, s>>>(a, w);
-    }
+  if (has_residual) {
+    if (vec) launch_timed(topk_main<true, kDenseRes, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
+    else launch_timed(topk_main<true, kDenseRes, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
+  } else {
+    if (vec) launch_timed(topk_main<false, kDenseRes, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
+    else launch_timed(topk_main<false, kDenseRes, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
   }
   GRACE_CHECK_LAUNCH("grace_topk_shard_main");
   return GRACE_OK;
