@@ -102,7 +102,7 @@ constexpr int kXcnt = 8;                                   // sharded exchange c
 constexpr int kSampleMax = GRACE_SAMPLE_MAX;               // stratified sample size
 constexpr int kSampleBlock = 1024;
 constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
-constexpr int kCursorStride = 32;                          // one placement cursor per 128-B line
+constexpr int kCoarseBins = 2048;                          // key >> 20: 1/8-octave bins
 constexpr int kHistStride = 1;
 
 // Workspace layout.  Every counter / histogram region is left zeroed by the step that used it
@@ -111,8 +111,8 @@ constexpr int kHistStride = 1;
 struct TopkWs {
   TopkCtl* ctl;
   uint32_t* hist;      // candidate histogram [kHistBins]
-  uint32_t* cursor;    // per-bin placement cursors [kHistBins * kCursorStride]
-  uint32_t* shist;     // sample histogram [kBracketBins]
+  uint32_t* chist;     // coarse sample histogram [kCoarseBins] (single-GPU bracket)
+  uint32_t* shist;     // fine sample histogram [kBracketBins]
   int2* cand;
   int2* bnd;
   int64_t cap;
@@ -134,8 +134,8 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   p += 256;
   w.hist = reinterpret_cast<uint32_t*>(p);
   p += align256(sizeof(uint32_t) * kHistBins * kHistStride);
-  w.cursor = reinterpret_cast<uint32_t*>(p);
-  p += align256(sizeof(uint32_t) * kHistBins * kCursorStride);
+  w.chist = reinterpret_cast<uint32_t*>(p);
+  p += align256(sizeof(uint32_t) * kCoarseBins);
   w.shist = reinterpret_cast<uint32_t*>(p);
   p += align256(sizeof(uint32_t) * kBracketBins);
   w.cand = reinterpret_cast<int2*>(p);
@@ -148,7 +148,7 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
 static size_t ws_bytes(int64_t n, int64_t k) {
   const int64_t cap = topk_cap(n, k);
   return 256 + align256(sizeof(uint32_t) * kHistBins * kHistStride) +
-         align256(sizeof(uint32_t) * kHistBins * kCursorStride) + align256(sizeof(uint32_t) * kBracketBins) +
+         align256(sizeof(uint32_t) * kCoarseBins) + align256(sizeof(uint32_t) * kBracketBins) +
          2 * align256(sizeof(int2) * cap);
 }
 
@@ -370,6 +370,11 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 #ifndef GRACE_SAMPLE_PER
 #define GRACE_SAMPLE_PER 1
 #endif
+#ifndef GRACE_SAMPLE_DEFF
+#define GRACE_SAMPLE_DEFF 1.0
+#endif
+// variance inflation allowed for in the bracket's margin (design effect of clustered samples)
+constexpr double kSampleDeff = GRACE_SAMPLE_DEFF;
 constexpr int kSamplePer = GRACE_SAMPLE_PER;               // samples per thread: 1 is fastest --
                                                            // the strided samples are latency-bound
                                                            // random loads that want many waves
@@ -426,7 +431,7 @@ __device__ void bracket_select(const StepArgs& a, const TopkWs& w, uint32_t* lh)
   // sample ranks (descending, 0-based) bracketing the k-th largest with ~6 sigma
   const double p = (double)a.k / (double)a.n;
   const double mu = p * (double)S;
-  const double sd = sqrt(mu * (1.0 - p) + 1.0);
+  const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
   const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
   const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
   const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
@@ -459,7 +464,7 @@ __device__ void bracket_select(const StepArgs& a, const TopkWs& w, uint32_t* lh)
   __syncthreads();
   const uint32_t d0 = s_res[0], d1 = s_res[1];
   // re-zero the state the next kernels accumulate into
-  for (int b = tid; b < kHistBins; b += kSelBlock) { w.hist[b * kHistStride] = 0; w.cursor[b * kCursorStride] = 0; }
+  for (int b = tid; b < kHistBins; b += kSelBlock) w.hist[b * kHistStride] = 0;
   if (tid < (int)(sizeof(TopkCtl) / 4)) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
   if (w.xcnt && tid < kXcnt) w.xcnt[tid] = 0u;
   __syncthreads();
@@ -498,13 +503,21 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
   STAMP(w.ctl, 5);
 }
 
-// sample + select in ONE launch: the sample workgroups flush their LDS histograms with global
-// atomics, wait for them (vmcnt(0)) and take a ticket; the last to arrive reads the merged
-// histogram back with agent-scope loads (the other XCDs' atomics are not in its L2) and runs
-// the select.  Saves a launch and the inter-kernel drain of the two-kernel bracket.
+// Single-GPU bracket: sample + select in ONE launch.  The sample workgroups count their keys into
+// a fine (key >> 16, 32768 bins) and a coarse (key >> 20, 2048 bins) LDS histogram and flush both
+// with global atomics, wait for them (vmcnt(0)) and take a ticket; the last to arrive reads the
+// merged COARSE histogram back with agent-scope loads (the other XCDs' atomics are not in its L2),
+// finds the coarse bin of each bracketing rank, then reads only those bins' 16 fine counts.
+// Nothing on this path waits on re-zeroing: the sample workgroups zero the counters the main pass
+// accumulates into (the previous step's finalize has completed, stream order), and the finalize
+// kernel zeroes both sample histograms once the main pass no longer needs them.
 template <bool HAS_RES>
 __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs w) {
   __shared__ uint32_t lh[kBracketBins];
+  __shared__ uint32_t lc[kCoarseBins];
+  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
+  __shared__ uint32_t s_fc[4];
+  __shared__ uint32_t s_res[2];
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
   STAMP(w.ctl, 0);
@@ -514,15 +527,30 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   float t = 0.f;
   if (valid) {
     const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+#ifdef GRACE_SAMPLE_SEQ   // diagnostic A/B build only: contiguous sample positions
+    t = compensate<HAS_RES>(a, sidx + 0 * off);
+#else
     t = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+#endif
   }
+  // counters of this step's main / finalize passes (their previous users have completed)
+  if (blockIdx.x == 0 && tid >= 3 && tid < 12) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
+  if (blockIdx.x < (unsigned)(kHistBins / kSampleBlock))
+    w.hist[(blockIdx.x * kSampleBlock + tid) * kHistStride] = 0u;
   for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
+  for (int b = tid; b < kCoarseBins; b += kSampleBlock) lc[b] = 0;
   __syncthreads();
   STAMP(w.ctl, 1);
-  if (valid) atomicAdd(&lh[abs_key(t) >> 16], 1u);
+  if (valid) {
+    const uint32_t key = abs_key(t);
+    atomicAdd(&lh[key >> 16], 1u);
+    atomicAdd(&lc[key >> 20], 1u);
+  }
   __syncthreads();
   for (int b = tid; b < kBracketBins; b += kSampleBlock)
     if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
+  for (int b = tid; b < kCoarseBins; b += kSampleBlock)
+    if (lc[b]) atomicAdd(&w.chist[b], lc[b]);
   STAMP(w.ctl, 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -530,21 +558,63 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   __syncthreads();
   if (!s_last) return;
   STAMP_IF(true, w.ctl, 3);
-  constexpr int kW64 = kBracketBins / 2 / kSelBlock;   // 16 x 8 B per thread
-  uint64_t* lh8 = reinterpret_cast<uint64_t*>(lh);
-  const uint64_t* gh8 = reinterpret_cast<const uint64_t*>(w.shist);
-  uint64_t v[kW64];
+  // sample ranks (descending, 0-based) bracketing the k-th largest with ~6 sigma
+  const int64_t S = a.sample_n;
+  const double p = (double)a.k / (double)a.n;
+  const double mu = p * (double)S;
+  const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
+  const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
+  const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
+  const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
+                          (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1)};
+  // coarse: thread t owns bins top, top-1 (descending); one block scan finds both coarse bins
+  static_assert(kCoarseBins == 2 * kSampleBlock, "two coarse bins per thread");
+  const int top = kCoarseBins - 1 - 2 * tid;
+  const uint32_t h0 = __hip_atomic_load(w.chist + top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t h1 = __hip_atomic_load(w.chist + top - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 4) s_fc[tid] = 0;
+  const uint32_t ex = block_excl_scan<kSelBlock>(h0 + h1, s_w, nullptr);
 #pragma unroll
-  for (int j = 0; j < kW64; ++j)
-    v[j] = __hip_atomic_load(gh8 + tid + j * kSelBlock, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int j = 0; j < kW64; ++j) lh8[tid + j * kSelBlock] = v[j];
+  for (int q = 0; q < 2; ++q)
+    if (ex < r1[q] && r1[q] <= ex + h0 + h1) {
+      const bool first = r1[q] <= ex + h0;
+      s_fc[2 * q] = (uint32_t)(first ? top : top - 1);
+      s_fc[2 * q + 1] = first ? ex : ex + h0;
+    }
   __syncthreads();
-  uint4* gz = reinterpret_cast<uint4*>(w.shist);
+  // fine: one 16-lane group per target rank, inclusive scan of the coarse bin's 16 fine bins
+  // (descending) and the first lane whose running count reaches the rank
+  if (tid < 64) {
+    const int q = (tid >> 4) & 1, j = tid & 15;
+    const uint32_t bin = s_fc[2 * q] * 16 + (15 - j);
+    uint32_t v = tid < 32 ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
-  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
+    for (int o = 1; o < 16; o <<= 1) {
+      const uint32_t u = __shfl_up(v, o, 16);
+      if (j >= o) v += u;
+    }
+    const uint64_t bal = __ballot(tid < 32 && s_fc[2 * q + 1] + v >= r1[q]);
+    const uint32_t hm = (uint32_t)(bal >> (16 * q)) & 0xFFFFu;
+    if (tid < 32 && j == __ffs(hm) - 1) s_res[q] = bin;
+  }
+  __syncthreads();
   STAMP_IF(true, w.ctl, 4);
-  bracket_select(a, w, lh);   // zeroes the whole ctl block, bticket included
+  if (tid == 0) {
+    // sure = key > hi: round up to the top of the fine bin (fewer sure); candidates start at the
+    // bottom of the low bin (more candidates)
+    uint32_t hi = (s_res[0] << 16) | 0xFFFFu;
+    uint32_t lo = s_res[1] << 16;
+    if (rank_hi < 0) hi = 0x7FFFFFFFu;
+    if (rank_lo >= S) lo = 0u;
+    if (lo > hi) lo = hi;
+    uint32_t sh = 0;
+    const uint64_t span = (uint64_t)hi - (uint64_t)lo;   // keys lo..hi -> bins 0..span>>sh
+    while ((span >> sh) >= (uint64_t)kHistBins) ++sh;
+    w.ctl->thr_lo = lo;
+    w.ctl->thr_hi = hi;
+    w.ctl->shift = sh;
+    w.ctl->bticket = 0u;
+  }
   STAMP_IF(true, w.ctl, 5);
 }
 
@@ -560,6 +630,7 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
 #define GRACE_MAIN_GROUP 4
 #endif
 constexpr int kGroup = GRACE_MAIN_GROUP;
+
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
@@ -610,14 +681,97 @@ struct MainShared {
   uint32_t cnt[4];   // packed staged counts (sure | cand << 16), base_sure, base_cand
 };
 
+// v2 classification of one group (kGroup float4 per lane per array, already loaded): per-lane LDS
+// reservation (one ds_add_rtn of the packed 16|16 counts by each lane that has entries, no wave
+// scan), one branch per flagged element position for both lists; the candidate histogram is built
+// from the staged entries at the flush instead of a masked ds_add per element in the stream.
 template <bool HAS_RES, int MODE, bool FAST>
-__device__ __forceinline__ void main_chunk(const StepArgs& a, const TopkWs& w, MainShared& sm,
-                                           uint32_t lo, uint32_t hi, uint32_t sh, int64_t chunk) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
+__device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                               uint32_t hi, uint32_t sh, int64_t gbase,
+                                               const float4 (&rc)[kGroup], const float4 (&gc)[kGroup]) {
   const int64_t n = a.n;
+  float4 t[kGroup];
+  uint32_t msure = 0, mcand = 0;   // bit u*4+j
+#pragma unroll
+  for (int u = 0; u < kGroup; ++u) {
+    if constexpr (HAS_RES) {
+      t[u].x = a.beta * rc[u].x + a.gamma * gc[u].x;
+      t[u].y = a.beta * rc[u].y + a.gamma * gc[u].y;
+      t[u].z = a.beta * rc[u].z + a.gamma * gc[u].z;
+      t[u].w = a.beta * rc[u].w + a.gamma * gc[u].w;
+    } else {
+      t[u] = gc[u];
+    }
+    const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
+    float4 rout = t[u], dout = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float tv = comp4(t[u], j);
+      const uint32_t key = abs_key(tv);
+      const bool valid = FAST || i0 + j < n;
+#ifdef GRACE_MAIN_STREAM_ONLY   // diagnostic A/B build only: the streaming ceiling of this layout
+      const bool sure = valid && key > 0x7F800000u, cand = false;
+#else
+      const bool sure = valid && key > hi;
+      const bool cand = valid && !sure && key >= lo;
+#endif
+      msure |= (uint32_t)sure << (u * 4 + j);
+      mcand |= (uint32_t)cand << (u * 4 + j);
+      if constexpr (MODE == kDenseFused) {
+        if (sure) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
+      }
+    }
+    if constexpr (MODE == kDenseRes || MODE == kDenseFused) st4<FAST>(a.r, i0, n, rout);
+    if constexpr (MODE == kDenseFused) st4<FAST>(a.out, i0, n, dout);
+  }
+  const uint32_t msel = msure | mcand;
+  if (msel) {
+    const uint32_t cs = __popc(msure), cc = __popc(mcand);
+    const uint32_t bse = atomicAdd(&sm.cnt[0], cs | (cc << 16));
+    uint32_t ps = bse & 0xFFFFu, pc = bse >> 16;
+    // entries past kStage spill to the global lists (rare: one global atomic per spilling lane)
+    const uint32_t over_s = ps + cs > (uint32_t)kStage ? min(ps + cs - (uint32_t)kStage, cs) : 0u;
+    const uint32_t over_c = pc + cc > (uint32_t)kStage ? min(pc + cc - (uint32_t)kStage, cc) : 0u;
+    uint32_t gs = 0, gcn = 0;
+    if (over_s) gs = atomicAdd(&w.ctl->n_sure, over_s);
+    if (over_c) gcn = atomicAdd(&w.ctl->n_cand, over_c);
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b = u * 4 + j;
+        if ((msel >> b) & 1u) {
+          const int64_t i = gbase + (int64_t)u * (kMainBlock * 4) + j;
+          const float tv = comp4(t[u], j);
+          const int2 e = make_int2((int)(i + a.idx_base), (int)f2u(tv));
+          if ((msure >> b) & 1u) {
+            if (ps < (uint32_t)kStage) {
+              sm.sure[ps] = e;
+            } else if (gs < (uint32_t)a.k) {
+              a.vals[gs] = tv; a.idx[gs] = e.x; ++gs;
+            }
+            ++ps;
+          } else {
+            if (pc < (uint32_t)kStage) {
+              sm.cand[pc] = e;
+            } else {
+              atomicAdd(&sm.hist[(abs_key(tv) - lo) >> sh], 1u);
+              if (gcn < (uint32_t)w.cap) w.cand[gcn] = e;
+              ++gcn;
+            }
+            ++pc;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <bool HAS_RES, int MODE, bool FAST>
+__device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
+                                              uint32_t lo, uint32_t hi, uint32_t sh, int64_t chunk) {
   constexpr int NG = kMainVec / kGroup;
-  const int64_t cbase = chunk * kMainChunk + (int64_t)tid * 4;
+  const int64_t cbase = chunk * kMainChunk + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
   load_group<HAS_RES, FAST>(a, cbase, rc, gc);
 #pragma unroll 1
@@ -625,96 +779,87 @@ __device__ __forceinline__ void main_chunk(const StepArgs& a, const TopkWs& w, M
     const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
     float4 rn[kGroup], gn[kGroup];
     if (q + 1 < NG) load_group<HAS_RES, FAST>(a, gbase + kGroup * (kMainBlock * 4), rn, gn);
-    float4 t[kGroup];
-    uint32_t msure = 0, mcand = 0;   // bit u*4+j
-#pragma unroll
-    for (int u = 0; u < kGroup; ++u) {
-      if constexpr (HAS_RES) {
-        t[u].x = a.beta * rc[u].x + a.gamma * gc[u].x;
-        t[u].y = a.beta * rc[u].y + a.gamma * gc[u].y;
-        t[u].z = a.beta * rc[u].z + a.gamma * gc[u].z;
-        t[u].w = a.beta * rc[u].w + a.gamma * gc[u].w;
-      } else {
-        t[u] = gc[u];
-      }
-      const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
-      float4 rout = t[u], dout = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float tv = comp4(t[u], j);
-        const uint32_t key = abs_key(tv);
-        const bool valid = FAST || i0 + j < n;
-        const bool sure = valid && key > hi;
-        const bool cand = valid && !sure && key >= lo;
-        msure |= (uint32_t)sure << (u * 4 + j);
-        mcand |= (uint32_t)cand << (u * 4 + j);
-        if constexpr (MODE == kDenseFused) {
-          if (sure) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
-        }
-        if (cand) atomicAdd(&sm.hist[(key - lo) >> sh], 1u);
-      }
-      if constexpr (MODE == kDenseRes || MODE == kDenseFused) st4<FAST>(a.r, i0, n, rout);
-      if constexpr (MODE == kDenseFused) st4<FAST>(a.out, i0, n, dout);
-    }
-    // ---- place this group's sure / candidate elements
-    const uint32_t cs = __popc(msure), cc = __popc(mcand);
-    const uint32_t packed = cs | (cc << 16);
-    if (__ballot(packed != 0)) {
-      const uint32_t incl = wave_incl_scan(packed);
-      const uint32_t excl = incl - packed;
-      uint32_t bse = 0;
-      if (lane == 63) bse = atomicAdd(&sm.cnt[0], incl);
-      bse = __shfl(bse, 63, 64);
-      // this lane's entries occupy staging slots [ps0, ps0 + cs) and [pc0, pc0 + cc); slots past
-      // kStage overflow to the global lists (contiguous at the end of the lane's range)
-      const uint32_t ps0 = (bse & 0xFFFFu) + (excl & 0xFFFFu);
-      const uint32_t pc0 = (bse >> 16) + (excl >> 16);
-      const uint32_t over_s = ps0 + cs > (uint32_t)kStage ? min(ps0 + cs - (uint32_t)kStage, cs) : 0u;
-      const uint32_t over_c = pc0 + cc > (uint32_t)kStage ? min(pc0 + cc - (uint32_t)kStage, cc) : 0u;
-      uint32_t gs0 = 0, gc0 = 0;
-      if (__builtin_expect(__ballot(over_s | over_c) != 0, 0)) {
-        const uint32_t sp = over_s | (over_c << 16);
-        const uint32_t sincl = wave_incl_scan(sp);
-        uint32_t bs = 0, bc = 0;
-        if (lane == 63) {
-          if (sincl & 0xFFFFu) bs = atomicAdd(&w.ctl->n_sure, sincl & 0xFFFFu);
-          if (sincl >> 16) bc = atomicAdd(&w.ctl->n_cand, sincl >> 16);
-        }
-        gs0 = __shfl(bs, 63, 64) + ((sincl - sp) & 0xFFFFu);
-        gc0 = __shfl(bc, 63, 64) + ((sincl - sp) >> 16);
-      }
-      const uint32_t lim_s = max(ps0, (uint32_t)kStage), lim_c = max(pc0, (uint32_t)kStage);
-      uint32_t ps = ps0, pc = pc0;
-#pragma unroll
-      for (int u = 0; u < kGroup; ++u) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int b = u * 4 + j;
-          const int64_t i = gbase + (int64_t)u * (kMainBlock * 4) + j;
-          const float tv = comp4(t[u], j);
-          if ((msure >> b) & 1u) {
-            if (ps < (uint32_t)kStage) {
-              sm.sure[ps] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
-            } else {
-              const uint32_t gp = gs0 + (ps - lim_s);
-              if (gp < (uint32_t)a.k) { a.vals[gp] = tv; a.idx[gp] = (int32_t)(i + a.idx_base); }
-            }
-            ++ps;
-          }
-          if ((mcand >> b) & 1u) {
-            if (pc < (uint32_t)kStage) {
-              sm.cand[pc] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
-            } else {
-              const uint32_t gp = gc0 + (pc - lim_c);
-              if (gp < (uint32_t)w.cap) w.cand[gp] = make_int2((int)(i + a.idx_base), (int)f2u(tv));
-            }
-            ++pc;
-          }
-        }
-      }
-    }
+    classify_group<HAS_RES, MODE, FAST>(a, w, sm, lo, hi, sh, gbase, rc, gc);
 #pragma unroll
     for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
+  }
+}
+
+// the staged lists of one chunk leave with one global atomic per list (v2: the staged candidates
+// are counted into the LDS histogram here); leaves sm.cnt zeroed for the next chunk
+__device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                             uint32_t sh) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
+  const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
+  if (tid == 0) {
+    sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
+    sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+  }
+  if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
+    const uint32_t all = sm.cnt[0];
+    if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
+    if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < ns; j += kMainBlock) {
+    const uint32_t gp = sm.cnt[1] + j;
+    if (gp < (uint32_t)a.k) {
+      const int2 e = sm.sure[j];
+      a.vals[gp] = u2f((uint32_t)e.y);
+      a.idx[gp] = e.x;
+    }
+  }
+  for (uint32_t j = tid; j < nc; j += kMainBlock) {
+    const uint32_t gp = sm.cnt[2] + j;
+    const int2 e = sm.cand[j];
+    atomicAdd(&sm.hist[(abs_key(u2f((uint32_t)e.y)) - lo) >> sh], 1u);
+    if (gp < (uint32_t)w.cap) w.cand[gp] = e;
+  }
+  __syncthreads();
+  if (tid < 4) sm.cnt[tid] = 0;
+}
+
+// Persistent, software-pipelined variant: gridDim.x resident workgroups walk their full chunks
+// group by group with the next group's loads (across chunk boundaries too) in flight while the
+// current group is classified, so a chunk's flush overlaps the next chunk's first loads.
+template <bool HAS_RES, int MODE>
+__global__ __launch_bounds__(kMainBlock) void topk_main_pp(StepArgs a, TopkWs w) {
+  __shared__ MainShared sm;
+  constexpr int NG = kMainVec / kGroup;
+  const int tid = threadIdx.x;
+  for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
+  if (tid < 4) sm.cnt[tid] = 0;
+  const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
+  const int64_t nfull = a.n / kMainChunk;
+  const int64_t nmine = (int64_t)blockIdx.x < nfull ? (nfull - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t steps = nmine * NG;
+  const int64_t lane4 = (int64_t)tid * 4;
+  auto gaddr = [&](int64_t st) {
+    const int64_t c = (int64_t)blockIdx.x + (st / NG) * gridDim.x;
+    return c * kMainChunk + lane4 + (st % NG) * (int64_t)(kGroup * kMainBlock * 4);
+  };
+  __syncthreads();
+  float4 rc[kGroup], gc[kGroup];
+  if (steps) load_group<HAS_RES, true>(a, gaddr(0), rc, gc);
+#pragma unroll 1
+  for (int64_t st = 0; st < steps; ++st) {
+    float4 rn[kGroup], gn[kGroup];
+    if (st + 1 < steps) load_group<HAS_RES, true>(a, gaddr(st + 1), rn, gn);
+    classify_group<HAS_RES, MODE, true>(a, w, sm, lo, hi, sh, gaddr(st), rc, gc);
+    if (st % NG == NG - 1) flush_staged(a, w, sm, lo, sh);
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
+  }
+  if (nfull * kMainChunk < a.n && (int64_t)blockIdx.x == nfull % gridDim.x) {
+    main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, nfull);
+    flush_staged(a, w, sm, lo, sh);
+  }
+  __syncthreads();
+  for (int b = tid; b < kHistBins; b += kMainBlock) {
+    const uint32_t h = sm.hist[b];
+    if (h) atomicAdd(&w.hist[b * kHistStride], h);
   }
 }
 
@@ -723,44 +868,20 @@ __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   __shared__ MainShared sm;
   const int tid = threadIdx.x;
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
+  if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
   const int64_t nchunks = (a.n + kMainChunk - 1) / kMainChunk;
-  // grid-stride over chunks (gridDim.x == nchunks unless GRACE_MAIN_PERSIST caps the grid);
-  // the staged lists leave after every chunk (packed 16|16 counts), the histogram once at the end
+  __syncthreads();
+  // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
+  // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    if (tid < 4) sm.cnt[tid] = 0;
-    __syncthreads();
     if (VEC && (chunk + 1) * kMainChunk <= a.n)
-      main_chunk<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, chunk);
+      main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, chunk);
     else
-      main_chunk<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, chunk);
-    __syncthreads();
-    const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
-    const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
-    if (tid == 0) {
-      sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
-      sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
-    }
-    if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
-      const uint32_t all = sm.cnt[0];
-      if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
-      if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
-    }
-    __syncthreads();
-    for (uint32_t j = tid; j < ns; j += kMainBlock) {
-      const uint32_t gp = sm.cnt[1] + j;
-      if (gp < (uint32_t)a.k) {
-        const int2 e = sm.sure[j];
-        a.vals[gp] = u2f((uint32_t)e.y);
-        a.idx[gp] = e.x;
-      }
-    }
-    for (uint32_t j = tid; j < nc; j += kMainBlock) {
-      const uint32_t gp = sm.cnt[2] + j;
-      if (gp < (uint32_t)w.cap) w.cand[gp] = sm.cand[j];
-    }
-    __syncthreads();
+      main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, chunk);
+    flush_staged(a, w, sm, lo, sh);
   }
+  __syncthreads();
   for (int b = tid; b < kHistBins; b += kMainBlock) {
     const uint32_t h = sm.hist[b];
     if (h) atomicAdd(&w.hist[b * kHistStride], h);
@@ -888,7 +1009,6 @@ template <int MODE>
 __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
   constexpr int PER = kHistBins / kSelBlock;
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_base[kHistBins];
   __shared__ uint32_t hist[2048];
   __shared__ uint64_t s_comp[kSelBlock];
   __shared__ int2 s_ent[kSelBlock];
@@ -900,6 +1020,13 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
   const uint32_t k = (uint32_t)a.k;
   const bool ok = c.n_sure <= k && (uint64_t)c.n_sure + c.n_cand >= k && c.n_cand <= (uint64_t)w.cap;
   const int t = threadIdx.x;
+  {  // the bracket's sample histograms are free again: zero them for the next step
+    constexpr int kZ4 = (kBracketBins + kCoarseBins) / 4;
+    static_assert(kZ4 <= kFinBlocks * kSelBlock, "finalize grid covers the sample histograms");
+    const int z = blockIdx.x * kSelBlock + t;
+    if (z < kBracketBins / 4) reinterpret_cast<uint4*>(w.shist)[z] = make_uint4(0, 0, 0, 0);
+    else if (z < kZ4) reinterpret_cast<uint4*>(w.chist)[z - kBracketBins / 4] = make_uint4(0, 0, 0, 0);
+  }
   int B = -1;
   uint32_t need = 0, nb = 0;
   if (ok) {
@@ -913,7 +1040,6 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
     uint32_t acc = ex;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      s_base[top - j] = acc;                       // candidates in bins above this one
       if (target > 0 && acc < target && target <= acc + h[j]) { s_B = top - j; s_need = target - acc; }
       acc += h[j];
     }
@@ -1039,11 +1165,18 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
   a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
   a.stratum = a.n / a.sample_n;
+  // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
+  static_assert(kSmallN >= 2 * kSampleBlock, "bracket grid covers the histogram zeroing");
   topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
   unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
 #ifdef GRACE_MAIN_PERSIST
   if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
+#endif
+#ifdef GRACE_MAIN_PP
+  if (vec && nblk > (unsigned)GRACE_MAIN_PP)
+    launch_timed(topk_main_pp<HAS_RES, MODE>, dim3(GRACE_MAIN_PP), dim3(kMainBlock), s, a, w);
+  else
 #endif
   if (vec)
     launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);

@@ -18,7 +18,8 @@ dev = torch.device("cuda", 0)
 g = torch.randn(n, device=dev)
 r = 0.1 * torch.randn(n, device=dev)
 out = torch.empty_like(g)
-for it in range(5):
+rows = []
+for it in range(8):
     ops.topk_residual_step(g, r, True, 1.0, 1.0, k, out=out)
     torch.cuda.synchronize()
     ws = ops.topk_workspace(n, k, dev)
@@ -28,8 +29,12 @@ for it in range(5):
     names = ["thr_lo", "thr_hi", "shift", "status", "n_sure", "n_cand", "n_sel", "n_bnd", "B", "need"]
     counters = dict(zip(names, u32[:10].tolist()))
     us = lambda a, b: (int(st[b]) - int(st[a])) / 100.0
-    print({"smp_b0_load_zero": us(0, 1), "smp_b0_flush": us(1, 2), "smp_to_select": us(2, 3),
+    rows.append({"smp_b0_load_zero": us(0, 1), "smp_b0_flush": us(1, 2), "smp_to_select": us(2, 3),
            "sel_copy": us(3, 4), "sel_find": us(4, 5), "br_total": us(0, 5),
            "fin_b0_findB": us(8, 9), "fin_b0_route": us(9, 10), "fin_b0_to_last": us(10, 11),
            "fin_last_bnd": us(11, 12), "fin_total": us(8, 12),
            "k": k, **counters})
+import statistics  # noqa: E402
+keys = [k for k in rows[0] if k not in ("thr_lo", "thr_hi", "shift", "B")]
+print(os.environ.get("GRACE_HIP_LIB", "default"),
+      {k: round(statistics.median(r[k] for r in rows[2:]), 2) for k in keys})

@@ -25,7 +25,7 @@ run() {  # name timeout cmd...
 for step in "$@"; do
   case "$step" in
     smoke)  run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest_gpu 1200 python3 -m pytest tests -m gpu -x -q ;;
+    pytest) run pytest_gpu 1200 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytopk) run pytest_topk 900 python3 -m pytest tests/test_gpu_topk.py -x -q ;;
     pytestall) run pytest_gpu_all 1200 python3 -m pytest tests -m gpu -q ;;
     bench)  run bench 600 python3 bench.py ;;
