@@ -17,6 +17,14 @@
 namespace grace {
 
 constexpr int kQBlock = 256;
+#ifndef GRACE_QNB
+#define GRACE_QNB 4
+#endif
+constexpr int kQNB = GRACE_QNB;   // QSGD encode: buckets per half-wave per iteration
+#ifndef GRACE_QGRID
+#define GRACE_QGRID 8192
+#endif
+constexpr int kQGridCap = GRACE_QGRID;
 constexpr int kSegLds = 512;     // offset tables up to this many segments are staged in LDS
 
 // segment containing flat element / bucket index `x`: largest s with off[s] <= x
@@ -105,8 +113,9 @@ __device__ __forceinline__ CodeT qsgd_code(float xv, float level, float ui, floa
   const float prev = floorf(level);
   if constexpr (VARIANT == 0) {
     const float nl = prev + ((ui < level - prev) ? 1.0f : 0.0f);
-    const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : (xv == 0.f ? 0.f : xv));   // torch.sign
-    const int32_t c16 = f2i16_x86(nl * sg);
+    // nl * torch.sign(x) == copysign(nl, x) on every input: nl >= 0 or NaN, and where sign(x) is
+    // 0 or NaN the product is 0 / NaN, which the int16 conversion maps to 0 either way
+    const int32_t c16 = f2i16_x86(copysignf(nl, xv));
     if constexpr (sizeof(CodeT) == 1) return (CodeT)(int8_t)c16;
     else return (CodeT)__float2half((float)(int16_t)c16);
   } else {
@@ -141,6 +150,170 @@ __device__ __forceinline__ void store_codes4(CodeT* __restrict__ codes, int64_t 
   }
 }
 
+// ---- 32-bit fast path (n < 2^31, nseg <= kSegLds, bucket 128): every index is an int32, the offset
+// tables sit in LDS as int32 and the generator key is hoisted, which roughly halves the VALU work
+// per element against the general kernels (64-bit index math was a third of their instructions).
+struct SegTables32 {
+  int32_t seg[kSegLds + 1];
+  int32_t sub[kSegLds + 1];
+};
+
+__device__ __forceinline__ void stage_tables32(SegTables32& t, const int64_t* seg, const int64_t* sub, int nseg) {
+  for (int i = threadIdx.x; i <= nseg; i += blockDim.x) {
+    t.seg[i] = (int32_t)seg[i];
+    t.sub[i] = (int32_t)sub[i];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int find_seg32(const int32_t* off, int nseg, int32_t x) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int seg_advance32(const int32_t* off, int nseg, int s, int32_t x) {
+  while (s + 1 < nseg && off[s + 1] <= x) ++s;
+  return s;
+}
+
+__device__ __forceinline__ void block_range32(int32_t total, int32_t step, int32_t& lo, int32_t& hi) {
+  int32_t per = (total + (int32_t)gridDim.x - 1) / (int32_t)gridDim.x;
+  per = (per + step - 1) / step * step;
+  lo = min((int32_t)blockIdx.x * per, total);
+  hi = min(lo + per, total);
+}
+
+// uniform01x4 for i < 2^32 with the key mix64(seed) precomputed: identical values
+__device__ __forceinline__ void uniform01x4_k(uint64_t key, uint32_t i, float (&u)[4]) {
+  uint32_t h = fmix32(((i * 0x9E3779B1u) ^ (uint32_t)key) + (uint32_t)(key >> 32));
+  u[0] = (float)(h >> 8) * (1.0f / 16777216.0f);
+  h = h ? h : 0x9E3779B9u;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    h ^= h << 13;
+    h ^= h >> 17;
+    h ^= h << 5;
+    u[j] = (float)(h >> 8) * (1.0f / 16777216.0f);
+  }
+}
+
+// 64-bit value moved across lanes by one DPP pattern (two 32-bit DPP movs)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// Sum over each 16-lane DPP row by symmetric butterflies (quad xor 1, quad xor 2, half-mirror,
+// mirror): every step adds the same two operands in every lane, so all 16 lanes hold the
+// bit-identical total -- no LDS traffic, no lgkm waits.
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return v;
+}
+
+// A 16-lane row owns a bucket of 128: each lane two quads (l16, l16 + 16; two 16-B loads), the norm is
+// one DPP row reduction; kQNB buckets per row per iteration with every load issued first.
+template <typename CodeT, int VARIANT>
+__global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
+    int nseg, int32_t nbuckets, float qf, const float* __restrict__ u, uint64_t seed,
+    const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes) {
+  __shared__ SegTables32 tab;
+  stage_tables32(tab, seg_off, bkt_off, nseg);
+  const int l16 = threadIdx.x & 15;
+  constexpr int kRows = kQBlock / 16;
+  const uint64_t key = mix64(seed);
+  int32_t blo, bhi;
+  block_range32(nbuckets, kRows, blo, bhi);
+  const int32_t b_first = blo + (int32_t)(threadIdx.x >> 4);
+  int s = b_first < bhi ? find_seg32(tab.sub, nseg, b_first) : 0;
+  for (int32_t b = b_first; b < bhi; b += kQNB * kRows) {
+    int32_t bb[kQNB], e[kQNB][2], end[kQNB];
+    bool ok[kQNB], fast[kQNB][2];
+    float v[kQNB][2][4];
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      bb[h] = b + h * kRows;
+      ok[h] = bb[h] < bhi;
+      if (ok[h]) s = seg_advance32(tab.sub, nseg, s, bb[h]);
+      const int32_t base = tab.seg[s] + (bb[h] - tab.sub[s]) * 128;
+      end[h] = ok[h] ? min(base + 128, tab.seg[s + 1]) : base;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        e[h][q] = base + 4 * l16 + 64 * q;   // quads l16 and l16 + 16: each instruction covers 256 contiguous bytes per row
+        fast[h][q] = ok[h] && (base & 3) == 0 && e[h][q] + 3 < end[h];
+        // unconditional 16-B load (element 0 stands in for a slow quad): a load under a divergent
+        // branch makes the compiler wait vmcnt(0) at the join, serialising the loads
+        const f4v t = *reinterpret_cast<const f4v*>(x + (fast[h][q] ? e[h][q] : 0));
+        v[h][q][0] = t.x; v[h][q][1] = t.y; v[h][q][2] = t.z; v[h][q][3] = t.w;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h)   // quads at a segment edge / unaligned segment (rare)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (!fast[h][q]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[h][q][j] = ok[h] && e[h][q] + j < end[h] ? x[e[h][q] + j] : 0.f;
+        }
+    float norm[kQNB];
+    if (norms_in) {
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) norm[h] = ok[h] ? norms_in[bb[h]] : 1.f;
+    } else {
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+        // squares of f32 values are exact in f64, so fma == add of the exact product
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (VARIANT == 0 || isfinite(v[h][q][j])) acc = fma((double)v[h][q][j], (double)v[h][q][j], acc);
+        acc = row16_sum(acc);
+        norm[h] = VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      if (!ok[h]) continue;
+      if (l16 == 0) norms_out[bb[h]] = norm[h];
+      const float scale = VARIANT == 0 ? (1.0f / norm[h]) * qf : qf / norm[h];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int32_t eq = e[h][q];
+        float uu[4];
+        if (u) {   // parity mode (injected stream): not the fast path
+#pragma unroll
+          for (int j = 0; j < 4; ++j) uu[j] = eq + j < end[h] ? u[eq + j] : 0.f;
+        } else {
+#ifdef GRACE_DIAG_NORNG   // diagnostic A/B build only: constant u
+          uu[0] = uu[1] = uu[2] = uu[3] = 0.5f + 0.f * (float)key;
+#else
+          uniform01x4_k(key, (uint32_t)eq, uu);
+#endif
+        }
+        CodeT c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float level = VARIANT == 0 ? scale * fabsf(v[h][q][j]) : qf / norm[h] * fabsf(v[h][q][j]);
+          c[j] = qsgd_code<CodeT, VARIANT>(v[h][q][j], level, uu[j], norm[h]);
+        }
+        store_codes4(codes, eq, end[h], fast[h][q], c);
+      }
+    }
+  }
+}
+
 template <typename CodeT, int VARIANT>
 __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
@@ -155,13 +328,14 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
   const int64_t b_first = blo + (threadIdx.x >> 5);
   int s = b_first < bhi ? find_seg(sv.sub, nseg, b_first) : 0;
   if (bucket <= 128) {
-    // two buckets per half-wave per iteration: both 16-B loads are in flight before either reduces
-    for (int64_t b = b_first; b < bhi; b += 2 * kHalves) {
-      int64_t bb[2], base[2], end[2];
-      bool ok[2], aligned[2];
-      float v[2][4];
+    // kQNB buckets per half-wave per iteration: every 16-B load is in flight before any bucket
+    // reduces, and the kQNB shuffle reductions interleave
+    for (int64_t b = b_first; b < bhi; b += kQNB * kHalves) {
+      int64_t bb[kQNB], base[kQNB], end[kQNB];
+      bool ok[kQNB], aligned[kQNB];
+      float v[kQNB][4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < kQNB; ++h) {
         bb[h] = b + h * kHalves;
         ok[h] = bb[h] < bhi;
         if (ok[h]) s = seg_advance(sv.sub, nseg, s, bb[h]);
@@ -170,35 +344,41 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
         aligned[h] = (base[h] & 3) == 0;
         load_quad(x, base[h] + 4 * l32, end[h], aligned[h], v[h]);
       }
+      float norm[kQNB];
+      if (norms_in) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (!ok[h]) break;
-        const int64_t e = base[h] + 4 * l32;
-        float norm;
-        if (norms_in) {
-          norm = norms_in[bb[h]];
-        } else {
-          double acc = 0.0;
+        for (int h = 0; h < kQNB; ++h) norm[h] = ok[h] ? norms_in[bb[h]] : 1.f;
+      } else {
+        double acc[kQNB];
+#pragma unroll
+        for (int h = 0; h < kQNB; ++h) {
+          acc[h] = 0.0;
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (VARIANT == 0 || isfinite(v[h][j])) acc += (double)v[h][j] * (double)v[h][j];
-          acc = half_sum(acc);
-          norm = VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
+            if (VARIANT == 0 || isfinite(v[h][j])) acc[h] += (double)v[h][j] * (double)v[h][j];
         }
-        if (l32 == 0) norms_out[bb[h]] = norm;
-        const float scale = VARIANT == 0 ? (1.0f / norm) * qf : qf / norm;
-        float uu[4];
-        if (u) {
-          load_quad(u, e, end[h], aligned[h], uu);
-        } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) uu[j] = uniform01(seed, (uint64_t)(e + j));
+        for (int o = 16; o > 0; o >>= 1) {
+#pragma unroll
+          for (int h = 0; h < kQNB; ++h) acc[h] += __shfl_xor(acc[h], o, 64);
         }
+#pragma unroll
+        for (int h = 0; h < kQNB; ++h) norm[h] = VARIANT == 0 ? sqrtf((float)acc[h]) : (float)sqrt(acc[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+        if (!ok[h]) continue;
+        const int64_t e = base[h] + 4 * l32;
+        if (l32 == 0) norms_out[bb[h]] = norm[h];
+        const float scale = VARIANT == 0 ? (1.0f / norm[h]) * qf : qf / norm[h];
+        float uu[4];
+        if (u) load_quad(u, e, end[h], aligned[h], uu);
+        else uniform01x4(seed, (uint64_t)e, uu);
         CodeT c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float level = VARIANT == 0 ? scale * fabsf(v[h][j]) : qf / norm * fabsf(v[h][j]);
-          c[j] = qsgd_code<CodeT, VARIANT>(v[h][j], level, uu[j], norm);
+          const float level = VARIANT == 0 ? scale * fabsf(v[h][j]) : qf / norm[h] * fabsf(v[h][j]);
+          c[j] = qsgd_code<CodeT, VARIANT>(v[h][j], level, uu[j], norm[h]);
         }
         store_codes4(codes, e, end[h], aligned[h], c);
       }
@@ -358,6 +538,95 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_kernel(
   }
 }
 
+// Bucket-of-128 decode, mirroring the encoder's layout: a 16-lane row owns a bucket (each lane two
+// quads), kQNB buckets per row per iteration, every load issued before any is used.  The segment
+// walk and the scale norm_w / q (one division) are per bucket and lane-pair of quads instead of
+// per quad.  Same arithmetic as qsgd_decode_kernel.
+template <typename CodeT, int VARIANT>
+__global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
+    const CodeT* __restrict__ codes, const float* __restrict__ norms, int64_t code_stride,
+    int64_t norm_stride, int world, const int64_t* __restrict__ seg_off,
+    const int64_t* __restrict__ bkt_off, int nseg, float qf, float divisor, int aggregate, int vec,
+    float* __restrict__ out) {
+  __shared__ SegTables32 tab;
+  stage_tables32(tab, seg_off, bkt_off, nseg);
+  const int l16 = threadIdx.x & 15;
+  constexpr int kRows = kQBlock / 16;
+  const int32_t nbuckets = tab.sub[nseg];
+  int32_t blo, bhi;
+  block_range32(nbuckets, kRows, blo, bhi);
+  const int32_t b_first = blo + (int32_t)(threadIdx.x >> 4);
+  int s = b_first < bhi ? find_seg32(tab.sub, nseg, b_first) : 0;
+  for (int32_t b = b_first; b < bhi; b += kQNB * kRows) {
+    int32_t bb[kQNB], e[kQNB][2], end[kQNB];
+    bool ok[kQNB], full[kQNB][2];
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      bb[h] = b + h * kRows;
+      ok[h] = bb[h] < bhi;
+      if (ok[h]) s = seg_advance32(tab.sub, nseg, s, bb[h]);
+      const int32_t base = tab.seg[s] + (bb[h] - tab.sub[s]) * 128;
+      end[h] = ok[h] ? min(base + 128, tab.seg[s + 1]) : base;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        e[h][q] = base + 4 * l16 + 64 * q;   // quads l16 and l16 + 16: each instruction covers 256 contiguous bytes per row
+        full[h][q] = ok[h] && vec && (base & 3) == 0 && e[h][q] + 3 < end[h];
+      }
+    }
+    float acc[kQNB][2][4] = {};
+    for (int w = 0; w < world; ++w) {
+      float c[kQNB][2][4], nrm[kQNB];
+      // unconditional loads first (see qsgd_encode128_kernel), edge quads fixed up after
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          load_codes4(codes + (full[h][q] ? w * code_stride + e[h][q] : 0), true, c[h][q]);
+        nrm[h] = norms[w * norm_stride + (ok[h] ? bb[h] : 0)];
+      }
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (ok[h] && !full[h][q]) {
+            const CodeT* p = codes + w * code_stride + e[h][q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c[h][q][j] = e[h][q] + j < end[h] ? load_code1(p + j) : 0.f;
+          }
+        const float sc = nrm[h] / qf;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float d = sc * c[h][q][j];
+            if (VARIANT == 1 && c[h][q][j] == -128.0f) d = __int_as_float(0x7FC00000);
+            acc[h][q][j] = (aggregate || w > 0) ? acc[h][q][j] + d : d;   // Python sum: 0 + d_0 + ...
+          }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      if (!ok[h]) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float* a4 = acc[h][q];
+        if (divisor != 1.0f) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a4[j] = a4[j] / divisor;
+        }
+        const int32_t eq = e[h][q];
+        if (full[h][q]) {
+          __builtin_nontemporal_store(f4v{a4[0], a4[1], a4[2], a4[3]}, reinterpret_cast<f4v*>(out + eq));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (eq + j < end[h]) out[eq + j] = a4[j];
+        }
+      }
+    }
+  }
+}
+
 // ================================================================================================
 // TernGrad (grace_dl/dist/compressor/terngrad.py:7-30)
 //   std    = sqrt(mean((x - mean x)^2))        (here: f64 sums of x and x^2, one read)
@@ -390,10 +659,11 @@ __device__ __forceinline__ void tern_acc(float v, double& sum, double& sq, float
 }
 
 // workgroup reduction of a TernPartial in a fixed order (deterministic)
+template <int BLOCK = kQBlock>
 __device__ __forceinline__ TernPartial block_tern_reduce(double sum, double sq, float amax, uint32_t nan) {
-  __shared__ double sh_s[kQBlock / kWave], sh_q[kQBlock / kWave];
-  __shared__ float sh_m[kQBlock / kWave];
-  __shared__ uint32_t sh_n[kQBlock / kWave];
+  __shared__ double sh_s[BLOCK / kWave], sh_q[BLOCK / kWave];
+  __shared__ float sh_m[BLOCK / kWave];
+  __shared__ uint32_t sh_n[BLOCK / kWave];
   sum = wave_sum(sum);
   sq = wave_sum(sq);
   amax = wave_max(amax);
@@ -402,17 +672,50 @@ __device__ __forceinline__ TernPartial block_tern_reduce(double sum, double sq, 
   if ((threadIdx.x & 63) == 0) { sh_s[w] = sum; sh_q[w] = sq; sh_m[w] = amax; sh_n[w] = nan; }
   __syncthreads();
   TernPartial p{0.0, 0.0, 0.f, 0u};
-  for (int j = 0; j < kQBlock / kWave; ++j) {
+  for (int j = 0; j < BLOCK / kWave; ++j) {
     p.sum += sh_s[j]; p.sq += sh_q[j]; p.amax = fmaxf(p.amax, sh_m[j]); p.nan |= sh_n[j];
   }
   return p;
 }
 
+// per-segment scale slot, kept at the segment's first unit (empty segments have none)
+struct TernScale { float c, scalar; };
+
+struct TernWs {
+  TernPartial* part;   // [nunits]
+  uint32_t* tick;      // [nunits] arrival counters, at the segment's first unit; left zeroed
+  TernScale* scale;    // [nunits]
+};
+// The tick counters come first, so they stay at a fixed place whatever nunits a call uses (the
+// workspace is shared by calls of different shapes and only the ticks must be left zeroed).
+__host__ __device__ inline size_t tern_ws_bytes(int64_t nunits) {
+  const size_t a = ((sizeof(uint32_t) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
+  const size_t b = ((sizeof(TernPartial) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
+  return a + b + sizeof(TernScale) * (size_t)(nunits + 1);
+}
+inline TernWs tern_ws(void* ws, int64_t nunits) {
+  char* p = reinterpret_cast<char*>(ws);
+  TernWs w;
+  w.tick = reinterpret_cast<uint32_t*>(p);
+  p += ((sizeof(uint32_t) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
+  w.part = reinterpret_cast<TernPartial*>(p);
+  p += ((sizeof(TernPartial) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
+  w.scale = reinterpret_cast<TernScale*>(p);
+  return w;
+}
+
+// Stage 1: per-unit f64 partials; the LAST unit of a segment to arrive reduces the segment's
+// partials in a fixed order (the same block reduction whichever unit it is, so the scale is
+// deterministic) and publishes (c, scalar) for stage 2.  Partials cross workgroups -- and XCDs,
+// whose L2s are not coherent -- so they are written and read back at agent scope (write-through),
+// ordered by vmcnt(0) before the arrival ticket: no cache-wide fences.
 __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __restrict__ x,
                                                             const int64_t* __restrict__ seg_off,
                                                             const int64_t* __restrict__ unit_off, int nseg,
-                                                            TernPartial* __restrict__ part) {
+                                                            const float* __restrict__ clip_in, TernWs w,
+                                                            float* __restrict__ scalars) {
   __shared__ SegTables tab;
+  __shared__ uint32_t s_last;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
   const int64_t unit = blockIdx.x;
   const int s = find_seg(sv.sub, nseg, unit);
@@ -436,13 +739,57 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
     tern_acc(v.w, sum, sq, amax, nan);
   }
   const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
-  if (threadIdx.x == 0) part[unit] = p;
+  uint64_t* pw = reinterpret_cast<uint64_t*>(w.part + unit);
+  if (t == 0) {
+    __hip_atomic_store(pw, (uint64_t)__double_as_longlong(p.sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pw + 1, (uint64_t)__double_as_longlong(p.sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pw + 2, (uint64_t)__float_as_uint(p.amax) | ((uint64_t)p.nan << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int64_t first = sv.sub[s], units = sv.sub[s + 1] - first;
+    s_last = atomicAdd(&w.tick[first], 1u) == (uint32_t)(units - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // last arrival: the segment's statistics from its units' partials, in a fixed order
+  const int64_t first = sv.sub[s];
+  sum = 0.0; sq = 0.0; amax = 0.f; nan = 0;
+  for (int64_t j = first + t; j < sv.sub[s + 1]; j += kQBlock) {
+    const uint64_t* pj = reinterpret_cast<const uint64_t*>(w.part + j);
+    sum += __longlong_as_double((long long)__hip_atomic_load(pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    sq += __longlong_as_double((long long)__hip_atomic_load(pj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint64_t mn = __hip_atomic_load(pj + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    amax = fmaxf(amax, __uint_as_float((uint32_t)mn));
+    nan |= (uint32_t)(mn >> 32);
+  }
+  const TernPartial q = block_tern_reduce(sum, sq, amax, nan);
+  if (t == 0) {
+    float c;
+    if (clip_in) {
+      c = clip_in[s];
+    } else {
+      const double nn = (double)(sv.seg[s + 1] - sv.seg[s]);
+      const double mean = q.sum / nn;
+      double var = q.sq / nn - mean * mean;
+      if (var < 0.0) var = 0.0;
+      c = (float)(2.5 * (double)(float)sqrt(var));
+    }
+    const float scalar = q.nan ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
+    w.scale[first] = TernScale{c, scalar};
+    scalars[s] = scalar;
+    w.tick[first] = 0u;   // left zeroed for the next call
+  }
 }
 
-__global__ __launch_bounds__(kQBlock) void tern_encode_kernel(
+#ifndef GRACE_TERN_BLOCK
+#define GRACE_TERN_BLOCK 256
+#endif
+constexpr int kTernBlock = GRACE_TERN_BLOCK;   // encode workgroup (A/B: 256 beats 512 and 1024)
+
+__global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
-    int nseg, const TernPartial* __restrict__ part, const float* __restrict__ clip_in,
-    const float* __restrict__ u, uint64_t seed, int8_t* __restrict__ codes, float* __restrict__ scalars) {
+    int nseg, const TernScale* __restrict__ scale, const float* __restrict__ u, uint64_t seed,
+    int8_t* __restrict__ codes) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
   const int64_t unit = blockIdx.x;
@@ -452,36 +799,16 @@ __global__ __launch_bounds__(kQBlock) void tern_encode_kernel(
   const QuadSplit qs = quad_split(base, end);
   const int t = threadIdx.x;
   const int64_t nq = (qs.a1 - qs.a0) >> 2;
-  // the unit's quads are loaded before the scale is known (their latency overlaps the reduction)
-  constexpr int kPer = kTernUnit / 4 / kQBlock;
+  constexpr int kPer = kTernUnit / 4 / kTernBlock;
   f4v xv[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int64_t j = t + (int64_t)k * kQBlock;
+    const int64_t j = t + (int64_t)k * kTernBlock;
     const int64_t jc = j < nq ? j : 0;
     if (nq > 0) xv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + qs.a0) + jc);
   }
-  // the segment's statistics from its units' partials, in a fixed order
-  double sum = 0.0, sq = 0.0;
-  float amax = 0.f;
-  uint32_t nan = 0;
-  for (int64_t j = sv.sub[s] + threadIdx.x; j < sv.sub[s + 1]; j += kQBlock) {
-    const TernPartial pj = part[j];
-    sum += pj.sum; sq += pj.sq; amax = fmaxf(amax, pj.amax); nan |= pj.nan;
-  }
-  const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
-  float c;
-  if (clip_in) {
-    c = clip_in[s];
-  } else {
-    const double nn = (double)(sv.seg[s + 1] - sv.seg[s]);
-    const double mean = p.sum / nn;
-    double var = p.sq / nn - mean * mean;
-    if (var < 0.0) var = 0.0;
-    c = (float)(2.5 * (double)(float)sqrt(var));
-  }
-  const float scalar = p.nan ? __int_as_float(0x7FC00000) : fminf(p.amax, c);
-  if (threadIdx.x == 0 && unit == sv.sub[s]) scalars[s] = scalar;
+  const TernScale sc = scale[sv.sub[s]];   // published by the segment's last stats unit
+  const float c = sc.c, scalar = sc.scalar;
 
   auto enc = [&](float xv, float ui) -> int8_t {
     const float cl = fminf(fmaxf(xv, -c), c);
@@ -504,7 +831,7 @@ __global__ __launch_bounds__(kQBlock) void tern_encode_kernel(
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int64_t j = t + (int64_t)k * kQBlock;
+    const int64_t j = t + (int64_t)k * kTernBlock;
     if (j >= nq) break;
     const int64_t i = qs.a0 + 4 * j;
     const f4v v = xv[k];
@@ -512,14 +839,108 @@ __global__ __launch_bounds__(kQBlock) void tern_encode_kernel(
     if (u) {
       uu = *reinterpret_cast<const f4v*>(u + i);
     } else {
-      uu.x = uniform01(seed, (uint64_t)i);
-      uu.y = uniform01(seed, (uint64_t)i + 1);
-      uu.z = uniform01(seed, (uint64_t)i + 2);
-      uu.w = uniform01(seed, (uint64_t)i + 3);
+      float r4[4];
+      uniform01x4(seed, (uint64_t)i, r4);
+      uu = f4v{r4[0], r4[1], r4[2], r4[3]};
     }
     const uint32_t w = (uint32_t)(uint8_t)enc(v.x, uu.x) | ((uint32_t)(uint8_t)enc(v.y, uu.y) << 8) |
                        ((uint32_t)(uint8_t)enc(v.z, uu.z) << 16) | ((uint32_t)(uint8_t)enc(v.w, uu.w) << 24);
     *reinterpret_cast<uint32_t*>(codes + i) = w;
+  }
+}
+
+// Row decoder: a 16-lane row owns a 128-element chunk of the flat buffer (each lane the quads l16
+// and l16 + 16), kQNB chunks per row per iteration, every load issued before any is used.  A chunk
+// inside one segment uses one scalar per rank; the few quads of a chunk that straddles a segment
+// boundary are decoded element-wise.  Same arithmetic as tern_decode_kernel.
+__global__ __launch_bounds__(kQBlock) void tern_decode_row_kernel(const int8_t* __restrict__ codes,
+                                                                 const float* __restrict__ scalars,
+                                                                 int64_t code_stride, int64_t scal_stride,
+                                                                 int world, const int64_t* __restrict__ seg_off,
+                                                                 int nseg, int32_t n, float divisor, int aggregate,
+                                                                 int vec, float* __restrict__ out) {
+  __shared__ int32_t seg[kSegLds + 1];
+  for (int i = threadIdx.x; i <= nseg; i += blockDim.x) seg[i] = (int32_t)seg_off[i];
+  __syncthreads();
+  const int l16 = threadIdx.x & 15;
+  constexpr int kRows = kQBlock / 16;
+  const int32_t nchunks = (n + 127) / 128;
+  int32_t blo, bhi;
+  block_range32(nchunks, kRows, blo, bhi);
+  const int32_t c_first = blo + (int32_t)(threadIdx.x >> 4);
+  int s = c_first < bhi ? find_seg32(seg, nseg, c_first * 128) : 0;
+  for (int32_t c = c_first; c < bhi; c += kQNB * kRows) {
+    int32_t e[kQNB][2], ce[kQNB];
+    int sidx[kQNB];
+    bool ok[kQNB], full[kQNB][2];
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      const int32_t cc = c + h * kRows;
+      ok[h] = cc < bhi;
+      const int32_t i0 = cc * 128;
+      if (ok[h]) s = seg_advance32(seg, nseg, s, i0);
+      sidx[h] = s;
+      ce[h] = ok[h] ? min(i0 + 128, n) : i0;
+      const bool uni = seg[s + 1] >= ce[h];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        e[h][q] = i0 + 4 * l16 + 64 * q;
+        full[h][q] = ok[h] && uni && vec && e[h][q] + 3 < ce[h];
+      }
+    }
+    float acc[kQNB][2][4] = {};
+    for (int w = 0; w < world; ++w) {
+      float cv[kQNB][2][4], sc[kQNB];
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          load_codes4(codes + (full[h][q] ? w * code_stride + e[h][q] : 0), true, cv[h][q]);
+        sc[h] = scalars[w * scal_stride + sidx[h]];
+      }
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (full[h][q]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float d = cv[h][q][j] * sc[h];
+              acc[h][q][j] = (aggregate || w > 0) ? acc[h][q][j] + d : d;
+            }
+          } else if (ok[h]) {   // chunk edge / segment boundary / unaligned codes: per element
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int32_t i = e[h][q] + j;
+              if (i < ce[h]) {
+                const int sj = seg_advance32(seg, nseg, sidx[h], i);
+                const float d = (float)codes[w * code_stride + i] * scalars[w * scal_stride + sj];
+                acc[h][q][j] = (aggregate || w > 0) ? acc[h][q][j] + d : d;
+              }
+            }
+          }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      if (!ok[h]) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float* a4 = acc[h][q];
+        if (divisor != 1.0f) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a4[j] = a4[j] / divisor;
+        }
+        const int32_t eq = e[h][q];
+        if (full[h][q]) {
+          __builtin_nontemporal_store(f4v{a4[0], a4[1], a4[2], a4[3]}, reinterpret_cast<f4v*>(out + eq));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (eq + j < ce[h]) out[eq + j] = a4[j];
+        }
+      }
+    }
   }
 }
 
@@ -690,8 +1111,21 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
                 "grace_qsgd_compress: bad arguments");
   if (nbuckets == 0) return GRACE_OK;
   GRACE_REQUIRE(variant == 0 || (variant == 1 && quantum_num < 128), "grace_qsgd_compress: bad variant");
-  const unsigned grid = stream_grid(nbuckets, 2 * kQBlock / 32, 4096);
+  const unsigned grid = stream_grid(nbuckets, kQNB * kQBlock / 32, kQGridCap);
   hipStream_t st = as_stream(stream);
+  if (bucket_size == 128 && nseg <= kSegLds && nbuckets < (int64_t(1) << 24)) {   // n < 2^31
+    const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQGridCap);
+#define GRACE_QENC128(CT, V)                                                                         \
+  qsgd_encode128_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
+                                                        (float)quantum_num, u, seed, norms_in,        \
+                                                        norms_out, reinterpret_cast<CT*>(codes))
+    if (variant == 1) GRACE_QENC128(int8_t, 1);
+    else if (quantum_num < 128) GRACE_QENC128(int8_t, 0);
+    else GRACE_QENC128(__half, 0);
+#undef GRACE_QENC128
+    GRACE_CHECK_LAUNCH("grace_qsgd_compress");
+    return GRACE_OK;
+  }
   if (variant == 1) {
     qsgd_encode_kernel<int8_t, 1><<<grid, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, nbuckets, bucket_size,
                                                            (float)quantum_num, u, seed, norms_in, norms_out,
@@ -728,6 +1162,20 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
                                                          bkt_off, nseg, n, bucket_size,              \
                                                          (float)quantum_num, divisor, aggregate, vec, out)
   const bool b128 = bucket_size == 128;
+  if (b128 && nseg <= kSegLds && n < (int64_t(1) << 31)) {
+    const unsigned bgrid = stream_grid((n + 127) / 128 + nseg, kQNB * kQBlock / 16, kQGridCap);
+#define GRACE_QDECB(CT, V)                                                                          \
+  qsgd_decode_bkt_kernel<CT, V><<<bgrid, kQBlock, 0, st>>>(reinterpret_cast<const CT*>(codes), norms, \
+                                                          code_stride, norm_stride, world, seg_off,  \
+                                                          bkt_off, nseg, (float)quantum_num, divisor, \
+                                                          aggregate, vec, out)
+    if (variant == 1) GRACE_QDECB(int8_t, 1);
+    else if (quantum_num < 128) GRACE_QDECB(int8_t, 0);
+    else GRACE_QDECB(__half, 0);
+#undef GRACE_QDECB
+    GRACE_CHECK_LAUNCH("grace_qsgd_decompress");
+    return GRACE_OK;
+  }
   if (variant == 1) {
     if (b128) GRACE_QDEC(int8_t, 1, true); else GRACE_QDEC(int8_t, 1, false);
   } else if (quantum_num < 128) {
@@ -740,7 +1188,7 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
   return GRACE_OK;
 }
 
-size_t grace_terngrad_workspace_bytes(int64_t nunits) { return sizeof(TernPartial) * (size_t)(nunits + 1); }
+size_t grace_terngrad_workspace_bytes(int64_t nunits) { return tern_ws_bytes(nunits); }
 int32_t grace_terngrad_unit(void) { return kTernUnit; }
 
 grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, const int64_t* unit_off,
@@ -749,11 +1197,12 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
                                        void* stream) {
   GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && nunits >= 1 && codes && scalars && ws,
                 "grace_terngrad_compress: bad arguments");
-  TernPartial* part = reinterpret_cast<TernPartial*>(ws);
-  tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, part);
+  const TernWs w = tern_ws(ws, nunits);
+  tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
+                                                                       scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
-  tern_encode_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, part,
-                                                                         clip_in, u, seed, codes, scalars);
+  tern_encode_kernel<<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w.scale,
+                                                                         u, seed, codes);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
   return GRACE_OK;
 }
@@ -766,6 +1215,13 @@ grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scala
                 "grace_terngrad_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
   const int vec = (code_stride % 4 == 0) && ((uintptr_t)codes % 4 == 0);
+  if (nseg <= kSegLds && n < (int64_t(1) << 31)) {
+    tern_decode_row_kernel<<<stream_grid((n + 127) / 128, kQNB * kQBlock / 16, kQGridCap), kQBlock, 0,
+                             as_stream(stream)>>>(codes, scalars, code_stride, scal_stride, world, seg_off, nseg,
+                                                  (int32_t)n, divisor, aggregate, vec, out);
+    GRACE_CHECK_LAUNCH("grace_terngrad_decompress");
+    return GRACE_OK;
+  }
   tern_decode_kernel<<<stream_grid((n + kDecRound - 1) / kDecRound, 1, 4096), kQBlock, 0, as_stream(stream)>>>(
       codes, scalars, code_stride, scal_stride, world, seg_off, nseg, n, divisor, aggregate, vec, out);
   GRACE_CHECK_LAUNCH("grace_terngrad_decompress");
