@@ -345,12 +345,23 @@ __global__ __launch_bounds__(kPBlockT) void psgd_qt_kernel(const float* __restri
 // MGS itself can handle.  A zero / dependent column gives R_cc = 0 and non-finite output, as MGS.
 constexpr int kOrthBlock = 1024;
 
-// standard normal draw of element i (Box-Muller on the counter-based generator)
-__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t i) {
-  const uint64_t h = mix64(seed ^ mix64(i * 2 + 1));
+// standard normal draws: Box-Muller on the counter-based generator, one (cos, sin) pair per two
+// consecutive elements; element e is component e & 1 of pair e >> 1 (normal_kernel, the generic and
+// the rank-4 fused draws all produce the same stream)
+__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t pair, float& z0, float& z1) {
+  const uint64_t h = mix64(seed ^ mix64(pair * 2 + 1));
   const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);   // (0, 1]
   const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
-  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+  const float rad = sqrtf(-2.0f * logf(u1));
+  float sn, cs;
+  sincosf(6.2831853071795864f * u2, &sn, &cs);
+  z0 = rad * cs;
+  z1 = rad * sn;
+}
+__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t i) {
+  float z0, z1;
+  normal_pair(seed, i >> 1, z0, z1);
+  return (i & 1) ? z1 : z0;
 }
 
 // R = r rounded up to a power of two (the Gram accumulators live in registers: R(R+1)/2 doubles).
@@ -471,6 +482,88 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth_kernel(float* __restrict
   }
 }
 
+// Rank-4 fast path (r == 4, n <= 4096 rows, 16-B aligned A: PowerSGD's P and q at rank 4): the
+// same Cholesky-QR with one 16-B load and store per row, the Gram entries reduced by DPP row
+// butterflies (no ds_bpermute chains) and, for DRAW, one Box-Muller pair per two entries.
+constexpr int kOrth4Rows = kOrthBlock * 4;
+
+template <bool DRAW>
+__global__ __launch_bounds__(kOrthBlock) void psgd_orth4_kernel(float* __restrict__ A, int64_t n, uint64_t seed) {
+  constexpr int R = 4, kGram = 10;
+  __shared__ double sh[kOrthBlock / 16][kGram];
+  __shared__ double Gs[kGram];
+  __shared__ double Rs[R][R];
+  __shared__ double Rinv[R];
+  float a[4][R];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = threadIdx.x + (int64_t)j * kOrthBlock;
+    const bool rv = i < n;
+    if constexpr (DRAW) {
+      normal_pair(seed, (uint64_t)i * 2, a[j][0], a[j][1]);
+      normal_pair(seed, (uint64_t)i * 2 + 1, a[j][2], a[j][3]);
+    } else {
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(A + (rv ? i : 0) * R);   // unconditional
+      a[j][0] = v.x; a[j][1] = v.y; a[j][2] = v.z; a[j][3] = v.w;
+    }
+    if (!rv) a[j][0] = a[j][1] = a[j][2] = a[j][3] = 0.f;
+  }
+  double g[kGram];
+#pragma unroll
+  for (int e = 0; e < kGram; ++e) g[e] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int e = 0;
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+#pragma unroll
+      for (int c2 = c; c2 < R; ++c2, ++e) g[e] = fma((double)a[j][c], (double)a[j][c2], g[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < kGram; ++e) g[e] = row16_sum(g[e]);
+  if ((threadIdx.x & 15) == 0) {
+#pragma unroll
+    for (int e = 0; e < kGram; ++e) sh[threadIdx.x >> 4][e] = g[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < kGram) {
+    double t = 0.0;
+    for (int k = 0; k < kOrthBlock / 16; ++k) t += sh[k][threadIdx.x];
+    Gs[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    auto gi = [](int c, int c2) { return c * R - c * (c - 1) / 2 + (c2 - c); };
+    for (int c = 0; c < R; ++c) {
+      double d = Gs[gi(c, c)];
+      for (int k = 0; k < c; ++k) d -= Rs[k][c] * Rs[k][c];
+      const double rcc = sqrt(d);
+      const double inv = 1.0 / rcc;
+      Rs[c][c] = rcc;
+      Rinv[c] = inv;
+      for (int c2 = c + 1; c2 < R; ++c2) {
+        double t = Gs[gi(c, c2)];
+        for (int k = 0; k < c; ++k) t -= Rs[k][c] * Rs[k][c2];
+        Rs[c][c2] = t * inv;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = threadIdx.x + (int64_t)j * kOrthBlock;
+    double x[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      double t = (double)a[j][c];
+#pragma unroll
+      for (int k = 0; k < c; ++k) t -= x[k] * Rs[k][c];
+      x[c] = t * Rinv[c];
+    }
+    if (i < n) *reinterpret_cast<f32x4v*>(A + i * R) = f32x4v{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // out = P Q^T (decompress, powersgd.py:58-65); optionally residual = M - out (PowerSGDMemory
 // update, memory/powersgd.py:32-37) in the same pass.  A workgroup owns 1024 columns x kOuterRows
@@ -532,8 +625,12 @@ __global__ __launch_bounds__(256) void psgd_outer_kernel(const float* __restrict
 
 // standard normal draws (Box-Muller on the counter-based generator), for q (powersgd.py:41)
 __global__ __launch_bounds__(256) void normal_kernel(float* __restrict__ x, int64_t n, uint64_t seed) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    x[i] = normal_at(seed, (uint64_t)i);
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; 2 * p < n; p += (int64_t)gridDim.x * 256) {
+    float z0, z1;
+    normal_pair(seed, (uint64_t)p, z0, z1);
+    x[2 * p] = z0;
+    if (2 * p + 1 < n) x[2 * p + 1] = z1;
+  }
 }
 
 }  // namespace grace
@@ -543,6 +640,10 @@ using namespace grace;
 namespace grace {
 template <bool DRAW>
 static void launch_orth(float* A, int64_t n, int32_t r, uint64_t seed, hipStream_t st) {
+  if (r == 4 && n <= kOrth4Rows && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
+    psgd_orth4_kernel<DRAW><<<1, kOrthBlock, 0, st>>>(A, n, seed);
+    return;
+  }
   if (r <= 1) psgd_orth_kernel<1, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
   else if (r <= 2) psgd_orth_kernel<2, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);
   else if (r <= 4) psgd_orth_kernel<4, DRAW><<<1, kOrthBlock, 0, st>>>(A, n, r, seed);

@@ -201,25 +201,6 @@ __device__ __forceinline__ void uniform01x4_k(uint64_t key, uint32_t i, float (&
   }
 }
 
-// 64-bit value moved across lanes by one DPP pattern (two 32-bit DPP movs)
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-// Sum over each 16-lane DPP row by symmetric butterflies (quad xor 1, quad xor 2, half-mirror,
-// mirror): every step adds the same two operands in every lane, so all 16 lanes hold the
-// bit-identical total -- no LDS traffic, no lgkm waits.
-__device__ __forceinline__ double row16_sum(double v) {
-  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_f64<0x141>(v);   // row_half_mirror
-  v += dpp_f64<0x140>(v);   // row_mirror
-  return v;
-}
-
 // A 16-lane row owns a bucket of 128: each lane two quads (l16, l16 + 16; two 16-B loads), the norm is
 // one DPP row reduction; kQNB buckets per row per iteration with every load issued first.
 template <typename CodeT, int VARIANT>

@@ -7,6 +7,8 @@ The default ``wire='u8'`` is the reference's payload."""
 import torch
 
 from grace_amd import ops
+from grace_amd.dist.communicator.allgather import Allgather
+from grace_amd.dist.memory.none import NoneMemory
 from grace_amd.dist import Compressor
 
 
@@ -48,8 +50,6 @@ class SignSGDCompressor(Compressor):
         return ops.sign_majority(codes, world_size, n).view(shape)
 
     def fused_step(self, communicator, tensor, name):
-        from grace_amd.dist.communicator.allgather import Allgather
-        from grace_amd.dist.memory.none import NoneMemory
         if (isinstance(communicator, Allgather) and type(communicator.memory) is NoneMemory
                 and int(communicator.world_size) == 1 and isinstance(tensor, torch.Tensor)
                 and tensor.is_cuda and tensor.dtype == torch.float32):

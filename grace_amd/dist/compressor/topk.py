@@ -10,6 +10,8 @@ import torch
 import torch.distributed as dist
 
 from grace_amd import ops
+from grace_amd.dist.communicator.allgather import Allgather
+from grace_amd.dist.memory.residual import ResidualMemory
 from grace_amd.dist import Compressor
 
 
@@ -44,8 +46,6 @@ class TopKCompressor(Compressor):
 
     def fused_step(self, communicator, tensor, name):
         """compensate -> compress -> update -> send_receive for (TopK, Residual|None, Allgather)."""
-        from grace_amd.dist.communicator.allgather import Allgather
-        from grace_amd.dist.memory.residual import ResidualMemory
         mem = communicator.memory
         if not (isinstance(communicator, Allgather) and type(mem) is ResidualMemory
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):

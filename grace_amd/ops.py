@@ -17,7 +17,13 @@ class GraceDeviceError(TypeError):
     """A grace_amd codec was handed a tensor that is not on the GPU."""
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream():
+    """The current HIP stream of the current device, as a raw pointer (no Stream object)."""
+    if _raw_stream is not None:
+        return _raw_stream(torch.cuda.current_device())
     return torch.cuda.current_stream().cuda_stream
 
 
