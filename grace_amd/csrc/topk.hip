@@ -63,6 +63,7 @@ constexpr int kSample = kSampleRuns * kSampleRunLen;       // 32768 keys, 32 per
 constexpr int kFinBlocks = GRACE_FIN_BLOCKS;
 constexpr int kFinPer = 8;                                 // candidates per thread per round
 
+
 struct TopkCtl {
   uint32_t thr_lo;
   uint32_t thr_hi;
@@ -273,7 +274,7 @@ __device__ __forceinline__ int2 ld_agent_i2(const int2* p) {
 
 // Exact single-workgroup radix select: returns T such that exactly `need` items of src have
 // composite >= T (composites are unique).  6 passes of 11/11/11/11/11/9 bits.
-template <typename Src>
+template <int BLOCK = kSelBlock, typename Src>
 __device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, uint32_t* hist,
                                       uint32_t* s_w, uint32_t* s_res) {
   uint64_t prefix = 0, pmask = 0;
@@ -281,15 +282,15 @@ __device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, 
   for (int p = 0; p < 6; ++p) {
     const int shift = p < 5 ? 53 - 11 * p : 0;
     const uint32_t dmask = p < 5 ? 2047u : 511u;
-    for (int b = threadIdx.x; b < 2048; b += kSelBlock) hist[b] = 0;
+    for (int b = threadIdx.x; b < 2048; b += BLOCK) hist[b] = 0;
     __syncthreads();
-    for (int64_t j = threadIdx.x; j < N; j += kSelBlock) {
+    for (int64_t j = threadIdx.x; j < N; j += BLOCK) {
       const uint64_t c = src(j);
       if ((c & pmask) == prefix) atomicAdd(&hist[(c >> shift) & dmask], 1u);
     }
     __syncthreads();
     uint32_t above;
-    const int d = find_bin_desc<kSelBlock, 2048>(hist, rem, s_w, s_res, &above);
+    const int d = find_bin_desc<BLOCK, 2048>(hist, rem, s_w, s_res, &above);
     rem -= above;
     prefix |= (uint64_t)d << shift;
     pmask |= (uint64_t)dmask << shift;
@@ -821,48 +822,6 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
   if (tid < 4) sm.cnt[tid] = 0;
 }
 
-// Persistent, software-pipelined variant: gridDim.x resident workgroups walk their full chunks
-// group by group with the next group's loads (across chunk boundaries too) in flight while the
-// current group is classified, so a chunk's flush overlaps the next chunk's first loads.
-template <bool HAS_RES, int MODE>
-__global__ __launch_bounds__(kMainBlock) void topk_main_pp(StepArgs a, TopkWs w) {
-  __shared__ MainShared sm;
-  constexpr int NG = kMainVec / kGroup;
-  const int tid = threadIdx.x;
-  for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
-  if (tid < 4) sm.cnt[tid] = 0;
-  const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
-  const int64_t nfull = a.n / kMainChunk;
-  const int64_t nmine = (int64_t)blockIdx.x < nfull ? (nfull - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int64_t steps = nmine * NG;
-  const int64_t lane4 = (int64_t)tid * 4;
-  auto gaddr = [&](int64_t st) {
-    const int64_t c = (int64_t)blockIdx.x + (st / NG) * gridDim.x;
-    return c * kMainChunk + lane4 + (st % NG) * (int64_t)(kGroup * kMainBlock * 4);
-  };
-  __syncthreads();
-  float4 rc[kGroup], gc[kGroup];
-  if (steps) load_group<HAS_RES, true>(a, gaddr(0), rc, gc);
-#pragma unroll 1
-  for (int64_t st = 0; st < steps; ++st) {
-    float4 rn[kGroup], gn[kGroup];
-    if (st + 1 < steps) load_group<HAS_RES, true>(a, gaddr(st + 1), rn, gn);
-    classify_group<HAS_RES, MODE, true>(a, w, sm, lo, hi, sh, gaddr(st), rc, gc);
-    if (st % NG == NG - 1) flush_staged(a, w, sm, lo, sh);
-#pragma unroll
-    for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
-  }
-  if (nfull * kMainChunk < a.n && (int64_t)blockIdx.x == nfull % gridDim.x) {
-    main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, nfull);
-    flush_staged(a, w, sm, lo, sh);
-  }
-  __syncthreads();
-  for (int b = tid; b < kHistBins; b += kMainBlock) {
-    const uint32_t h = sm.hist[b];
-    if (h) atomicAdd(&w.hist[b * kHistStride], h);
-  }
-}
-
 template <bool HAS_RES, int MODE, bool VEC>
 __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   __shared__ MainShared sm;
@@ -899,25 +858,13 @@ __device__ __forceinline__ void emit(const StepArgs& a, uint32_t pos, int64_t i,
   if constexpr (MODE == kDenseFused) a.out[i] = 0.f + v;   // (0 + d) of the Python sum
 }
 
-// t as recorded by the main pass (fallback input)
-template <int MODE>
-struct MainT {
-  const float* g; const float* r; const float* out;
-  __device__ float operator()(int64_t i) const {
-    if constexpr (MODE == kDenseNone) return g[i];
-    if constexpr (MODE == kDenseRes) return r[i];
-    const float o = out[i];
-    return f2u(o) != 0u ? o : r[i];
-  }
-};
-
 // Ordered (ascending index) single-workgroup write of every element with composite >= T over a
 // source f(i) of length n: payload from `pos0`, dense outputs rewritten for every element.
-template <int MODE, typename F>
+template <int MODE, int BLOCK = kSelBlock, typename F>
 __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, uint64_t T,
                                      uint32_t pos0, uint32_t* s_w) {
   uint32_t run = pos0;
-  for (int64_t j0 = 0; j0 < n; j0 += kSelBlock) {
+  for (int64_t j0 = 0; j0 < n; j0 += BLOCK) {
     const int64_t i = j0 + threadIdx.x;
     float v = 0.f;
     bool sel = false;
@@ -926,7 +873,7 @@ __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, u
       sel = comp_key(abs_key(v), (uint32_t)i) >= T;
     }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<kSelBlock>(sel ? 1u : 0u, s_w, &tot);
+    const uint32_t ex = block_excl_scan<BLOCK>(sel ? 1u : 0u, s_w, &tot);
     if (i < n) {
       if (sel) {
         emit<MODE>(a, run + ex, i, v);
@@ -939,42 +886,83 @@ __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, u
   }
 }
 
-// 3. finalize (+ boundary): every workgroup scans the candidate histogram (2 bins per thread) for
-// the boundary bin B and the payload base of every bin above it; each selected candidate takes its
-// slot from a per-bin cursor (atomics spread over the ~1000 live bins, one 128-B line each, not one
-// hot counter), the boundary bin's entries go to the boundary list.  The last workgroup to arrive
-// (release -> ticket -> acquire) then ranks the boundary list exactly by (key, -index) -- or, if
-// the sampled bracket failed or a list overflowed, runs the exact single-workgroup radix select
-// over the whole bucket (slow, rare, same result).
-template <int MODE>
+// 3. finalize (+ boundary): every finalize workgroup scans the candidate histogram for the
+// boundary bin B; candidates above B go to the payload (one block scan + one global atomic per
+// round), those in B to the boundary list.  The last workgroup to arrive then ranks the boundary
+// list exactly by (key, -index) -- or, if the sampled bracket failed or a list overflowed, runs the
+// exact single-workgroup radix select over the whole bucket (slow, rare, same result).
+// Generic over the workgroup size and over agent-scope loads (AG: for a caller that reads data other
+// workgroups wrote earlier in the same launch).  A main + finalize fusion built on it (write-through
+// main stores, the last 64 chunks finalizing) was correct but 30 us slower per step, so the
+// finalize stays its own launch.
+constexpr int kPairCap = 1024;   // boundary lists up to this size are ranked pairwise
+
+template <int BLOCK>
+struct FinShared {
+  uint32_t s_w[BLOCK / kWave + 1];
+  uint32_t hist[2048];
+  uint64_t s_comp[kPairCap];
+  int2 s_ent[kPairCap];
+  uint32_t s_res[2];
+  int s_B;
+  uint32_t s_need, s_pos, s_last;
+};
+
+template <bool AG>
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
+  if constexpr (AG) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool AG>
+__device__ __forceinline__ float ld_f32(const float* p) {
+  if constexpr (AG) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+template <bool AG>
+__device__ __forceinline__ int2 ld_i2(const int2* p) {
+  if constexpr (AG) return ld_agent_i2(p);
+  return *p;
+}
+
+// t as recorded by the main pass (fallback input); agent-scope loads when AG
+template <int MODE, bool AG>
+struct MainTs {
+  const float* g; const float* r; const float* out;
+  __device__ float operator()(int64_t i) const {
+    if constexpr (MODE == kDenseNone) return g[i];
+    if constexpr (MODE == kDenseRes) return ld_f32<AG>(r + i);
+    const float o = ld_f32<AG>(out + i);
+    return f2u(o) != 0u ? o : ld_f32<AG>(r + i);
+  }
+};
+
+template <int MODE, int BLOCK, bool AG>
 __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint32_t need, uint32_t nb,
-                              uint32_t* hist, uint64_t* s_comp, int2* s_ent, uint32_t* s_w,
-                              uint32_t* s_res, uint32_t* s_pos) {
+                              FinShared<BLOCK>& fs) {
   const uint32_t k = (uint32_t)a.k;
   if (ok) {
     if (need == 0) return;
     const uint32_t pos0 = k - need;
-    if (nb <= (uint32_t)kSelBlock) {
+    if (nb <= (uint32_t)kPairCap) {
       // rank by pairwise comparison of unique composites; G adjacent lanes share one entry's
-      // comparisons (G = 4 at nb = 256) and combine their counts with xor-shuffles
-      const int j = threadIdx.x;
+      // comparisons and combine their counts with xor-shuffles
       const int nbi = (int)nb;
-      if (j < nbi) {
+      for (int j = threadIdx.x; j < nbi; j += BLOCK) {
         const int2 e = ld_agent_i2(w.bnd + j);
-        s_ent[j] = e;
-        s_comp[j] = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
+        fs.s_ent[j] = e;
+        fs.s_comp[j] = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
       }
       int G = 1;
-      while (G < 16 && nbi * (G * 2) <= kSelBlock) G *= 2;
+      while (G < 16 && nbi * (G * 2) <= BLOCK) G *= 2;
       __syncthreads();
-      const int el = j / G, part = j % G;
-      if (el < nbi) {
-        const uint64_t me = s_comp[el];
+      const int part = threadIdx.x % G;
+      for (int el = threadIdx.x / G; el < nbi; el += BLOCK / G) {
+        const uint64_t me = fs.s_comp[el];
         uint32_t rank = 0;
-        for (int q = part; q < nbi; q += G) rank += s_comp[q] > me;
+        for (int q = part; q < nbi; q += G) rank += fs.s_comp[q] > me;
         for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
         if (part == 0 && rank < need) {
-          const int2 e = s_ent[el];
+          const int2 e = fs.s_ent[el];
           emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
         }
       }
@@ -985,13 +973,13 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
       const int2 e = ld_agent_i2(bnd + j);
       return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
     };
-    const uint64_t T = block_select_comp(src, nb, need, hist, s_w, s_res);
-    if (threadIdx.x == 0) *s_pos = 0;
+    const uint64_t T = block_select_comp<BLOCK>(src, nb, need, fs.hist, fs.s_w, fs.s_res);
+    if (threadIdx.x == 0) fs.s_pos = 0;
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < nb; j += kSelBlock) {
+    for (uint32_t j = threadIdx.x; j < nb; j += BLOCK) {
       const int2 e = ld_agent_i2(bnd + j);
       if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) {
-        const uint32_t p = atomicAdd(s_pos, 1u);
+        const uint32_t p = atomicAdd(&fs.s_pos, 1u);
         emit<MODE>(a, pos0 + p, e.x, u2f((uint32_t)e.y));
       }
     }
@@ -999,96 +987,92 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
   }
   // ---- exact fallback over the whole bucket (bracket failed or a list overflowed)
   if (threadIdx.x == 0) w.ctl->status = 1;
-  const MainT<MODE> f{a.g, a.r, a.out};
+  const MainTs<MODE, AG> f{a.g, a.r, a.out};
   auto src = [f](int64_t i) { return comp_key(abs_key(f(i)), (uint32_t)i); };
-  const uint64_t T = block_select_comp(src, a.n, k, hist, s_w, s_res);
-  block_write_selected<MODE>(a, f, a.n, T, 0u, s_w);
+  const uint64_t T = block_select_comp<BLOCK>(src, a.n, k, fs.hist, fs.s_w, fs.s_res);
+  block_write_selected<MODE, BLOCK>(a, f, a.n, T, 0u, fs.s_w);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
-  constexpr int PER = kHistBins / kSelBlock;
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t hist[2048];
-  __shared__ uint64_t s_comp[kSelBlock];
-  __shared__ int2 s_ent[kSelBlock];
-  __shared__ uint32_t s_res[2];
-  __shared__ int s_B;
-  __shared__ uint32_t s_need, s_pos, s_last;
-  STAMP(w.ctl, 8);
-  const TopkCtl c = *w.ctl;
-  const uint32_t k = (uint32_t)a.k;
-  const bool ok = c.n_sure <= k && (uint64_t)c.n_sure + c.n_cand >= k && c.n_cand <= (uint64_t)w.cap;
+// finalize workgroup `fi` of `fcnt`; returns true in the workgroup that ran the boundary step
+template <int MODE, int BLOCK, bool AG>
+__device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
+  constexpr int PER = kHistBins / BLOCK;
   const int t = threadIdx.x;
+  const uint32_t n_sure = ld_u32<AG>(&w.ctl->n_sure), n_cand = ld_u32<AG>(&w.ctl->n_cand);
+  const uint32_t thr_lo = w.ctl->thr_lo, shift = w.ctl->shift;   // written by the bracket launch
+  const uint32_t k = (uint32_t)a.k;
+  const bool ok = n_sure <= k && (uint64_t)n_sure + n_cand >= k && n_cand <= (uint64_t)w.cap;
   {  // the bracket's sample histograms are free again: zero them for the next step
     constexpr int kZ4 = (kBracketBins + kCoarseBins) / 4;
-    static_assert(kZ4 <= kFinBlocks * kSelBlock, "finalize grid covers the sample histograms");
-    const int z = blockIdx.x * kSelBlock + t;
-    if (z < kBracketBins / 4) reinterpret_cast<uint4*>(w.shist)[z] = make_uint4(0, 0, 0, 0);
-    else if (z < kZ4) reinterpret_cast<uint4*>(w.chist)[z - kBracketBins / 4] = make_uint4(0, 0, 0, 0);
+    for (int z = fi * BLOCK + t; z < kZ4; z += fcnt * BLOCK) {
+      if (z < kBracketBins / 4) reinterpret_cast<uint4*>(w.shist)[z] = make_uint4(0, 0, 0, 0);
+      else reinterpret_cast<uint4*>(w.chist)[z - kBracketBins / 4] = make_uint4(0, 0, 0, 0);
+    }
   }
   int B = -1;
   uint32_t need = 0, nb = 0;
   if (ok) {
-    const uint32_t target = k - c.n_sure;
+    const uint32_t target = k - n_sure;
     const int top = kHistBins - 1 - t * PER;
     uint32_t h[PER], sum = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) { h[j] = w.hist[(top - j) * kHistStride]; sum += h[j]; }
-    if (t == 0) { s_B = -1; s_need = 0; }
-    const uint32_t ex = block_excl_scan<kSelBlock>(sum, s_w, nullptr);
+    for (int j = 0; j < PER; ++j) { h[j] = ld_u32<AG>(&w.hist[(top - j) * kHistStride]); sum += h[j]; }
+    if (t == 0) { fs.s_B = -1; fs.s_need = 0; }
+    const uint32_t ex = block_excl_scan<BLOCK>(sum, fs.s_w, nullptr);
     uint32_t acc = ex;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (target > 0 && acc < target && target <= acc + h[j]) { s_B = top - j; s_need = target - acc; }
+      if (target > 0 && acc < target && target <= acc + h[j]) { fs.s_B = top - j; fs.s_need = target - acc; }
+      if (target > 0 && acc < target && target <= acc + h[j]) fs.s_res[0] = h[j];
       acc += h[j];
     }
     __syncthreads();
-    B = s_B;
-    need = s_need;
-    nb = B >= 0 ? w.hist[B * kHistStride] : 0u;
-    if (blockIdx.x == 0 && t == 0) {
+    B = fs.s_B;
+    need = fs.s_need;
+    nb = B >= 0 ? fs.s_res[0] : 0u;
+    __syncthreads();
+    if (fi == 0 && t == 0) {
       w.ctl->boundary_bin = B;
       w.ctl->need = need;
       w.ctl->n_bnd = nb;
     }
-    STAMP(w.ctl, 9);
+    STAMP_IF(fi == 0, w.ctl, 9);
     // residual-only mode: sure entries still hold t in r; zero them now
     if constexpr (MODE == kDenseRes) {
-      for (uint32_t j = blockIdx.x * kSelBlock + t; j < c.n_sure; j += gridDim.x * kSelBlock) {
-        const float v = a.vals[j];
-        a.r[a.idx[j]] = v - v;
+      for (uint32_t j = fi * BLOCK + t; j < n_sure; j += fcnt * BLOCK) {
+        const float v = ld_f32<AG>(a.vals + j);
+        a.r[(int32_t)ld_u32<AG>(reinterpret_cast<const uint32_t*>(a.idx) + j)] = v - v;
       }
     }
     if (B >= 0) {
       // contiguous slice per workgroup, kFinPer candidates per thread per round held in registers;
       // one block scan places them, one global atomic per list per round reserves the space
-      const uint32_t per = (c.n_cand + gridDim.x - 1) / gridDim.x;
-      const uint32_t b0 = blockIdx.x * per, b1 = min(c.n_cand, b0 + per);
-      for (uint32_t r0 = b0; r0 < b1; r0 += kSelBlock * kFinPer) {
+      const uint32_t per = (n_cand + fcnt - 1) / fcnt;
+      const uint32_t b0 = fi * per, b1 = min(n_cand, b0 + per);
+      for (uint32_t r0 = b0; r0 < b1; r0 += BLOCK * kFinPer) {
         int2 e[kFinPer];
-        uint32_t fs = 0, fb = 0;
+        uint32_t fsel = 0, fb = 0;
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u) {
-          const uint32_t j = r0 + u * kSelBlock + t;
-          e[u] = j < b1 ? w.cand[j] : make_int2(0, 0);
-          const int bin = j < b1 ? (int)((abs_key(u2f((uint32_t)e[u].y)) - c.thr_lo) >> c.shift) : -1;
-          fs |= (uint32_t)(bin > B) << u;
+          const uint32_t j = r0 + u * BLOCK + t;
+          e[u] = ld_i2<AG>(w.cand + (j < b1 ? j : b0));   // clamped, unconditional
+          const int bin = j < b1 ? (int)((abs_key(u2f((uint32_t)e[u].y)) - thr_lo) >> shift) : -1;
+          fsel |= (uint32_t)(bin > B) << u;
           fb |= (uint32_t)(bin == B) << u;
         }
-        const uint32_t packed = (uint32_t)__popc(fs) | ((uint32_t)__popc(fb) << 16);
+        const uint32_t packed = (uint32_t)__popc(fsel) | ((uint32_t)__popc(fb) << 16);
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<kSelBlock>(packed, s_w, &tot);
+        const uint32_t ex = block_excl_scan<BLOCK>(packed, fs.s_w, &tot);
         if (t == 0) {
-          s_res[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
-          s_res[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
+          fs.s_res[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
+          fs.s_res[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
         }
         __syncthreads();
-        uint32_t ps = c.n_sure + s_res[0] + (ex & 0xFFFFu), pb = s_res[1] + (ex >> 16);
+        uint32_t ps = n_sure + fs.s_res[0] + (ex & 0xFFFFu), pb = fs.s_res[1] + (ex >> 16);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u) {
-          if ((fs >> u) & 1u) {
+          if ((fsel >> u) & 1u) {
             const float v = u2f((uint32_t)e[u].y);
             a.vals[ps] = v;
             a.idx[ps] = e[u].x;
@@ -1103,16 +1087,24 @@ __global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w)
   }
   // arrival: every wave's (write-through) boundary stores complete, then one ticket per
   // workgroup; the last one finishes the boundary bin
-  STAMP(w.ctl, 10);
+  STAMP_IF(fi == 0, w.ctl, 10);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
+  if (t == 0) fs.s_last = atomicAdd(&w.ctl->ticket, 1u) == (uint32_t)fcnt - 1;
   __syncthreads();
-  if (!s_last) return;
+  if (!fs.s_last) return false;
   STAMP_IF(true, w.ctl, 11);
-  boundary_work<MODE>(a, w, ok, need, nb, hist, s_comp, s_ent, s_w, s_res, &s_pos);
+  boundary_work<MODE, BLOCK, AG>(a, w, ok, need, nb, fs);
   __syncthreads();
   STAMP_IF(true, w.ctl, 12);
+  return true;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
+  __shared__ FinShared<kSelBlock> fs;
+  STAMP(w.ctl, 8);
+  finalize_run<MODE, kSelBlock, false>(a, w, blockIdx.x, gridDim.x, fs);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1169,15 +1161,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   static_assert(kSmallN >= 2 * kSampleBlock, "bracket grid covers the histogram zeroing");
   topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
-  unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
-#ifdef GRACE_MAIN_PERSIST
-  if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
-#endif
-#ifdef GRACE_MAIN_PP
-  if (vec && nblk > (unsigned)GRACE_MAIN_PP)
-    launch_timed(topk_main_pp<HAS_RES, MODE>, dim3(GRACE_MAIN_PP), dim3(kMainBlock), s, a, w);
-  else
-#endif
+  const unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
   if (vec)
     launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
   else
