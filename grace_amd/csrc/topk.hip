@@ -993,6 +993,23 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
   block_write_selected<MODE, BLOCK>(a, f, a.n, T, 0u, fs.s_w);
 }
 
+// payload + dense writes of a round's above-boundary candidates (bits of fsel), from slot ps on
+template <int MODE>
+__device__ __forceinline__ void write_selected(const StepArgs& a, const int2 (&e)[kFinPer], uint32_t fsel,
+                                               uint32_t ps) {
+#pragma unroll
+  for (int u = 0; u < kFinPer; ++u) {
+    if ((fsel >> u) & 1u) {
+      const float v = u2f((uint32_t)e[u].y);
+      a.vals[ps] = v;
+      a.idx[ps] = e[u].x;
+      if constexpr (MODE != kDenseNone) a.r[e[u].x] = v - v;
+      if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
+      ++ps;
+    }
+  }
+}
+
 // finalize workgroup `fi` of `fcnt`; returns true in the workgroup that ran the boundary step
 template <int MODE, int BLOCK, bool AG>
 __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
@@ -1011,6 +1028,9 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   }
   int B = -1;
   uint32_t need = 0, nb = 0;
+  int2 e[kFinPer];
+  uint32_t fsel = 0, ps = 0;
+  bool defer = false;
   if (ok) {
     const uint32_t target = k - n_sure;
     const int top = kHistBins - 1 - t * PER;
@@ -1046,12 +1066,15 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
     }
     if (B >= 0) {
       // contiguous slice per workgroup, kFinPer candidates per thread per round held in registers;
-      // one block scan places them, one global atomic per list per round reserves the space
+      // one block scan places them, one global atomic per list per round reserves the space.  The
+      // boundary-list stores go first; a single-round slice (the common case) defers its payload
+      // and dense writes past the arrival ticket, so the boundary ranking does not wait for them.
       const uint32_t per = (n_cand + fcnt - 1) / fcnt;
       const uint32_t b0 = fi * per, b1 = min(n_cand, b0 + per);
+      defer = b1 > b0 && b1 - b0 <= (uint32_t)(BLOCK * kFinPer);
       for (uint32_t r0 = b0; r0 < b1; r0 += BLOCK * kFinPer) {
-        int2 e[kFinPer];
-        uint32_t fsel = 0, fb = 0;
+        uint32_t fb = 0;
+        fsel = 0;
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u) {
           const uint32_t j = r0 + u * BLOCK + t;
@@ -1068,20 +1091,13 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
           fs.s_res[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
         }
         __syncthreads();
-        uint32_t ps = n_sure + fs.s_res[0] + (ex & 0xFFFFu), pb = fs.s_res[1] + (ex >> 16);
+        ps = n_sure + fs.s_res[0] + (ex & 0xFFFFu);
+        uint32_t pb = fs.s_res[1] + (ex >> 16);
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kFinPer; ++u) {
-          if ((fsel >> u) & 1u) {
-            const float v = u2f((uint32_t)e[u].y);
-            a.vals[ps] = v;
-            a.idx[ps] = e[u].x;
-            if constexpr (MODE != kDenseNone) a.r[e[u].x] = v - v;
-            if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
-            ++ps;
-          }
+        for (int u = 0; u < kFinPer; ++u)
           if ((fb >> u) & 1u) st_agent_i2(w.bnd + pb++, e[u]);
-        }
+        if (!defer) write_selected<MODE>(a, e, fsel, ps);
       }
     }
   }
@@ -1092,6 +1108,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   __syncthreads();
   if (t == 0) fs.s_last = atomicAdd(&w.ctl->ticket, 1u) == (uint32_t)fcnt - 1;
   __syncthreads();
+  if (defer) write_selected<MODE>(a, e, fsel, ps);
   if (!fs.s_last) return false;
   STAMP_IF(true, w.ctl, 11);
   boundary_work<MODE, BLOCK, AG>(a, w, ok, need, nb, fs);
