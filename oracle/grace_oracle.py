@@ -273,17 +273,21 @@ def qsgd_decode(codes, norms, quantum_num, bucket_size, numel):
     return ((norm / F32(quantum_num)).astype(F32) * codes.astype(F32)).astype(F32)
 
 
-def qsgd_cuda_compress(x, u, quantum_num, bucket_size):
+def qsgd_cuda_compress(x, u, quantum_num, bucket_size, norms=None):
     """qsgd_cuda restatement (qsgd_cuda.cu:320-388): f64 bucket norms over finite elements,
-    level = (float)level / (float)norm * |x|, NaN/Inf -> -128.  Parity unpinned (CUDA only)."""
+    level = (float)level / (float)norm * |x|, NaN/Inf -> -128.  Parity unpinned (CUDA only).
+    ``norms`` (optional) injects the bucket norms, as qsgd_compress does."""
     xf = _f32(x).ravel()
     n = xf.size
     nb = -(-n // bucket_size)
-    norms = np.zeros(nb, dtype=np.float64)
     fin = np.isfinite(xf)
-    xd = np.where(fin, xf.astype(np.float64), 0.0)
-    np.add.at(norms, np.arange(n) // bucket_size, xd * xd)
-    norms = np.sqrt(norms)
+    if norms is None:
+        norms = np.zeros(nb, dtype=np.float64)
+        xd = np.where(fin, xf.astype(np.float64), 0.0)
+        np.add.at(norms, np.arange(n) // bucket_size, xd * xd)
+        norms = np.sqrt(norms)
+    else:
+        norms = np.asarray(norms, dtype=np.float64)
     nsc = norms.astype(F32)[np.arange(n) // bucket_size]
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         lf = ((F32(quantum_num) / nsc).astype(F32) * np.abs(xf)).astype(F32)

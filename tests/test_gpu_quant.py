@@ -207,3 +207,81 @@ def test_segmented_terngrad_decode_world3_ragged():
     decs = [codes[w * n:(w + 1) * n].astype(np.float32) * scal[w * len(sizes) + seg] for w in range(3)]
     exp = (O.python_sum(decs) / np.float32(3)).astype(np.float32)
     assert same_bits(out, exp)
+
+
+def test_qsgd_cuda_variant_vs_oracle_with_specials():
+    """QSGDCompressor_CUDA semantics (variant 1) on the bucket-of-128 row kernels: f64 norms over
+    finite elements, NaN/Inf -> -128, decoded back to NaN; ragged segments (parity unpinned: the
+    oracle restates qsgd_cuda.cu:320-388, CUDA-only in the reference)."""
+    rng = np.random.default_rng(8)
+    sizes = [130, 1, 4096, 257, 128]
+    xs = [(rng.standard_normal(n) * 0.01).astype(np.float32) for n in sizes]
+    xs[0][[3, 77]] = [np.nan, np.inf]
+    xs[2][1000:1128] = 0.0                       # an all-zero bucket
+    xs[3][-1] = -np.inf
+    flat = np.concatenate(xs)
+    u = rng.random(flat.size, dtype=np.float32)
+    codes, norms = ops.qsgd_compress(_t(flat), 127, 128, sizes=sizes, variant=1, u=_t(u))
+    dec = _np(ops.qsgd_decompress(codes, norms, 127, 128, flat.size, sizes=sizes, variant=1))
+    off = noff = 0
+    cn, nn = _np(codes), _np(norms)
+    for n, x in zip(sizes, xs):
+        nb = -(-n // 128)
+        _, ref_n = O.qsgd_cuda_compress(x, u[off:off + n], 127, 128)
+        # device norms: f64 sums in another order, so within 1 ulp of the oracle's; the codewords
+        # are then checked bit-exactly given the device norms
+        assert ops.isclose_f32_ulps(nn[noff:noff + nb], ref_n.astype(np.float32), 1), n
+        exp_c, exp_n = O.qsgd_cuda_compress(x, u[off:off + n], 127, 128, norms=nn[noff:noff + nb])
+        assert np.array_equal(cn[off:off + n], exp_c), n
+        d = dec[off:off + n]
+        assert np.all(np.isnan(d[exp_c == -128]))
+        ok = exp_c != -128
+        exp_d = ((exp_n.astype(np.float32)[np.arange(n) // 128] / np.float32(127)).astype(np.float32)
+                 * exp_c.astype(np.float32)).astype(np.float32)
+        assert same_bits(d[ok], exp_d[ok]), n
+        off += n
+        noff += nb
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_qsgd_bucket_decoder_multi_rank_aggregate(world):
+    """The bucket-of-128 decoder's rank-ordered W-payload aggregate and divisor against the oracle
+    over ragged segments (including a code stride that is not a multiple of 4)."""
+    rng = np.random.default_rng(world)
+    sizes = [5, 300, 4096, 1, 131]
+    n = sum(sizes)
+    nb = sum(-(-s // 128) for s in sizes)
+    cs, ns = [], []
+    for w in range(world):
+        x = (rng.standard_normal(n) * 0.01).astype(np.float32)
+        c, nm = ops.qsgd_compress(_t(x), 127, 128, sizes=sizes, u=_t(rng.random(n, dtype=np.float32)))
+        cs.append(_np(c))
+        ns.append(_np(nm))
+    out = _np(ops.qsgd_decompress(_t(np.concatenate(cs)), _t(np.concatenate(ns)), 127, 128, n, sizes=sizes,
+                                  world=world, aggregate=True, divisor=float(world)))
+    bidx = np.concatenate([sum(-(-sizes[j] // 128) for j in range(i)) + np.arange(s) // 128
+                           for i, s in enumerate(sizes)])
+    decs = [((ns[w][bidx] / np.float32(127)).astype(np.float32) * cs[w].astype(np.float32)).astype(np.float32)
+            for w in range(world)]
+    exp = (O.python_sum(decs) / np.float32(world)).astype(np.float32)
+    assert nb == ns[0].size
+    assert same_bits(out, exp)
+
+
+def test_terngrad_workspace_reuse_across_shapes():
+    """The TernGrad workspace is shared by calls of different unit counts: its arrival counters
+    must stay zeroed whichever shape ran before (a regression the segmented test first caught).
+    Segmented results must equal each tensor compressed on its own, call after call."""
+    rng = np.random.default_rng(9)
+    shapes = [[70000, 3], [5], [16384 * 3 + 1, 2, 40000], [9]]
+    for sizes in shapes * 2:
+        xs = [(rng.standard_normal(s) * 0.01).astype(np.float32) for s in sizes]
+        flat = np.concatenate(xs)
+        u = rng.random(flat.size, dtype=np.float32)
+        codes, scal = ops.terngrad_compress(_t(flat), sizes=sizes, u=_t(u))
+        off = 0
+        for i, (s, x) in enumerate(zip(sizes, xs)):
+            c1, s1 = ops.terngrad_compress(_t(x), u=_t(u[off:off + s]))
+            assert same_bits(_np(codes[off:off + s]), _np(c1)), (sizes, i)
+            assert same_bits(_np(scal[i:i + 1]), _np(s1)), (sizes, i)
+            off += s
