@@ -78,7 +78,9 @@ struct TopkCtl {
   uint32_t ticket;     // finalize kernel arrival counter
   uint32_t n_bacc;     // boundary-list fill counter
   uint32_t bticket;    // bracket kernel arrival counter (reset by its last workgroup)
-  uint32_t pad[3];
+  uint32_t bar_count;  // finalize grid barrier (parallel exact fallback): arrivals
+  uint32_t bar_gen;    //   and generation
+  uint32_t pad;
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 
@@ -931,8 +933,8 @@ struct MainTs {
   __device__ float operator()(int64_t i) const {
     if constexpr (MODE == kDenseNone) return g[i];
     if constexpr (MODE == kDenseRes) return ld_f32<AG>(r + i);
-    const float o = ld_f32<AG>(out + i);
-    return f2u(o) != 0u ? o : ld_f32<AG>(r + i);
+    const float o = ld_f32<AG>(out + i), rr = ld_f32<AG>(r + i);   // both issued: no dependent load
+    return f2u(o) != 0u ? o : rr;
   }
 };
 
@@ -1010,6 +1012,148 @@ __device__ __forceinline__ void write_selected(const StepArgs& a, const int2 (&e
   }
 }
 
+// ---- parallel exact fallback (the sampled bracket missed or a list overflowed: in practice massive
+// ties, e.g. a bucket that is mostly exact zeros, or a constant one).  All finalize workgroups
+// (co-resident: 64 of them) radix-select the k-th largest KEY over the whole bucket together, one
+// digit per pass with a grid barrier after each global histogram merge (3 passes); the ties at that
+// key are then taken lowest index first straight from per-slice counts: a count pass and an
+// ordered write pass, each slice in index order after exclusive scans of the (key > T, key == T)
+// counts.  Five streaming passes over t by 64 workgroups instead of one workgroup's radix select
+// and ordered write.  Scratch: the start of the (already re-zeroed) fine sample histogram, zeroed
+// again at the end.
+template <int BLOCK>
+__device__ __forceinline__ void grid_barrier(const TopkWs& w, int fcnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t gen = __hip_atomic_load(&w.ctl->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (atomicAdd(&w.ctl->bar_count, 1u) == (uint32_t)fcnt - 1) {
+      __hip_atomic_store(&w.ctl->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&w.ctl->bar_gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&w.ctl->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 26)) { w.ctl->status = 2; break; }   // bounded: never expected
+      }
+    }
+  }
+  __syncthreads();
+}
+
+constexpr int kFbUnroll = 8;   // parallel fallback: elements in flight per thread
+
+template <int MODE, int BLOCK, bool AG>
+__device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
+  const int t = threadIdx.x;
+  const uint32_t k = (uint32_t)a.k;
+  const int64_t per = (a.n + fcnt - 1) / fcnt;
+  const int64_t s0 = min((int64_t)fi * per, a.n), s1 = min(s0 + per, a.n);
+  uint32_t* gh = w.shist;                      // [3][2048] key-digit histograms
+  uint32_t* cnt = w.shist + 3 * 2048;          // [fcnt][2] per-slice (key > T, key == T) counts
+  if (fi == 0 && t == 0) w.ctl->status = 1;
+  const MainTs<MODE, AG> f{a.g, a.r, a.out};
+  grid_barrier<BLOCK>(w, fcnt);                // every workgroup is past its histogram zeroing
+  // 1. the exact k-th largest key T (31-bit keys: digits of 11, 11 and 9 bits)
+  uint32_t prefix = 0, pmask = 0, rem = k;
+  for (int p = 0; p < 3; ++p) {
+    const int shift = p == 0 ? 20 : (p == 1 ? 9 : 0);
+    const uint32_t dmask = p < 2 ? 2047u : 511u;
+    for (int b = t; b < 2048; b += BLOCK) fs.hist[b] = 0;
+    __syncthreads();
+    for (int64_t i0 = s0 + t; i0 < s1; i0 += BLOCK * kFbUnroll) {
+      uint32_t key[kFbUnroll];
+#pragma unroll
+      for (int u = 0; u < kFbUnroll; ++u) {   // every load issued before any is used
+        const int64_t i = i0 + (int64_t)u * BLOCK;
+        key[u] = abs_key(f(i < s1 ? i : s0));
+      }
+#pragma unroll
+      for (int u = 0; u < kFbUnroll; ++u)
+        if (i0 + (int64_t)u * BLOCK < s1 && (key[u] & pmask) == prefix) atomicAdd(&fs.hist[(key[u] >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    for (int b = t; b < 2048; b += BLOCK)
+      if (fs.hist[b]) atomicAdd(&gh[p * 2048 + b], fs.hist[b]);
+    grid_barrier<BLOCK>(w, fcnt);
+    for (int b = t; b < 2048; b += BLOCK)
+      fs.hist[b] = __hip_atomic_load(&gh[p * 2048 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    uint32_t above;
+    const int d = find_bin_desc<BLOCK, 2048>(fs.hist, rem, fs.s_w, fs.s_res, &above);
+    rem -= above;
+    prefix |= (uint32_t)d << shift;
+    pmask |= dmask << shift;
+  }
+  const uint32_t T = prefix, need_eq = rem;    // take every key > T and the need_eq lowest-index == T
+  // 2. per-slice counts
+  uint32_t ngt = 0, neq = 0;
+  for (int64_t i0 = s0 + t; i0 < s1; i0 += BLOCK * kFbUnroll) {
+    uint32_t key[kFbUnroll];
+#pragma unroll
+    for (int u = 0; u < kFbUnroll; ++u) {
+      const int64_t i = i0 + (int64_t)u * BLOCK;
+      key[u] = abs_key(f(i < s1 ? i : s0));
+    }
+#pragma unroll
+    for (int u = 0; u < kFbUnroll; ++u) {
+      const bool in = i0 + (int64_t)u * BLOCK < s1;
+      ngt += in && key[u] > T;
+      neq += in && key[u] == T;
+    }
+  }
+  uint32_t tgt, teq;
+  block_excl_scan<BLOCK>(ngt, fs.s_w, &tgt);
+  block_excl_scan<BLOCK>(neq, fs.s_w, &teq);
+  if (t == 0) {
+    __hip_atomic_store(&cnt[2 * fi], tgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cnt[2 * fi + 1], teq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  grid_barrier<BLOCK>(w, fcnt);
+  uint32_t gt_run = 0, eq_run = 0;             // before this slice
+  for (int j = 0; j < fi; ++j) {
+    gt_run += __hip_atomic_load(&cnt[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    eq_run += __hip_atomic_load(&cnt[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 3. the slice in index order: selected-before = (# key > T before) + min(# key == T before, need_eq);
+  //    each thread owns kFbUnroll consecutive elements of a round, one block scan per round
+  for (int64_t j0 = s0; j0 < s1; j0 += (int64_t)BLOCK * kFbUnroll) {
+    const int64_t ib = j0 + (int64_t)t * kFbUnroll;
+    float v[kFbUnroll];
+    uint32_t cg = 0, ce = 0;
+#pragma unroll
+    for (int u = 0; u < kFbUnroll; ++u) {
+      v[u] = f(ib + u < s1 ? ib + u : s0);
+      const uint32_t key = abs_key(v[u]);
+      cg += ib + u < s1 && key > T;
+      ce += ib + u < s1 && key == T;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<BLOCK>(cg | (ce << 16), fs.s_w, &tot);
+    uint32_t g_before = gt_run + (ex & 0xFFFFu), e_before = eq_run + (ex >> 16);
+#pragma unroll
+    for (int u = 0; u < kFbUnroll; ++u) {
+      const int64_t i = ib + u;
+      if (i < s1) {
+        const uint32_t key = abs_key(v[u]);
+        const bool gt = key > T, eq = key == T;
+        if (gt || (eq && e_before < need_eq)) {
+          emit<MODE>(a, g_before + min(e_before, need_eq), i, v[u]);
+        } else {
+          if constexpr (MODE != kDenseNone) a.r[i] = v[u];
+          if constexpr (MODE == kDenseFused) a.out[i] = 0.f;
+        }
+        g_before += gt;
+        e_before += eq;
+      }
+    }
+    gt_run += tot & 0xFFFFu;
+    eq_run += tot >> 16;
+  }
+  grid_barrier<BLOCK>(w, fcnt);                // every slice has read the scratch
+  for (int z = fi * BLOCK + t; z < 3 * 2048 + 2 * fcnt; z += fcnt * BLOCK) gh[z] = 0u;
+}
+
 // finalize workgroup `fi` of `fcnt`; returns true in the workgroup that ran the boundary step
 template <int MODE, int BLOCK, bool AG>
 __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
@@ -1019,12 +1163,19 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   const uint32_t thr_lo = w.ctl->thr_lo, shift = w.ctl->shift;   // written by the bracket launch
   const uint32_t k = (uint32_t)a.k;
   const bool ok = n_sure <= k && (uint64_t)n_sure + n_cand >= k && n_cand <= (uint64_t)w.cap;
-  {  // the bracket's sample histograms are free again: zero them for the next step
-    constexpr int kZ4 = (kBracketBins + kCoarseBins) / 4;
-    for (int z = fi * BLOCK + t; z < kZ4; z += fcnt * BLOCK) {
-      if (z < kBracketBins / 4) reinterpret_cast<uint4*>(w.shist)[z] = make_uint4(0, 0, 0, 0);
-      else reinterpret_cast<uint4*>(w.chist)[z - kBracketBins / 4] = make_uint4(0, 0, 0, 0);
+  {  // the bracket's sample histograms are free again: zero them for the next step.  Write-through
+     // (agent scope): the parallel fallback below accumulates into this memory with device
+     // atomics in the same launch, which a dirty zero line left in some XCD's L2 would overwrite
+    constexpr int kZ2 = (kBracketBins + kCoarseBins) / 2;
+    for (int z = fi * BLOCK + t; z < kZ2; z += fcnt * BLOCK) {
+      uint64_t* q = z < kBracketBins / 2 ? reinterpret_cast<uint64_t*>(w.shist) + z
+                                         : reinterpret_cast<uint64_t*>(w.chist) + (z - kBracketBins / 2);
+      __hip_atomic_store(q, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  if (!ok && fcnt > 1 && fcnt <= kFinBlocks) {   // every finalize workgroup: the parallel fallback
+    parallel_exact<MODE, BLOCK, AG>(a, w, fi, fcnt, fs);
+    return fi == 0;
   }
   int B = -1;
   uint32_t need = 0, nb = 0;

@@ -169,3 +169,37 @@ def test_topk_full_bucket_256mib():
     assert same_bits(res[~sel], t[~sel]) and not np.any(res[sel])
     o = _np(out)
     assert same_bits(o[sel], t[sel]) and not np.any(o[~sel])
+
+
+def test_topk_parallel_fallback_sparse_256mib():
+    """A 256 MiB bucket that is 99.75 % exact zeros (k = 1 % > non-zeros: massive ties at 0, so the
+    candidate list overflows): the parallel exact fallback (all finalize workgroups, grid barriers)
+    must give the oracle's result -- every non-zero plus the lowest-index zeros -- in milliseconds,
+    not the single-workgroup path's ~150 ms."""
+    from grace_amd import ops
+    n = 64 * 1024 * 1024
+    k = O.ratio_k(n, 0.01)
+    rng = np.random.default_rng(11)
+    g0 = np.zeros(n, dtype=np.float32)
+    pos = rng.choice(n, size=n // 400, replace=False)
+    g0[pos] = rng.standard_normal(pos.size).astype(np.float32)
+    r0 = np.zeros(n, dtype=np.float32)
+    g, r = torch.from_numpy(g0).to(DEV), torch.from_numpy(r0).to(DEV)
+    out = torch.empty_like(g)
+    ops.topk_residual_step(g, r.clone(), True, 1.0, 1.0, k, out=torch.empty_like(g))   # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _, vals, idx = ops.topk_residual_step(g, r, True, 1.0, 1.0, k, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    assert ops.topk_status(n, k, g.device) == 1
+    assert e0.elapsed_time(e1) < 30.0, e0.elapsed_time(e1)
+    ov, oi = O.topk_select(g0, k)
+    v, i = _sorted_payload(vals, idx)
+    assert np.array_equal(i, oi.astype(np.int64))
+    assert same_bits(v, ov)
+    sel = np.zeros(n, dtype=bool)
+    sel[oi] = True
+    res, o = _np(r), _np(out)
+    assert same_bits(res[~sel], g0[~sel]) and not np.any(res[sel])
+    assert same_bits(o[sel], g0[sel]) and not np.any(o[~sel])
