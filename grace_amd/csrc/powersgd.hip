@@ -57,7 +57,16 @@ __device__ __forceinline__ float sum_partials(const float* __restrict__ p, int64
   return t;
 }
 
+#ifdef GRACE_KFAN
+constexpr int kFan = GRACE_KFAN;
+#else
 constexpr int kFan = 8;                     // slabs per first-level reduction group
+#endif
+#ifdef GRACE_PS_OCC
+#define PS_OCC __attribute__((amdgpu_waves_per_eu(GRACE_PS_OCC, 8)))
+#else
+#define PS_OCC
+#endif
 
 // t[i] = sum over k < cnt (in order) of p[k * stride + f0 + threadIdx.x + i * 256], i < 4, for
 // entries below `nent`; 4 x 8 loads in flight per round
@@ -86,6 +95,24 @@ __device__ __forceinline__ void sum_partials4(const float* __restrict__ p, int64
   }
 }
 
+// 16-B write-through partials (buffer ops with the sc1 cache policy, aux = 16): one fabric write per
+// 16 B instead of one per dword, and loads that bypass the (non-coherent) local L2
+constexpr int kSc1 = 16;
+// elementwise sum over k < cnt (in order) of the 16-B runs at byte offset off + k * sb of `rs`,
+// 8 loads in flight
+__device__ __forceinline__ f32x4v sum_partials_v4(__amdgpu_buffer_rsrc_t rs, int sb, int cnt, int off) {
+  f32x4v t = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < cnt; k += 8) {
+    f32x4v v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + (k + u < cnt ? k + u : 0) * sb, 0, kSc1);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k + u < cnt) t += v[u];
+  }
+  return t;
+}
+
 // returns true in exactly one (the last-arriving) workgroup of the tile; every thread's partial
 // stores (st_agent) are complete before the workgroup takes its ticket
 __device__ __forceinline__ bool last_arrival(uint32_t* ticket, uint32_t expected) {
@@ -102,47 +129,64 @@ __device__ __forceinline__ bool last_arrival(uint32_t* ticket, uint32_t expected
 }
 
 // ------------------------------------------------------------------------------------------------
-// Both contractions stream M through LDS in tiles of 16 rows x 256 columns: every global load is
-// one row's 1 KB contiguous run (64 lanes x 16 B, non-temporal), the next tile's loads are in
-// flight while the MFMAs consume the current one, and the MFMA operand reads come from LDS (rows
-// padded by 4 floats so the 16-row operand reads spread over the banks).
+// Both contractions stream M through LDS in tiles of 16 rows x 256·CPL columns: every global load
+// is one row's 1 KB contiguous run (64 lanes x 16 B, non-temporal) and a lane's CPL loads of a row
+// are adjacent, so a wave reads CPL KB of each row back to back (wide runs keep DRAM pages open:
+// 1-KB runs at a 16-KB row stride read at about half the rate of 4-KB runs).  The next tile's loads
+// are in flight while the MFMAs consume the current one, and the MFMA operand reads come from LDS
+// (rows padded by 4 floats so the 16-row operand reads spread over the banks).
 constexpr int kTileR = 16;
-constexpr int kTileC = 256;
-constexpr int kTileLd = kTileC + 4;
 constexpr int kPW = 4;                      // waves per workgroup (both kernels)
 constexpr int kPBlockT = kPW * kWave;
+#ifdef GRACE_TILE_CPL
+constexpr int kCPL = GRACE_TILE_CPL;        // columns per lane / 4 of the streamed tiles
+#else
+constexpr int kCPL = 1;
+#endif
+template <int CPL> struct Tile {
+  static constexpr int C = 256 * CPL;       // tile columns
+  static constexpr int LD = C + 4;          // padded LDS row
+};
 
-// prefetch tile (row0, col0) of M into registers: wave w loads rows w, w+4, w+8, w+12
-template <bool VEC>
+// prefetch tile (row0, col0) of M into registers: wave w loads rows w, w+4, w+8, w+12, each as CPL
+// consecutive 1-KB runs
+template <int CPL, bool VEC>
 __device__ __forceinline__ void tile_load(const float* __restrict__ M, int64_t n, int64_t m, int64_t rlo,
-                                          int64_t rhi, int64_t row0, int64_t col0, f32x4v (&pre)[4]) {
+                                          int64_t rhi, int64_t row0, int64_t col0, f32x4v (&pre)[4 * CPL]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t col = col0 + 4 * lane;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t row = row0 + w + 4 * j;
     const bool rv = row >= rlo && row < rhi && row < n;
-    if (VEC) {
-      const int64_t rc = rv ? row : rlo;
-      const int64_t cc = col < m ? col : m - 4;
-      const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + rc * m + cc));
-      const bool in = rv && col < m;
-      pre[j] = in ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
-    } else {
-      f32x4v v;
-      v.x = (rv && col + 0 < m) ? M[row * m + col + 0] : 0.f;
-      v.y = (rv && col + 1 < m) ? M[row * m + col + 1] : 0.f;
-      v.z = (rv && col + 2 < m) ? M[row * m + col + 2] : 0.f;
-      v.w = (rv && col + 3 < m) ? M[row * m + col + 3] : 0.f;
-      pre[j] = v;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int64_t col = col0 + 256 * c + 4 * lane;
+      if (VEC) {
+        const int64_t rc = rv ? row : rlo;
+        const int64_t cc = col < m ? col : m - 4;
+        const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + rc * m + cc));
+        const bool in = rv && col < m;
+        pre[j * CPL + c] = in ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
+      } else {
+        f32x4v v;
+        v.x = (rv && col + 0 < m) ? M[row * m + col + 0] : 0.f;
+        v.y = (rv && col + 1 < m) ? M[row * m + col + 1] : 0.f;
+        v.z = (rv && col + 2 < m) ? M[row * m + col + 2] : 0.f;
+        v.w = (rv && col + 3 < m) ? M[row * m + col + 3] : 0.f;
+        pre[j * CPL + c] = v;
+      }
     }
   }
 }
 
-__device__ __forceinline__ void tile_store(float (*tile)[kTileLd], const f32x4v (&pre)[4]) {
+template <int CPL>
+__device__ __forceinline__ void tile_store(float (*tile)[Tile<CPL>::LD], const f32x4v (&pre)[4 * CPL]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4v*>(&tile[w + 4 * j][4 * lane]) = pre[j];
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+      *reinterpret_cast<f32x4v*>(&tile[w + 4 * j][256 * c + 4 * lane]) = pre[j * CPL + c];
 }
 
 // prefetch `cnt` rows [row0, row0 + cnt) of a small row-major [rows x r] factor (q or P) as a
@@ -169,23 +213,38 @@ __device__ __forceinline__ void fac_store(float* fs, int r, int cnt, const float
     if (e < total) fs[e] = pre[j];
   }
 }
-constexpr int kQPer = kTileC * kMaxRank / kPBlockT;   // 16: q rows of one K tile
+// rank 4: thread t holds rows row0 + t + 256 c (c < CPL) of a [rows x 4] factor, one 16-B load each
+// (zero past `rhi`)
+template <int CPL>
+__device__ __forceinline__ void fac_load_r4(const float* __restrict__ F, int64_t row0, int64_t rhi,
+                                            f32x4v (&pre)[CPL]) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int64_t row = row0 + threadIdx.x + 256 * c;
+    const f32x4v v = *reinterpret_cast<const f32x4v*>(F + 4 * (row < rhi ? row : row0));
+    pre[c] = row < rhi ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+}
 constexpr int kPPer = kTileR * kMaxRank / kPBlockT;   // 1: P rows of one row tile
 
 // ------------------------------------------------------------------------------------------------
 // P[n x r] = M[n x m] q[m x r].  Grid = (K chunks, 16-row tiles).  Per tile wave w owns columns
-// [64w, 64w + 64): per 16-wide k-step lane l reads A = M[l&15][k + 4(l>>4) .. +3] and B = the
-// matching q rows from LDS and issues 4 MFMAs (MFMA s = k-slice {k + 4g + s}).  The only global
-// loads in the loop are the NEXT tile's (M and its q rows), so they overlap the MFMAs instead of
-// being serialised behind in-loop loads.  The 4 waves and the K chunks are reduced
-// deterministically (LDS, then the last workgroup of the row tile).
-template <bool VEC>
-__global__ __launch_bounds__(kPBlockT) void psgd_p_kernel(const float* __restrict__ M, int64_t n, int64_t m,
+// [64·CPL·w, 64·CPL·(w + 1)): per 16-wide k-step lane l reads A = M[l&15][k + 4(l>>4) .. +3] and
+// B = the matching q rows from LDS and issues 4 MFMAs (MFMA s = k-slice {k + 4g + s}).  The only
+// global loads in the loop are the NEXT tile's (M and its q rows), so they overlap the MFMAs
+// instead of being serialised behind in-loop loads.  The 4 waves and the K chunks are reduced
+// deterministically (LDS, then the last workgroup of the row tile).  R4: q staged as 16-B rows,
+// wide tiles; otherwise one 1-KB run per row and flat scalar q staging.
+template <bool VEC, bool R4>
+__global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_p_kernel(const float* __restrict__ M, int64_t n, int64_t m,
                                                          const float* __restrict__ q, int r,
                                                          float* __restrict__ P, float* __restrict__ part,
                                                          uint32_t* __restrict__ tickets) {
-  __shared__ float tile[kTileR][kTileLd];
-  __shared__ float qs[kTileC * kMaxRank];
+  constexpr int CPL = R4 ? kCPL : 1;
+  constexpr int TC = Tile<CPL>::C;
+  constexpr int QPER = TC * kMaxRank / kPBlockT;
+  __shared__ float tile[kTileR][Tile<CPL>::LD];
+  __shared__ float qs[TC * (R4 ? 4 : kMaxRank)];
   __shared__ float red[kPW][16][17];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ks = blockIdx.x, nks = gridDim.x;
@@ -193,30 +252,43 @@ __global__ __launch_bounds__(kPBlockT) void psgd_p_kernel(const float* __restric
   const int64_t i0 = rt * kTileR;
   const int g = lane >> 4;
   const int col = lane & 15;
-  const int64_t nkt = (m + kTileC - 1) / kTileC;
+  const int64_t nkt = (m + TC - 1) / TC;
   const int64_t per = (nkt + nks - 1) / nks;
   const int64_t kt0 = ks * per, kt1 = min(nkt, kt0 + per);
   f32x4v acc = {0.f, 0.f, 0.f, 0.f};
-  f32x4v pre[4];
-  float qpre[kQPer];
+  f32x4v pre[4 * CPL];
+  float qpre[R4 ? 1 : QPER];
+  f32x4v q4[CPL];
   if (kt0 < kt1) {
-    tile_load<VEC>(M, n, m, i0, i0 + kTileR, i0, kt0 * kTileC, pre);
-    fac_load(q, r, kt0 * kTileC, m, kTileC, qpre);
+    tile_load<CPL, VEC>(M, n, m, i0, i0 + kTileR, i0, kt0 * TC, pre);
+    if constexpr (R4) fac_load_r4<CPL>(q, kt0 * TC, m, q4);
+    else fac_load(q, r, kt0 * TC, m, TC, qpre);
   }
   for (int64_t kt = kt0; kt < kt1; ++kt) {
-    tile_store(tile, pre);
-    fac_store(qs, r, kTileC, qpre);
+    tile_store<CPL>(tile, pre);
+    if constexpr (R4) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) *reinterpret_cast<f32x4v*>(&qs[4 * (threadIdx.x + 256 * c)]) = q4[c];
+    } else {
+      fac_store(qs, r, TC, qpre);
+    }
     __syncthreads();
     if (kt + 1 < kt1) {
-      tile_load<VEC>(M, n, m, i0, i0 + kTileR, i0, (kt + 1) * kTileC, pre);
-      fac_load(q, r, (kt + 1) * kTileC, m, kTileC, qpre);
+      tile_load<CPL, VEC>(M, n, m, i0, i0 + kTileR, i0, (kt + 1) * TC, pre);
+      if constexpr (R4) fac_load_r4<CPL>(q, (kt + 1) * TC, m, q4);
+      else fac_load(q, r, (kt + 1) * TC, m, TC, qpre);
     }
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int kl = 64 * w + 16 * st + 4 * g;
+    for (int st = 0; st < 4 * CPL; ++st) {
+      const int kl = 64 * CPL * w + 16 * st + 4 * g;
       const f32x4v av = *reinterpret_cast<const f32x4v*>(&tile[lane & 15][kl]);
+      if constexpr (R4) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma4(av[s], col < r ? qs[(kl + s) * r + col] : 0.f, acc);
+        for (int s = 0; s < 4; ++s) acc = mfma4(av[s], col < 4 ? qs[(kl + s) * 4 + col] : 0.f, acc);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(av[s], col < r ? qs[(kl + s) * r + col] : 0.f, acc);
+      }
     }
     __syncthreads();
   }
@@ -233,83 +305,150 @@ __global__ __launch_bounds__(kPBlockT) void psgd_p_kernel(const float* __restric
     if (valid) P[(i0 + rr) * r + cc] = sum;
     return;
   }
+  if constexpr (R4) {
+    // rank 4: the tile's 16 x 4 partial is 16 rows of 16 B, written through (sc1) and summed as
+    // 16-B runs by the last K chunk to arrive (same per-entry order as the scalar path)
+    __syncthreads();
+    float* stg = &tile[0][0];
+    if (cc < 4) stg[rr * 4 + cc] = sum;
+    __syncthreads();
+    const int64_t rows = min((int64_t)kTileR, n - i0);
+    const int sb = (int)(n * 4 * sizeof(float));
+    if (threadIdx.x < rows) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(part + ((int64_t)ks * n + i0) * 4, (short)0,
+                                                        (int)(rows * 16), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4v*>(&stg[4 * threadIdx.x]), rs,
+                                             threadIdx.x * 16, 0, kSc1);
+    }
+    if (!last_arrival(tickets + rt, (uint32_t)nks)) return;
+    if (threadIdx.x < rows) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(part + i0 * 4, (short)0, sb * (nks - 1) + (int)(rows * 16),
+                                                        0x00020000);
+      *reinterpret_cast<f32x4v*>(P + (i0 + threadIdx.x) * 4) = sum_partials_v4(rs, sb, nks, threadIdx.x * 16);
+    }
+    return;
+  }
   if (valid) st_agent(part + ((int64_t)ks * n + i0 + rr) * r + cc, sum);
   if (!last_arrival(tickets + rt, (uint32_t)nks)) return;
   if (valid) P[(i0 + rr) * r + cc] = sum_partials(part + (i0 + rr) * r + cc, (int64_t)n * r, nks);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Q = M^T P.  Grid = (256-column groups, row slabs).  Per 16-row tile wave w owns columns
-// [64w, 64w + 64) of the group: per 4-row step lane l reads B = M[4st + (l>>4)][64w + 4(l&15) ..
-// +3] and A = P^T[c = l&15][row] from LDS and issues 4 MFMAs (tile s = columns 4jj + s).  As in
-// P, the loop's only global loads are the next tile's (M rows and their P rows).  The slabs are
-// reduced in two fixed-order levels (groups of kFan slabs, then the groups), each by the last
-// workgroup to arrive.
+// Q = M^T P.  Grid = (256·CPL-column groups, row slabs).  Per 16-row tile wave w owns columns
+// [64·CPL·w, 64·CPL·(w + 1)) of the group: per 4-row step lane l reads B = M[4st + (l>>4)][64·CPL·w
+// + 64c + 4(l&15) .. +3] and A = P^T[c = l&15][row] from LDS and issues 4 MFMAs per 64-column
+// block c (tile 4c + s = columns 64c + 4jj + s).  As in P, the loop's only global loads are the
+// next tile's (M rows and their P rows).  The slabs are reduced in two fixed-order levels (groups
+// of kFan slabs, then the groups), each by the last workgroup to arrive.
 template <bool VEC>
-__global__ __launch_bounds__(kPBlockT) void psgd_qt_kernel(const float* __restrict__ M, int64_t n, int64_t m,
+__global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_qt_kernel(const float* __restrict__ M, int64_t n, int64_t m,
                                                           const float* __restrict__ P, int r, int64_t slab,
                                                           float* __restrict__ Q, float* __restrict__ part,
                                                           uint32_t* __restrict__ tickets) {
-  __shared__ float tile[kTileR][kTileLd];
+  constexpr int CPL = kCPL;
+  constexpr int TC = Tile<CPL>::C;
+  __shared__ float tile[kTileR][Tile<CPL>::LD];
   __shared__ float ps[kTileR * kMaxRank];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t cg = blockIdx.x;
-  const int64_t j0 = cg * kTileC;
+  const int64_t j0 = cg * TC;
   const int64_t ilo = (int64_t)blockIdx.y * slab, ihi = min(n, ilo + slab);
   const int kk = lane >> 4, jj = lane & 15;
-  f32x4v acc[4];
+  f32x4v acc[4 * CPL];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) acc[s] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  f32x4v pre[4];
+  for (int s = 0; s < 4 * CPL; ++s) acc[s] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  f32x4v pre[4 * CPL];
   float ppre[kPPer];
   if (ilo < ihi) {
-    tile_load<VEC>(M, n, m, ilo, ihi, ilo, j0, pre);
+    tile_load<CPL, VEC>(M, n, m, ilo, ihi, ilo, j0, pre);
     fac_load(P, r, ilo, ihi, kTileR, ppre);
   }
   for (int64_t i = ilo; i < ihi; i += kTileR) {
-    tile_store(tile, pre);
+    tile_store<CPL>(tile, pre);
     fac_store(ps, r, kTileR, ppre);
     __syncthreads();
     if (i + kTileR < ihi) {
-      tile_load<VEC>(M, n, m, ilo, ihi, i + kTileR, j0, pre);
+      tile_load<CPL, VEC>(M, n, m, ilo, ihi, i + kTileR, j0, pre);
       fac_load(P, r, i + kTileR, ihi, kTileR, ppre);
     }
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int rl = 4 * st + kk;
       const float a = jj < r ? ps[rl * r + jj] : 0.f;
-      const f32x4v bv = *reinterpret_cast<const f32x4v*>(&tile[rl][64 * w + 4 * jj]);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[s] = mfma4(a, bv[s], acc[s]);
+      for (int c = 0; c < CPL; ++c) {
+        const f32x4v bv = *reinterpret_cast<const f32x4v*>(&tile[rl][64 * CPL * w + 64 * c + 4 * jj]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[4 * c + s] = mfma4(a, bv[s], acc[4 * c + s]);
+      }
     }
     __syncthreads();
   }
-  // tile s, lane l, reg q4: column j0 + 64w + 4 (l & 15) + s, rank row c = (l >> 4) * 4 + q4
-  const int nslab = gridDim.y;
+  // the slab's [TC columns x r] result goes through LDS (the tile is free after the loop's last
+  // barrier) so that it leaves as flat 16-B runs: tile 4c + s, lane l, reg q4 is column
+  // 64·CPL·w + 64c + 4 (l & 15) + s of the group, rank row (l >> 4) * 4 + q4
+  static_assert(TC * kMaxRank <= kTileR * Tile<CPL>::LD, "staging fits the tile");
+  float* stg = &tile[0][0];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int64_t j = j0 + 64 * w + 4 * (lane & 15) + s;
+  for (int c = 0; c < CPL; ++c)
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int c = (lane >> 4) * 4 + q4;
-      if (j < m && c < r) {
-        if (nslab == 1) Q[j * r + c] = acc[s][q4];
-        else st_agent(part + ((int64_t)blockIdx.y * m + j) * r + c, acc[s][q4]);
+    for (int s = 0; s < 4; ++s) {
+      const int jl = 64 * CPL * w + 64 * c + 4 * (lane & 15) + s;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int cr = (lane >> 4) * 4 + q4;
+        if (cr < r) stg[jl * r + cr] = acc[4 * c + s][q4];
       }
     }
+  __syncthreads();
+  const int nslab = gridDim.y;
+  const int64_t ncol = min((int64_t)TC, m - j0);
+  const int nent = (int)(ncol * r);
+  if (nslab == 1) {
+    for (int f = threadIdx.x; f < nent; f += kPBlockT) Q[j0 * r + f] = stg[f];
+    return;
   }
-  if (nslab == 1) return;
+  const int64_t sstride = (int64_t)m * r;
+  // 16-B write-through runs when every slab's run is 16-B aligned and short enough for 32-bit offsets
+  const bool v4 = (nent % 4) == 0 && (sstride % 4) == 0 && (((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(Q)) & 15u) == 0) &&
+                  sstride * (int64_t)sizeof(float) * kFan < (1ll << 31) &&
+                  sstride * (int64_t)sizeof(float) * ((nslab + kFan - 1) / kFan) < (1ll << 31);
+  float* mine = part + (int64_t)blockIdx.y * sstride + j0 * r;
+  if (v4) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT)
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4v*>(&stg[4 * f4]), rs, f4 * 16, 0, kSc1);
+  } else {
+    for (int f = threadIdx.x; f < nent; f += kPBlockT) st_agent(mine + f, stg[f]);
+  }
   // two-level deterministic reduction over the slabs: groups of kFan slabs, then the groups
   const int ngroups = (nslab + kFan - 1) / kFan;
   const int sg = blockIdx.y / kFan;
   const int in_group = min(kFan, nslab - sg * kFan);
   if (!last_arrival(tickets + cg * ngroups + sg, (uint32_t)in_group)) return;
   float* part2 = part + (int64_t)nslab * m * r;
+  if (v4) {
+    const float* src = part + ((int64_t)sg * kFan) * sstride + j0 * r;
+    const int sb = (int)(sstride * sizeof(float));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
+                                                      sb * (in_group - 1) + nent * (int)sizeof(float), 0x00020000);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(part2 + (int64_t)sg * sstride + j0 * r, (short)0,
+                                                      nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT) {
+      const f32x4v t = sum_partials_v4(rs, sb, in_group, f4 * 16);
+      if (ngroups == 1) *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = t;
+      else __builtin_amdgcn_raw_buffer_store_b128(t, rd, f4 * 16, 0, kSc1);
+    }
+    if (ngroups == 1) return;
+    if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
+    const auto r2 = __builtin_amdgcn_make_buffer_rsrc(part2 + j0 * r, (short)0,
+                                                      sb * (ngroups - 1) + nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT)
+      *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = sum_partials_v4(r2, sb, ngroups, f4 * 16);
+    return;
+  }
   // the group's entries are one contiguous run of (columns x r) floats per slab; each thread
   // sums up to 4 of them at once so all of their partial loads are in flight together
-  const int64_t ncol = min((int64_t)kTileC, m - j0);
-  const int nent = (int)(ncol * r);
-  const int64_t sstride = (int64_t)m * r;
   for (int f0 = 0; f0 < nent; f0 += 4 * kPBlockT) {
     float t[4];
     sum_partials4(part + ((int64_t)sg * kFan) * sstride + j0 * r, sstride, in_group, f0, nent, t);
@@ -570,6 +709,11 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth4_kernel(float* __restric
 // rows: each thread keeps Q[j .. j+3][0 .. r) in registers, P's rows for the band sit in LDS, and
 // the band is streamed with 16-B non-temporal stores (and loads of M for the residual).
 constexpr int kOuterRows = 16;
+#ifdef GRACE_OUTER_ROWS
+constexpr int kOuter4Rows = GRACE_OUTER_ROWS;
+#else
+constexpr int kOuter4Rows = 16;
+#endif
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void psgd_outer_kernel(const float* __restrict__ P, const float* __restrict__ Q,
@@ -623,6 +767,41 @@ __global__ __launch_bounds__(256) void psgd_outer_kernel(const float* __restrict
   }
 }
 
+// Rank 4, 16-B aligned, m % 4 == 0: Q's four rows per thread are four 16-B loads (a thread's 64 B
+// are contiguous across the wave), the band's P rows are workgroup-uniform 16-B loads; the same
+// f32 operation order as psgd_outer_kernel, so both give identical bits.
+template <int ROWS>
+__global__ __launch_bounds__(256) void psgd_outer4_kernel(const float* __restrict__ P, const float* __restrict__ Q,
+                                                         int64_t n, int64_t m, float* __restrict__ out,
+                                                         const float* __restrict__ M, float* __restrict__ res) {
+  const int64_t i0 = (int64_t)blockIdx.y * ROWS;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j >= m) return;
+  f32x4v qv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qv[s] = *reinterpret_cast<const f32x4v*>(Q + (j + s) * 4);
+  const int64_t rows = min((int64_t)ROWS, n - i0);
+#pragma unroll 4
+  for (int rr = 0; rr < rows; ++rr) {
+    const int64_t i = i0 + rr;
+    const f32x4v p = *reinterpret_cast<const f32x4v*>(P + i * 4);
+    f32x4v mv;
+    if (res) mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + i * m + j));
+    float o[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t = t + p[c] * qv[s][c];
+      o[s] = t;
+    }
+    if (out) __builtin_nontemporal_store(f32x4v{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4v*>(out + i * m + j));
+    if (res)
+      __builtin_nontemporal_store(f32x4v{mv.x - o[0], mv.y - o[1], mv.z - o[2], mv.w - o[3]},
+                                  reinterpret_cast<f32x4v*>(res + i * m + j));
+  }
+}
+
 // standard normal draws (Box-Muller on the counter-based generator), for q (powersgd.py:41)
 __global__ __launch_bounds__(256) void normal_kernel(float* __restrict__ x, int64_t n, uint64_t seed) {
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; 2 * p < n; p += (int64_t)gridDim.x * 256) {
@@ -655,37 +834,40 @@ static void launch_orth(float* A, int64_t n, int32_t r, uint64_t seed, hipStream
 
 extern "C" {
 
-static int p_ksplit(int64_t n, int64_t m) {
+static int p_ksplit(int64_t n, int64_t m, int64_t tc) {
   const int64_t tiles = (n + kTileR - 1) / kTileR;
   if (tiles > kTickets) return 1;
+  const int64_t nkt = (m + tc - 1) / tc;
 #ifdef GRACE_P_KS
-  return (int)min((int64_t)GRACE_P_KS, (m + kTileC - 1) / kTileC);
+  return (int)min((int64_t)GRACE_P_KS, nkt);
 #endif
-  const int64_t nkt = (m + kTileC - 1) / kTileC;
   int64_t ks = (2048 + tiles - 1) / tiles;                  // aim for >= 2048 workgroups
   if (ks > nkt) ks = nkt;
   if (ks > 64) ks = 64;
   return ks < 1 ? 1 : (int)ks;
 }
 
+#ifndef GRACE_QT_WG
+#define GRACE_QT_WG 1024
+#endif
 static int64_t qt_slab(int64_t n, int64_t m) {
-  const int64_t groups = (m + kTileC - 1) / kTileC;
-  if (groups * 64 > kTickets / 2) return n;
+  const int64_t groups = (m + Tile<kCPL>::C - 1) / Tile<kCPL>::C;
+  if (groups * 128 > kTickets / 2) return n;
 #ifdef GRACE_QT_SLAB
   return GRACE_QT_SLAB;
 #endif
-  const int64_t ns = (1024 + groups - 1) / groups;          // aim for >= 1024 workgroups
+  const int64_t ns = (GRACE_QT_WG + groups - 1) / groups;   // aim for >= GRACE_QT_WG workgroups
   int64_t slab = (n + ns - 1) / ns;
   slab = (slab + kTileR - 1) / kTileR * kTileR;
   if (slab < 2 * kTileR) slab = 2 * kTileR;                 // keep the prefetch pipeline busy
-  while ((n + slab - 1) / slab > 64) slab *= 2;             // <= 64 slabs: two levels of kFan
+  while ((n + slab - 1) / slab > 16 * kFan) slab *= 2;      // <= 16 groups of kFan slabs
   return slab;
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r) {
-  const size_t pp = sizeof(float) * (size_t)p_ksplit(n, m) * n * r;
+  const size_t pp = sizeof(float) * (size_t)p_ksplit(n, m, Tile<1>::C) * n * r;   // >= the R4 split
   const int64_t slab = qt_slab(n, m);
   const int64_t nslab = (n + slab - 1) / slab;
   const size_t qp = sizeof(float) * (size_t)(nslab + (nslab + kFan - 1) / kFan) * m * r;
@@ -697,11 +879,15 @@ grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const floa
   GRACE_REQUIRE(M && q && P && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
                 "grace_powersgd_p: bad arguments");
   const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
-  const dim3 grid((unsigned)p_ksplit(n, m), (unsigned)((n + kTileR - 1) / kTileR));
+  const bool r4 = r == 4 &&
+                  ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(ws)) & 15u) == 0 &&
+                  n * 16 * 64 < (1ll << 31);   // partial offsets: <= 64 K chunks of n 16-B rows
+  const dim3 grid((unsigned)p_ksplit(n, m, vec && r4 ? Tile<kCPL>::C : Tile<1>::C), (unsigned)((n + kTileR - 1) / kTileR));
   uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
-  if (vec) psgd_p_kernel<true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
-  else psgd_p_kernel<false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  if (vec && r4) psgd_p_kernel<true, true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  else if (vec) psgd_p_kernel<true, false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  else psgd_p_kernel<false, false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
   GRACE_CHECK_LAUNCH("grace_powersgd_p");
   return GRACE_OK;
 }
@@ -713,7 +899,7 @@ grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const flo
   const int64_t slab = qt_slab(n, m);
   const int64_t nslab = (n + slab - 1) / slab;
   const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
-  const dim3 grid((unsigned)((m + kTileC - 1) / kTileC), (unsigned)nslab);
+  const dim3 grid((unsigned)((m + Tile<kCPL>::C - 1) / Tile<kCPL>::C), (unsigned)nslab);
   uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
   if (vec) psgd_qt_kernel<true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, P, r, slab, Q, part, tickets);
@@ -743,6 +929,12 @@ grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, i
   const bool vec = (m % 4 == 0) &&
                    (((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(M) |
                       reinterpret_cast<uintptr_t>(residual)) & 15u) == 0);
+  if (vec && r == 4 && ((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(Q)) & 15u) == 0) {
+    const dim3 g4((unsigned)((m + 1023) / 1024), (unsigned)((n + kOuter4Rows - 1) / kOuter4Rows));
+    psgd_outer4_kernel<kOuter4Rows><<<g4, 256, 0, as_stream(stream)>>>(P, Q, n, m, out, M, residual);
+    GRACE_CHECK_LAUNCH("grace_powersgd_outer");
+    return GRACE_OK;
+  }
   const dim3 grid((unsigned)((m + 1023) / 1024), (unsigned)((n + kOuterRows - 1) / kOuterRows));
   if (vec) psgd_outer_kernel<true><<<grid, 256, 0, as_stream(stream)>>>(P, Q, n, m, r, out, M, residual);
   else psgd_outer_kernel<false><<<grid, 256, 0, as_stream(stream)>>>(P, Q, n, m, r, out, M, residual);
