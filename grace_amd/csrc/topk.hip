@@ -1165,12 +1165,16 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   const bool ok = n_sure <= k && (uint64_t)n_sure + n_cand >= k && n_cand <= (uint64_t)w.cap;
   {  // the bracket's sample histograms are free again: zero them for the next step.  Write-through
      // (agent scope): the parallel fallback below accumulates into this memory with device
-     // atomics in the same launch, which a dirty zero line left in some XCD's L2 would overwrite
-    constexpr int kZ2 = (kBracketBins + kCoarseBins) / 2;
-    for (int z = fi * BLOCK + t; z < kZ2; z += fcnt * BLOCK) {
-      uint64_t* q = z < kBracketBins / 2 ? reinterpret_cast<uint64_t*>(w.shist) + z
-                                         : reinterpret_cast<uint64_t*>(w.chist) + (z - kBracketBins / 2);
-      __hip_atomic_store(q, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+     // atomics in the same launch, which a dirty zero line left in some XCD's L2 would overwrite.
+     // 16-B sc1 buffer stores: one fabric write per 16 B
+    constexpr int kZ4 = (kBracketBins + kCoarseBins) / 4;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(w.shist, (short)0, kBracketBins * 4, 0x00020000);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(w.chist, (short)0, kCoarseBins * 4, 0x00020000);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v zero = {0.f, 0.f, 0.f, 0.f};
+    for (int z = fi * BLOCK + t; z < kZ4; z += fcnt * BLOCK) {
+      if (z < kBracketBins / 4) __builtin_amdgcn_raw_buffer_store_b128(zero, rs, z * 16, 0, 16);
+      else __builtin_amdgcn_raw_buffer_store_b128(zero, rc, (z - kBracketBins / 4) * 16, 0, 16);
     }
   }
   if (!ok && fcnt > 1 && fcnt <= kFinBlocks) {   // every finalize workgroup: the parallel fallback
