@@ -103,10 +103,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and world == 1:
         raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+    # rehearsal knobs for a one-GPU box (never used by the driver's runs): every rank on cuda:0,
+    # gloo instead of RCCL (RCCL needs one device per rank)
+    if os.environ.get("GRACE_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("GRACE_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
