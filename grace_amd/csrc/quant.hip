@@ -662,28 +662,18 @@ __device__ __forceinline__ TernPartial block_tern_reduce(double sum, double sq, 
 // per-segment scale slot, kept at the segment's first unit (empty segments have none)
 struct TernScale { float c, scalar; };
 
-struct TernWs {
-  TernPartial* part;   // [nunits]
-  uint32_t* tick;      // [nunits] arrival counters, at the segment's first unit; left zeroed
-  TernScale* scale;    // [nunits]
+// Per-unit workspace slot, an array of structs indexed by unit: a unit's counter sits at the same
+// address whatever nunits a call uses and no call's partials overlap another call's counters, so one
+// zero-initialised buffer serves calls of any shape (each segment's last unit leaves its counter
+// zeroed).  A struct-of-arrays layout sized by nunits let a smaller call's partials land on a larger
+// call's counters.
+struct TernSlot {
+  TernPartial part;    // the unit's partial (agent-scope stores)
+  TernScale scale;     // the segment's (c, scalar), at its first unit
+  uint32_t tick, pad;  // arrivals, at the segment's first unit
 };
-// The tick counters come first, so they stay at a fixed place whatever nunits a call uses (the
-// workspace is shared by calls of different shapes and only the ticks must be left zeroed).
-__host__ __device__ inline size_t tern_ws_bytes(int64_t nunits) {
-  const size_t a = ((sizeof(uint32_t) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
-  const size_t b = ((sizeof(TernPartial) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
-  return a + b + sizeof(TernScale) * (size_t)(nunits + 1);
-}
-inline TernWs tern_ws(void* ws, int64_t nunits) {
-  char* p = reinterpret_cast<char*>(ws);
-  TernWs w;
-  w.tick = reinterpret_cast<uint32_t*>(p);
-  p += ((sizeof(uint32_t) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
-  w.part = reinterpret_cast<TernPartial*>(p);
-  p += ((sizeof(TernPartial) * (size_t)(nunits + 1)) + 255) & ~(size_t)255;
-  w.scale = reinterpret_cast<TernScale*>(p);
-  return w;
-}
+static_assert(sizeof(TernSlot) == 40, "TernSlot layout");
+__host__ __device__ inline size_t tern_ws_bytes(int64_t nunits) { return sizeof(TernSlot) * (size_t)(nunits + 1); }
 
 // Stage 1: per-unit f64 partials; the LAST unit of a segment to arrive reduces the segment's
 // partials in a fixed order (the same block reduction whichever unit it is, so the scale is
@@ -693,7 +683,7 @@ inline TernWs tern_ws(void* ws, int64_t nunits) {
 __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __restrict__ x,
                                                             const int64_t* __restrict__ seg_off,
                                                             const int64_t* __restrict__ unit_off, int nseg,
-                                                            const float* __restrict__ clip_in, TernWs w,
+                                                            const float* __restrict__ clip_in, TernSlot* __restrict__ w,
                                                             float* __restrict__ scalars) {
   __shared__ SegTables tab;
   __shared__ uint32_t s_last;
@@ -713,14 +703,14 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
   const int64_t nq = (qs.a1 - qs.a0) >> 2;
 #pragma unroll 4
   for (int64_t j = t; j < nq; j += kQBlock) {
-    const f4v v = __builtin_nontemporal_load(xq + j);
+    const f4v v = xq[j];   // a plain load (allocates in the caches): the encoder re-reads x (A/B: -4 %)
     tern_acc(v.x, sum, sq, amax, nan);
     tern_acc(v.y, sum, sq, amax, nan);
     tern_acc(v.z, sum, sq, amax, nan);
     tern_acc(v.w, sum, sq, amax, nan);
   }
   const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
-  uint64_t* pw = reinterpret_cast<uint64_t*>(w.part + unit);
+  uint64_t* pw = reinterpret_cast<uint64_t*>(&w[unit].part);
   if (t == 0) {
     __hip_atomic_store(pw, (uint64_t)__double_as_longlong(p.sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(pw + 1, (uint64_t)__double_as_longlong(p.sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -728,7 +718,7 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
                        __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int64_t first = sv.sub[s], units = sv.sub[s + 1] - first;
-    s_last = atomicAdd(&w.tick[first], 1u) == (uint32_t)(units - 1);
+    s_last = atomicAdd(&w[first].tick, 1u) == (uint32_t)(units - 1);
   }
   __syncthreads();
   if (!s_last) return;
@@ -736,7 +726,7 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
   const int64_t first = sv.sub[s];
   sum = 0.0; sq = 0.0; amax = 0.f; nan = 0;
   for (int64_t j = first + t; j < sv.sub[s + 1]; j += kQBlock) {
-    const uint64_t* pj = reinterpret_cast<const uint64_t*>(w.part + j);
+    const uint64_t* pj = reinterpret_cast<const uint64_t*>(&w[j].part);
     sum += __longlong_as_double((long long)__hip_atomic_load(pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     sq += __longlong_as_double((long long)__hip_atomic_load(pj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const uint64_t mn = __hip_atomic_load(pj + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -756,9 +746,9 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
       c = (float)(2.5 * (double)(float)sqrt(var));
     }
     const float scalar = q.nan ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
-    w.scale[first] = TernScale{c, scalar};
+    w[first].scale = TernScale{c, scalar};
     scalars[s] = scalar;
-    w.tick[first] = 0u;   // left zeroed for the next call
+    w[first].tick = 0u;   // left zeroed for the next call
   }
 }
 
@@ -769,7 +759,7 @@ constexpr int kTernBlock = GRACE_TERN_BLOCK;   // encode workgroup (A/B: 256 bea
 
 __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
-    int nseg, const TernScale* __restrict__ scale, const float* __restrict__ u, uint64_t seed,
+    int nseg, const TernSlot* __restrict__ w, const float* __restrict__ u, uint64_t seed,
     int8_t* __restrict__ codes) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
@@ -788,7 +778,7 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const int64_t jc = j < nq ? j : 0;
     if (nq > 0) xv[k] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + qs.a0) + jc);
   }
-  const TernScale sc = scale[sv.sub[s]];   // published by the segment's last stats unit
+  const TernScale sc = w[sv.sub[s]].scale;   // published by the segment's last stats unit
   const float c = sc.c, scalar = sc.scalar;
 
   auto enc = [&](float xv, float ui) -> int8_t {
@@ -1178,11 +1168,11 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
                                        void* stream) {
   GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && nunits >= 1 && codes && scalars && ws,
                 "grace_terngrad_compress: bad arguments");
-  const TernWs w = tern_ws(ws, nunits);
+  TernSlot* const w = reinterpret_cast<TernSlot*>(ws);
   tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
                                                                        scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
-  tern_encode_kernel<<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w.scale,
+  tern_encode_kernel<<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w,
                                                                          u, seed, codes);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
   return GRACE_OK;

@@ -268,6 +268,24 @@ def test_qsgd_bucket_decoder_multi_rank_aggregate(world):
     assert same_bits(out, exp)
 
 
+def test_terngrad_workspace_many_units_alternating():
+    """A call with hundreds of units alternating with 3-unit calls on the same workspace: each
+    segment's arrival counter must not share memory with a smaller call's partials (the
+    struct-of-arrays layout sized by nunits put them there once a segment started past unit 64)."""
+    rng = np.random.default_rng(11)
+    sizes = [16384 * 2 + 7] * 120
+    flat = (rng.standard_normal(sum(sizes)) * 0.01).astype(np.float32)
+    u = rng.random(flat.size, dtype=np.float32)
+    for _ in range(2):
+        codes, scal = ops.terngrad_compress(_t(flat), sizes=sizes, u=_t(u))
+        off = 0
+        for i, s in enumerate(sizes):
+            c1, s1 = ops.terngrad_compress(_t(flat[off:off + s]), u=_t(u[off:off + s]))
+            assert same_bits(_np(codes[off:off + s]), _np(c1)), i
+            assert same_bits(_np(scal[i:i + 1]), _np(s1)), i
+            off += s
+
+
 def test_terngrad_workspace_reuse_across_shapes():
     """The TernGrad workspace is shared by calls of different unit counts: its arrival counters
     must stay zeroed whichever shape ran before (a regression the segmented test first caught).
