@@ -191,7 +191,9 @@ extern "C" {
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
   (void)k;
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  return sizeof(uint32_t) * (size_t)nchunks + 256 + 256;   // counts, then the ticket (zero between calls)
+  // the ticket first (left zeroed by every call, at a fixed place whatever n), then the counts: a
+  // ticket placed after the n-sized counts landed on a larger earlier call's counts
+  return 256 + sizeof(uint32_t) * (size_t)nchunks + 256;
 }
 
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is
@@ -204,9 +206,8 @@ grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t
                 "grace_sort_payload: bad arguments (n <= 2^28)");
   if (k == 0) return GRACE_OK;
   hipStream_t s = as_stream(stream);
-  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) +
-                                                 ((sizeof(uint32_t) * nchunks + 255) & ~(size_t)255));
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + 256);
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
   if (e != hipSuccess) { set_error("grace_sort_payload", e); return GRACE_ERR_HIP; }
   const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));

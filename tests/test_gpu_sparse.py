@@ -139,3 +139,20 @@ def test_sparse_aggregate_rank_ordered(world, n, k):
         assert same_bits(out, exp), (world, divisor)
         out2 = _np(G.sparse_aggregate_sorted(sorted_buf, k, world, n, divisor))
         assert same_bits(out2, exp), ("sorted", world, divisor)
+
+
+def test_sort_payload_workspace_reuse_across_sizes():
+    """grace_sort_payload's arrival ticket sits at a fixed place in the shared workspace: a small-n
+    call after a large-n call (whose chunk counts filled the workspace) must still group correctly."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    for n, k in ((1 << 24, 20000), (100000, 1000), (1 << 24, 20000), (50000, 700)):
+        idx = rng.choice(n, size=k, replace=False).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        buf = torch.cat([torch.from_numpy(vals), torch.from_numpy(idx.view(np.float32))]).to(dev)
+        out = ops.sort_payload(buf, k, n).cpu().numpy()
+        ov, oi = out[:k], out[k:].view(np.int32)
+        assert np.all(np.diff(oi // 8192) >= 0), (n, k)
+        order = np.argsort(idx)
+        o2 = np.argsort(oi)
+        assert np.array_equal(idx[order], oi[o2]) and np.array_equal(vals[order], ov[o2]), (n, k)
