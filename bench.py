@@ -366,8 +366,9 @@ def bench_powersgd(args, world, rank, dev):
     n = m = 4096
     r = 4
     comm = Allreduce(PowerSGDCompressor(rank=r, world_size=world), NoneMemory(), world)
-    grads = [torch.randn(n, m, device=dev) for _ in range(3)]
-    elapsed = timed(lambda i: comm.step(grads[i % 3], "w"), args.steps, args.warmup, world, dev)
+    nbuf = 5   # 5 x 64 MiB rotated: more than the 256 MB MALL holds, so no step reuses the last one's M
+    grads = [torch.randn(n, m, device=dev) for _ in range(nbuf)]
+    elapsed = timed(lambda i: comm.step(grads[i % nbuf], "w"), args.steps, args.warmup, world, dev)
     t = elapsed / args.steps
     flops = 3 * 2 * n * m * r
     line = base_line(args, world, elapsed, 4.0 * n * m,

@@ -130,7 +130,7 @@ __device__ __forceinline__ bool last_arrival(uint32_t* ticket, uint32_t expected
 
 // ------------------------------------------------------------------------------------------------
 // Both contractions stream M through LDS in tiles of 16 rows x 256·CPL columns: every global load
-// is one row's 1 KB contiguous run (64 lanes x 16 B, non-temporal) and a lane's CPL loads of a row
+// is one row's 1 KB contiguous run (64 lanes x 16 B) and a lane's CPL loads of a row
 // are adjacent, so a wave reads CPL KB of each row back to back (wide runs keep DRAM pages open:
 // 1-KB runs at a 16-KB row stride read at about half the rate of 4-KB runs).  The next tile's loads
 // are in flight while the MFMAs consume the current one, and the MFMA operand reads come from LDS
@@ -164,7 +164,9 @@ __device__ __forceinline__ void tile_load(const float* __restrict__ M, int64_t n
       if (VEC) {
         const int64_t rc = rv ? row : rlo;
         const int64_t cc = col < m ? col : m - 4;
-        const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(M + rc * m + cc));
+        // plain (cache-allocating) load: P's pass leaves part of M in the MALL for Qt's re-read
+        // (A/B with 5 rotated 64 MiB matrices: step 67.2 -> 65.9 us against non-temporal loads)
+        const f32x4v v = *reinterpret_cast<const f32x4v*>(M + rc * m + cc);
         const bool in = rv && col < m;
         pre[j * CPL + c] = in ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
       } else {
