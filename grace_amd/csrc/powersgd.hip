@@ -335,6 +335,87 @@ __global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_p_kernel(const float* __
   if (valid) P[(i0 + rr) * r + cc] = sum_partials(part + (i0 + rr) * r + cc, (int64_t)n * r, nks);
 }
 
+// The slabs' [TC columns x r] results (staged in LDS as stg[column * r + rank]) are reduced over
+// the slabs in two fixed-order levels (groups of kFan slabs, then the groups), each by the last
+// workgroup to arrive; the partials travel as 16-B write-through runs.  Grid = (column groups of TC,
+// slabs).
+template <int TC, int BLOCK = kPBlockT>
+__device__ __forceinline__ void qt_reduce_slabs(const float* stg, int64_t m, int r, int64_t j0, int64_t cg,
+                                                float* __restrict__ Q, float* __restrict__ part,
+                                                uint32_t* __restrict__ tickets) {
+  const int nslab = gridDim.y;
+  const int64_t ncol = min((int64_t)TC, m - j0);
+  const int nent = (int)(ncol * r);
+  if (nslab == 1) {
+    for (int f = threadIdx.x; f < nent; f += BLOCK) Q[j0 * r + f] = stg[f];
+    return;
+  }
+  const int64_t sstride = (int64_t)m * r;
+  // 16-B write-through runs when every slab's run is 16-B aligned and short enough for 32-bit offsets
+  const bool v4 = (nent % 4) == 0 && (sstride % 4) == 0 && (((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(Q)) & 15u) == 0) &&
+                  sstride * (int64_t)sizeof(float) * kFan < (1ll << 31) &&
+                  sstride * (int64_t)sizeof(float) * ((nslab + kFan - 1) / kFan) < (1ll << 31);
+  float* mine = part + (int64_t)blockIdx.y * sstride + j0 * r;
+  if (v4) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += BLOCK)
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4v*>(&stg[4 * f4]), rs, f4 * 16, 0, kSc1);
+  } else {
+    for (int f = threadIdx.x; f < nent; f += BLOCK) st_agent(mine + f, stg[f]);
+  }
+  // two-level deterministic reduction over the slabs: groups of kFan slabs, then the groups
+  const int ngroups = (nslab + kFan - 1) / kFan;
+  const int sg = blockIdx.y / kFan;
+  const int in_group = min(kFan, nslab - sg * kFan);
+  if (!last_arrival(tickets + cg * ngroups + sg, (uint32_t)in_group)) return;
+  float* part2 = part + (int64_t)nslab * m * r;
+  if (v4) {
+    const float* src = part + ((int64_t)sg * kFan) * sstride + j0 * r;
+    const int sb = (int)(sstride * sizeof(float));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
+                                                      sb * (in_group - 1) + nent * (int)sizeof(float), 0x00020000);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(part2 + (int64_t)sg * sstride + j0 * r, (short)0,
+                                                      nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += BLOCK) {
+      const f32x4v t = sum_partials_v4(rs, sb, in_group, f4 * 16);
+      if (ngroups == 1) *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = t;
+      else __builtin_amdgcn_raw_buffer_store_b128(t, rd, f4 * 16, 0, kSc1);
+    }
+    if (ngroups == 1) return;
+    if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
+    const auto r2 = __builtin_amdgcn_make_buffer_rsrc(part2 + j0 * r, (short)0,
+                                                      sb * (ngroups - 1) + nent * (int)sizeof(float), 0x00020000);
+    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += BLOCK)
+      *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = sum_partials_v4(r2, sb, ngroups, f4 * 16);
+    return;
+  }
+  // the group's entries are one contiguous run of (columns x r) floats per slab; each thread
+  // sums up to 4 of them at once so all of their partial loads are in flight together
+  for (int f0 = 0; f0 < nent; f0 += 4 * BLOCK) {
+    float t[4];
+    sum_partials4(part + ((int64_t)sg * kFan) * sstride + j0 * r, sstride, in_group, f0, nent, t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + threadIdx.x + i * BLOCK;
+      if (f < nent) {
+        if (ngroups == 1) Q[j0 * r + f] = t[i];
+        else st_agent(part2 + (int64_t)sg * sstride + j0 * r + f, t[i]);
+      }
+    }
+  }
+  if (ngroups == 1) return;
+  if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
+  for (int f0 = 0; f0 < nent; f0 += 4 * BLOCK) {
+    float t[4];
+    sum_partials4(part2 + j0 * r, sstride, ngroups, f0, nent, t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + threadIdx.x + i * BLOCK;
+      if (f < nent) Q[j0 * r + f] = t[i];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Q = M^T P.  Grid = (256·CPL-column groups, row slabs).  Per 16-row tile wave w owns columns
 // [64·CPL·w, 64·CPL·(w + 1)) of the group: per 4-row step lane l reads B = M[4st + (l>>4)][64·CPL·w
@@ -403,77 +484,77 @@ __global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_qt_kernel(const float* _
       }
     }
   __syncthreads();
-  const int nslab = gridDim.y;
-  const int64_t ncol = min((int64_t)TC, m - j0);
-  const int nent = (int)(ncol * r);
-  if (nslab == 1) {
-    for (int f = threadIdx.x; f < nent; f += kPBlockT) Q[j0 * r + f] = stg[f];
-    return;
-  }
-  const int64_t sstride = (int64_t)m * r;
-  // 16-B write-through runs when every slab's run is 16-B aligned and short enough for 32-bit offsets
-  const bool v4 = (nent % 4) == 0 && (sstride % 4) == 0 && (((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(Q)) & 15u) == 0) &&
-                  sstride * (int64_t)sizeof(float) * kFan < (1ll << 31) &&
-                  sstride * (int64_t)sizeof(float) * ((nslab + kFan - 1) / kFan) < (1ll << 31);
-  float* mine = part + (int64_t)blockIdx.y * sstride + j0 * r;
-  if (v4) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(mine, (short)0, nent * (int)sizeof(float), 0x00020000);
-    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT)
-      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const f32x4v*>(&stg[4 * f4]), rs, f4 * 16, 0, kSc1);
-  } else {
-    for (int f = threadIdx.x; f < nent; f += kPBlockT) st_agent(mine + f, stg[f]);
-  }
-  // two-level deterministic reduction over the slabs: groups of kFan slabs, then the groups
-  const int ngroups = (nslab + kFan - 1) / kFan;
-  const int sg = blockIdx.y / kFan;
-  const int in_group = min(kFan, nslab - sg * kFan);
-  if (!last_arrival(tickets + cg * ngroups + sg, (uint32_t)in_group)) return;
-  float* part2 = part + (int64_t)nslab * m * r;
-  if (v4) {
-    const float* src = part + ((int64_t)sg * kFan) * sstride + j0 * r;
-    const int sb = (int)(sstride * sizeof(float));
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
-                                                      sb * (in_group - 1) + nent * (int)sizeof(float), 0x00020000);
-    const auto rd = __builtin_amdgcn_make_buffer_rsrc(part2 + (int64_t)sg * sstride + j0 * r, (short)0,
-                                                      nent * (int)sizeof(float), 0x00020000);
-    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT) {
-      const f32x4v t = sum_partials_v4(rs, sb, in_group, f4 * 16);
-      if (ngroups == 1) *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = t;
-      else __builtin_amdgcn_raw_buffer_store_b128(t, rd, f4 * 16, 0, kSc1);
-    }
-    if (ngroups == 1) return;
-    if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
-    const auto r2 = __builtin_amdgcn_make_buffer_rsrc(part2 + j0 * r, (short)0,
-                                                      sb * (ngroups - 1) + nent * (int)sizeof(float), 0x00020000);
-    for (int f4 = threadIdx.x; f4 < nent / 4; f4 += kPBlockT)
-      *reinterpret_cast<f32x4v*>(Q + j0 * r + 4 * f4) = sum_partials_v4(r2, sb, ngroups, f4 * 16);
-    return;
-  }
-  // the group's entries are one contiguous run of (columns x r) floats per slab; each thread
-  // sums up to 4 of them at once so all of their partial loads are in flight together
-  for (int f0 = 0; f0 < nent; f0 += 4 * kPBlockT) {
-    float t[4];
-    sum_partials4(part + ((int64_t)sg * kFan) * sstride + j0 * r, sstride, in_group, f0, nent, t);
+  qt_reduce_slabs<TC>(stg, m, r, j0, cg, Q, part, tickets);
+}
+
+// Rank-4 Q = M^T P on the vector ALUs (4 FMAs per element of M: the contraction needs no matrix
+// cores).  A 1024-thread workgroup owns 1024 columns and a slab of rows: column wave cw = w & 3
+// holds the 256 columns [256cw, 256cw + 256) (one 16-B quad per lane per row, so the workgroup
+// reads 4 KB of each row) and row wave rw = w >> 2 a quarter of the slab.  Every lane issues kQ4D
+// rows' loads before any is used (no LDS, no barriers in the loop) and accumulates its 4 columns x
+// 4 ranks in registers, row by row in order; P's row is a wave-uniform 16-B load.  The 4 row waves
+// are summed in LDS in a fixed order, then the slabs as in psgd_qt_kernel.  The big workgroups
+// exist for that last step: the slab reduction was the kernel's critical path (streaming alone:
+// ~9 us; with 512 small workgroups' partials, 22 us), and 4x fewer slabs make it one round of
+// loads per level.
+constexpr int kQ4C = 1024;
+constexpr int kQ4D = 16;
+constexpr int kQ4Block = 1024;
+__global__ __launch_bounds__(kQ4Block) void psgd_qt4_kernel(const float* __restrict__ M, int64_t n, int64_t m,
+                                                           const float* __restrict__ P, int64_t slab,
+                                                           float* __restrict__ Q, float* __restrict__ part,
+                                                           uint32_t* __restrict__ tickets) {
+  __shared__ float stg[kQ4C * 4];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cw = w & 3, rw = w >> 2;
+  const int64_t cg = blockIdx.x, j0 = cg * kQ4C;
+  const int64_t jc = j0 + 256 * cw + 4 * lane;       // this lane's 4 columns (m % 4 == 0)
+  const float* mp = M + (jc < m ? jc : 0);
+  const int64_t slo = (int64_t)blockIdx.y * slab, shi = min(n, slo + slab);
+  const int64_t quarter = slab / 4;                   // slab is a multiple of 4 * kQ4D
+  const int64_t ilo = min(shi, slo + rw * quarter), ihi = min(shi, ilo + quarter);
+  float acc[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = f0 + threadIdx.x + i * kPBlockT;
-      if (f < nent) {
-        if (ngroups == 1) Q[j0 * r + f] = t[i];
-        else st_agent(part2 + (int64_t)sg * sstride + j0 * r + f, t[i]);
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[s][c] = 0.f;
+  for (int64_t i = ilo; i < ihi; i += kQ4D) {
+    f32x4v v[kQ4D];
+#pragma unroll
+    for (int d = 0; d < kQ4D; ++d) {
+      const int64_t row = i + d < ihi ? i + d : ilo;  // unconditional loads: a clamped row stands in
+      v[d] = *reinterpret_cast<const f32x4v*>(mp + row * m);
+    }
+#pragma unroll
+    for (int d = 0; d < kQ4D; ++d) {
+      if (i + d < ihi) {
+        const f32x4v pr = *reinterpret_cast<const f32x4v*>(P + (i + d) * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[s][c] = fmaf(v[d][s], pr[c], acc[s][c]);
       }
     }
   }
-  if (ngroups == 1) return;
-  if (!last_arrival(tickets + kTickets / 2 + cg, (uint32_t)ngroups)) return;
-  for (int f0 = 0; f0 < nent; f0 += 4 * kPBlockT) {
-    float t[4];
-    sum_partials4(part2 + j0 * r, sstride, ngroups, f0, nent, t);
+  // row waves 0, 1, 2, 3 in order: column jl = 256cw + 4 lane + s, rank c -> stg[jl * 4 + c]
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = f0 + threadIdx.x + i * kPBlockT;
-      if (f < nent) Q[j0 * r + f] = t[i];
+  for (int q = 0; q < 4; ++q) {
+    if (rw == q) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        f32x4v* dst = reinterpret_cast<f32x4v*>(&stg[(256 * cw + 4 * lane + s) * 4]);
+        const f32x4v mine = f32x4v{acc[s][0], acc[s][1], acc[s][2], acc[s][3]};
+        *dst = q == 0 ? mine : *dst + mine;
+      }
     }
+    __syncthreads();
   }
+#ifdef GRACE_QT4_NORED   // diagnostic A/B build only: no slab reduction (wrong Q)
+  if (blockIdx.y == 0) for (int f = threadIdx.x; f < kQ4C * 4 && j0 * 4 + f < m * 4; f += kQ4Block) Q[j0 * 4 + f] = stg[f];
+  return;
+#endif
+  qt_reduce_slabs<kQ4C, kQ4Block>(stg, m, 4, j0, cg, Q, part, tickets);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -867,12 +948,27 @@ static int64_t qt_slab(int64_t n, int64_t m) {
   return slab;
 }
 
+// psgd_qt4_kernel: slabs of 4 x kQ4D-multiples, aiming at >= 256 workgroups, <= 16 groups of kFan
+static bool qt4_ok(int64_t m) { return ((m + kQ4C - 1) / kQ4C) * 16 <= kTickets / 2; }
+static int64_t qt4_slab(int64_t n, int64_t m) {
+  const int64_t groups = (m + kQ4C - 1) / kQ4C;
+#ifndef GRACE_QT4_WG
+#define GRACE_QT4_WG 256
+#endif
+  const int64_t ns = (GRACE_QT4_WG + groups - 1) / groups;
+  int64_t slab = (n + ns - 1) / ns;
+  slab = (slab + 4 * kQ4D - 1) / (4 * kQ4D) * (4 * kQ4D);   // four row waves of whole batches
+  while ((n + slab - 1) / slab > 16 * kFan) slab *= 2;
+  return slab;
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r) {
   const size_t pp = sizeof(float) * (size_t)p_ksplit(n, m, Tile<1>::C) * n * r;   // >= the R4 split
-  const int64_t slab = qt_slab(n, m);
-  const int64_t nslab = (n + slab - 1) / slab;
+  // the larger of the two Qt kernels' slab partials (the rank-4 kernel needs 16-B aligned M and P)
+  int64_t nslab = (n + qt_slab(n, m) - 1) / qt_slab(n, m);
+  if (r == 4 && qt4_ok(m)) nslab = max(nslab, (n + qt4_slab(n, m) - 1) / qt4_slab(n, m));
   const size_t qp = sizeof(float) * (size_t)(nslab + (nslab + kFan - 1) / kFan) * m * r;
   return kTicketBytes + align256(pp > qp ? pp : qp);
 }
@@ -899,12 +995,21 @@ grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const flo
                                  void* ws, void* stream) {
   GRACE_REQUIRE(M && P && Q && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
                 "grace_powersgd_qt: bad arguments");
-  const int64_t slab = qt_slab(n, m);
-  const int64_t nslab = (n + slab - 1) / slab;
   const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
-  const dim3 grid((unsigned)((m + Tile<kCPL>::C - 1) / Tile<kCPL>::C), (unsigned)nslab);
   uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
+#ifndef GRACE_QT_MFMA
+  if (r == 4 && vec && qt4_ok(m) && ((reinterpret_cast<uintptr_t>(P) & 15u) == 0)) {
+    const int64_t slab = qt4_slab(n, m);
+    const dim3 grid((unsigned)((m + kQ4C - 1) / kQ4C), (unsigned)((n + slab - 1) / slab));
+    psgd_qt4_kernel<<<grid, kQ4Block, 0, as_stream(stream)>>>(M, n, m, P, slab, Q, part, tickets);
+    GRACE_CHECK_LAUNCH("grace_powersgd_qt");
+    return GRACE_OK;
+  }
+#endif
+  const int64_t slab = qt_slab(n, m);
+  const int64_t nslab = (n + slab - 1) / slab;
+  const dim3 grid((unsigned)((m + Tile<kCPL>::C - 1) / Tile<kCPL>::C), (unsigned)nslab);
   if (vec) psgd_qt_kernel<true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, P, r, slab, Q, part, tickets);
   else psgd_qt_kernel<false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, P, r, slab, Q, part, tickets);
   GRACE_CHECK_LAUNCH("grace_powersgd_qt");
