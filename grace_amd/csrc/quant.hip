@@ -17,14 +17,22 @@
 namespace grace {
 
 constexpr int kQBlock = 256;
+// Row kernels: buckets (chunks) per 16-lane row per iteration, and grid caps.  A/B on the ResNet-50
+// set (tools/exp_tern_ab.py, two boxes): 2 buckets per row beat 4 for every row kernel (fewer
+// registers, more rows in flight); the QSGD encoder is best at <= 4096 workgroups (a few
+// iterations per row: 38 -> 34 us), the decoders at <= 8192 (QSGD 24 -> 22 us, TernGrad 25 -> 21 us).
 #ifndef GRACE_QNB
-#define GRACE_QNB 4
+#define GRACE_QNB 2
 #endif
-constexpr int kQNB = GRACE_QNB;   // QSGD encode: buckets per half-wave per iteration
+constexpr int kQNB = GRACE_QNB;
 #ifndef GRACE_QGRID
 #define GRACE_QGRID 8192
 #endif
-constexpr int kQGridCap = GRACE_QGRID;
+constexpr int kQGridCap = GRACE_QGRID;      // decoders
+#ifndef GRACE_QENC_GRID
+#define GRACE_QENC_GRID 4096
+#endif
+constexpr int kQEncGridCap = GRACE_QENC_GRID;   // QSGD encoder
 constexpr int kSegLds = 512;     // offset tables up to this many segments are staged in LDS
 
 // segment containing flat element / bucket index `x`: largest s with off[s] <= x
@@ -1107,7 +1115,7 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
   const unsigned grid = stream_grid(nbuckets, kQNB * kQBlock / 32, kQGridCap);
   hipStream_t st = as_stream(stream);
   if (bucket_size == 128 && nseg <= kSegLds && nbuckets < (int64_t(1) << 24)) {   // n < 2^31
-    const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQGridCap);
+    const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
 #define GRACE_QENC128(CT, V)                                                                         \
   qsgd_encode128_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
                                                         (float)quantum_num, u, seed, norms_in,        \
