@@ -131,11 +131,16 @@ def load():
     return _lib
 
 
+_fns = {}
+
+
 def call(name, *args):
-    lib = load()
-    st = getattr(lib, name)(*args)
+    fn = _fns.get(name)
+    if fn is None:   # first call: resolve once (the per-call CDLL attribute lookup costs host time
+        fn = _fns[name] = getattr(load(), name)   # on launch-bound steps such as a 4 MiB sign step)
+    st = fn(*args)
     if st != 0:
-        msg = lib.grace_last_error()
+        msg = load().grace_last_error()
         raise GraceNativeError(f"{name} failed ({st}): {msg.decode() if msg else ''}")
     return st
 

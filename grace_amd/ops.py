@@ -135,10 +135,11 @@ def signum_encode(g, momentum_buf, has_prev, momentum):
 
 
 def sign_step_w1(x, want_codes=True):
-    x = dev_f32(x)
+    if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == F32 and x.is_contiguous()):
+        x = dev_f32(x)   # (the checks dev_f32 would make, without its reshape on the common path)
     codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device) if want_codes else None
     out = torch.empty_like(x)
-    _lib.call("grace_sign_step_w1", _p(x), _p(codes), _p(out), x.numel(), _stream())
+    _lib.call("grace_sign_step_w1", x.data_ptr(), _p(codes), out.data_ptr(), x.numel(), _stream())
     return codes, out
 
 
