@@ -15,7 +15,9 @@
  *   - all work is stream-ordered: nothing allocates, frees or synchronises, so the calls can be
  *     captured into a hipGraph;
  *   - scratch comes from a caller-provided workspace whose size is given by the matching
- *     *_workspace_bytes() query;
+ *     *_workspace_bytes() query; zero it once when it is allocated.  Every entry point leaves the
+ *     counters it uses zeroed, at offsets that do not depend on the call's sizes, so one workspace
+ *     (at least as large as each call's query) serves calls of any shape on its stream;
  *   - return value is a grace_status_t (0 = launched OK, negative = error; see grace_last_error()).
  *   - f32 arithmetic follows the reference's torch ops exactly (no FMA contraction) unless a
  *     function's comment states a tolerance.
