@@ -796,7 +796,7 @@ constexpr int kOuterRows = 16;
 #ifdef GRACE_OUTER_ROWS
 constexpr int kOuter4Rows = GRACE_OUTER_ROWS;
 #else
-constexpr int kOuter4Rows = 16;
+constexpr int kOuter4Rows = 4;   // A/B (tools/exp_psgd.py): 4-row bands 12.3 us, 2: 12.7, 8-32: 13.4
 #endif
 
 template <bool VEC>
