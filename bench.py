@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
     ap.add_argument("--cpu-baseline-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="at N > 1, skip the nested sharded (configs[4]) measurement of the default workload")
     return ap.parse_args()
 
 
@@ -119,6 +121,12 @@ def main():
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
     line = run(args, world, rank, dev)
+    if args.workload == "topk" and world > 1 and not args.no_sharded:
+        # BASELINE configs[4] (one 256 MiB bucket sharded over the ranks, top-k 0.1 %) rides in the
+        # same JSON line, so the driver's 1 -> 8 GPU record covers it next to the DP replicas
+        sh = bench_topk_sharded(args, world, rank, dev)
+        line["sharded"] = {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config",
+                                                    "roofline")}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -78,6 +78,12 @@ SIGNATURES = {
     "grace_sparse_aggregate_sorted": (ST, [P, P, I64, I64, I32, F32, P, I64, P, P]),
     "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
     "grace_qsgd_decompress": (ST, [P, P, I64, I64, I32, P, P, I32, I64, I32, I32, I32, I32, F32, P, P]),
+    "grace_qsgd_global_workspace_bytes": (SZ, []),
+    "grace_qsgd_global_compress": (ST, [P, I64, I32, P, U64, P, P, P, P, P]),
+    "grace_randomk_perm_indices": (ST, [U64, I64, I64, P, P]),
+    "grace_widen_i32": (ST, [P, I64, P, P]),
+    "grace_threshold_count_fixed": (ST, [P, I64, F32, P, P]),
+    "grace_threshold_write_i64": (ST, [P, I64, P, P, P, P]),
     "grace_terngrad_unit": (I32, []),
     "grace_terngrad_workspace_bytes": (SZ, [I64]),
     "grace_terngrad_compress": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),

@@ -562,10 +562,138 @@ __global__ __launch_bounds__(kQ4Block) void psgd_qt4_kernel(const float* __restr
 //   G = A^T A (f64 accumulation of the f32 entries, one read of A)
 //   R = chol(G)  (upper, positive diagonal)  -- the R of modified Gram-Schmidt
 //   A <- A R^-1  (row-wise forward substitution in f64, one write of A)
-// In exact arithmetic this is the reference's MGS result; with f64 Gram and solve the difference
-// from the f32 MGS is far below the parity tolerance for any A whose condition number the f32
-// MGS itself can handle.  A zero / dependent column gives R_cc = 0 and non-finite output, as MGS.
+// In exact arithmetic this is the reference's MGS result.  One Cholesky-QR pass loses
+// orthogonality like kappa(A)^2 * eps64, so the Cholesky pivots are checked: when the smallest
+// relative pivot d_c / G_cc falls below kOrthPivotMin (kappa(A) above ~1e4), or a pivot is not
+// finite, the workgroup switches to modified Gram-Schmidt with re-orthogonalisation in f64
+// (orth_mgs2, below).  That returns the exact QR factor of the f32 input to ~1e-7 for ANY
+// input, including near-rank-deficient ones (P = M q of a low-rank gradient), where the
+// reference's f32 MGS itself is only determined to ~kappa * eps32.  A column that is EXACTLY
+// dependent (residual exactly 0) comes out as zeros, where the reference's 0/0 gives NaN
+// (DESIGN.md section 2).
 constexpr int kOrthBlock = 1024;
+constexpr double kOrthPivotMin = 1e-8;
+
+// Robust path: MGS2 (every column projected twice against the finished ones, then normalised).
+// Register version: the rows a thread holds (row threadIdx.x + j * kOrthBlock) stay in f64
+// registers for the whole factorisation, so the result is the exact factor of the f32 input to
+// f64 accuracy; only the dot products meet in LDS.
+template <int R, int ROWS>
+__device__ void orth_mgs2_regs(double (&x)[ROWS][R], int r) {
+  constexpr int NW = kOrthBlock / kWave;
+  __shared__ double red[NW][R];
+  __shared__ double coef[R];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < R; ++c) {
+    if (c >= r) break;
+    for (int pass = 0; pass < 2 && c > 0; ++pass) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        if (j < c) {
+          double d = 0.0;
+#pragma unroll
+          for (int q = 0; q < ROWS; ++q) d = fma(x[q][j], x[q][c], d);
+          d = wave_sum(d);
+          if (lane == 0) red[w][j] = d;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < c) {
+        double t = 0.0;
+        for (int ww = 0; ww < NW; ++ww) t += red[ww][threadIdx.x];
+        coef[threadIdx.x] = t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < ROWS; ++q)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (j < c) x[q][c] -= coef[j] * x[q][j];
+      __syncthreads();   // red / coef are reused
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) s = fma(x[q][c], x[q][c], s);
+    s = wave_sum(s);
+    if (lane == 0) red[w][0] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int ww = 0; ww < NW; ++ww) t += red[ww][0];
+      coef[0] = t;
+    }
+    __syncthreads();
+    const double nrm = sqrt(coef[0]);
+    const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;   // exactly dependent column -> zeros
+#pragma unroll
+    for (int q = 0; q < ROWS; ++q) x[q][c] *= inv;
+    __syncthreads();
+  }
+}
+
+// Global version (A taller than the register chunk): f64 arithmetic on A in place in global
+// memory, f32 storage between sweeps (still well inside the reference's own f32 error).  Each thread owns rows threadIdx.x + j *
+// kOrthBlock for every sweep, so a thread only ever re-reads what it wrote itself; the column dot
+// products meet in LDS.  Rare (ill-conditioned inputs only), so simplicity over speed: 3 sweeps
+// and 3 block reductions per column.
+template <int R>
+__device__ void orth_mgs2(float* __restrict__ A, int64_t n, int r) {
+  constexpr int NW = kOrthBlock / kWave;
+  __shared__ double red[NW][R];
+  __shared__ double coef[R];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  auto block_sums = [&](double (&v)[R], int cnt) {   // coef[j] = sum over the block of v[j], j < cnt
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (j < cnt) {
+        const double t = wave_sum(v[j]);
+        if (lane == 0) red[w][j] = t;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < cnt) {
+      double t = 0.0;
+      for (int ww = 0; ww < NW; ++ww) t += red[ww][threadIdx.x];
+      coef[threadIdx.x] = t;
+    }
+    __syncthreads();
+  };
+  for (int c = 0; c < r; ++c) {
+    for (int pass = 0; pass < 2 && c > 0; ++pass) {
+      double d[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) d[j] = 0.0;
+      for (int64_t i = threadIdx.x; i < n; i += kOrthBlock) {
+        const double ac = (double)A[i * r + c];
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (j < c) d[j] += (double)A[i * r + j] * ac;
+      }
+      block_sums(d, c);
+      for (int64_t i = threadIdx.x; i < n; i += kOrthBlock) {
+        double ac = (double)A[i * r + c];
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (j < c) ac -= coef[j] * (double)A[i * r + j];
+        A[i * r + c] = (float)ac;
+      }
+      __syncthreads();   // coef is reused
+    }
+    double s2[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) s2[j] = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += kOrthBlock) {
+      const double v = (double)A[i * r + c];
+      s2[0] += v * v;
+    }
+    block_sums(s2, 1);
+    const double nrm = sqrt(coef[0]);
+    const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;   // exactly dependent column -> zeros
+    for (int64_t i = threadIdx.x; i < n; i += kOrthBlock) A[i * r + c] = (float)((double)A[i * r + c] * inv);
+    __syncthreads();
+  }
+}
 
 // standard normal draws: Box-Muller on the counter-based generator, one (cos, sin) pair per two
 // consecutive elements; element e is component e & 1 of pair e >> 1 (normal_kernel, the generic and
@@ -657,12 +785,15 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth_kernel(float* __restrict
     Gs[threadIdx.x] = t;
   }
   __syncthreads();
+  __shared__ int s_robust;
   if (threadIdx.x == 0) {
     // packed upper-triangle index of (c, c2), c <= c2
     auto gi = [](int c, int c2) { return c * R - c * (c - 1) / 2 + (c2 - c); };
+    int robust = 0;
     for (int c = 0; c < R; ++c) {
       double d = Gs[gi(c, c)];
       for (int k = 0; k < c; ++k) d -= Rs[k][c] * Rs[k][c];
+      if (c < r && !(d > kOrthPivotMin * Gs[gi(c, c)] && isfinite(d))) robust = 1;
       const double rcc = c < r ? sqrt(d) : 1.0;
       const double inv = 1.0 / rcc;
       Rs[c][c] = rcc;
@@ -673,8 +804,29 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth_kernel(float* __restrict
         Rs[c][c2] = c2 < r ? t * inv : 0.0;
       }
     }
+    s_robust = robust;
   }
   __syncthreads();
+  if (s_robust) {   // ill-conditioned: MGS2 (in f64 registers when A fits the register chunk)
+    if (single) {
+      double x[kOrthRows][R];
+#pragma unroll
+      for (int j = 0; j < kOrthRows; ++j)
+#pragma unroll
+        for (int c = 0; c < R; ++c) x[j][c] = (double)a[j][c];
+      orth_mgs2_regs<R, kOrthRows>(x, r);
+#pragma unroll
+      for (int j = 0; j < kOrthRows; ++j) {
+        const int64_t i = threadIdx.x + (int64_t)j * kOrthBlock;
+#pragma unroll
+        for (int c = 0; c < R; ++c)
+          if (i < n && c < r) A[i * r + c] = (float)x[j][c];
+      }
+    } else {
+      orth_mgs2<R>(A, n, r);
+    }
+    return;
+  }
   // A <- A R^-1, row-wise forward substitution
   for (int64_t base = 0; base < n; base += (int64_t)kOrthBlock * kOrthRows) {
     if (!single) load_chunk(base);   // single chunk: the rows are still in registers
@@ -755,11 +907,14 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth4_kernel(float* __restric
     Gs[threadIdx.x] = t;
   }
   __syncthreads();
+  __shared__ int s_robust;
   if (threadIdx.x == 0) {
     auto gi = [](int c, int c2) { return c * R - c * (c - 1) / 2 + (c2 - c); };
+    int robust = 0;
     for (int c = 0; c < R; ++c) {
       double d = Gs[gi(c, c)];
       for (int k = 0; k < c; ++k) d -= Rs[k][c] * Rs[k][c];
+      if (!(d > kOrthPivotMin * Gs[gi(c, c)] && isfinite(d))) robust = 1;
       const double rcc = sqrt(d);
       const double inv = 1.0 / rcc;
       Rs[c][c] = rcc;
@@ -770,8 +925,24 @@ __global__ __launch_bounds__(kOrthBlock) void psgd_orth4_kernel(float* __restric
         Rs[c][c2] = t * inv;
       }
     }
+    s_robust = robust;
   }
   __syncthreads();
+  if (s_robust) {   // ill-conditioned: MGS2 in f64 registers
+    double x[4][R];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int c = 0; c < R; ++c) x[j][c] = (double)a[j][c];
+    orth_mgs2_regs<R, 4>(x, R);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = threadIdx.x + (int64_t)j * kOrthBlock;
+      if (i < n)
+        *reinterpret_cast<f32x4v*>(A + i * R) = f32x4v{(float)x[j][0], (float)x[j][1], (float)x[j][2], (float)x[j][3]};
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t i = threadIdx.x + (int64_t)j * kOrthBlock;

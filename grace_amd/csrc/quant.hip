@@ -1097,6 +1097,78 @@ __global__ __launch_bounds__(kQBlock) void f16_to_f32_kernel(const __half* __res
     x[i] = __half2float(h[i]);
 }
 
+// ================================================================================================
+// QSGD, Horovod flavour (grace_dl/torch/compressor/qsgd.py:12-39): ONE norm over the whole tensor
+// (tensor.norm(), no buckets, no padding), then the same codeword rule as above.  Three launches:
+// f64 partial sums of x^2 per workgroup, one workgroup sums them in workgroup order and writes
+// norm = (float)sqrt(total) (or passes an injected norm through), and an elementwise encoder that
+// reads the norm once per thread.
+constexpr int kQgBlocks = 1024;
+
+__global__ __launch_bounds__(kQBlock) void qsgd_global_sumsq_kernel(const float* __restrict__ x, int64_t n,
+                                                                   double* __restrict__ part) {
+  double acc = 0.0;
+  const int64_t n4 = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) ? n >> 2 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kQBlock) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x) + i);
+    acc = fma((double)v.x, (double)v.x, acc);
+    acc = fma((double)v.y, (double)v.y, acc);
+    acc = fma((double)v.z, (double)v.z, acc);
+    acc = fma((double)v.w, (double)v.w, acc);
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock)
+    acc = fma((double)x[i], (double)x[i], acc);
+  __shared__ double sh[kQBlock / kWave];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kQBlock / kWave; ++w) t += sh[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kQBlock) void qsgd_global_norm_kernel(const double* __restrict__ part, int nparts,
+                                                                  const float* __restrict__ norm_in,
+                                                                  float* __restrict__ norm_out) {
+  __shared__ double sh[kQBlock];
+  double t = 0.0;
+  for (int b = threadIdx.x; b < nparts; b += kQBlock) t += part[b];
+  sh[threadIdx.x] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (norm_in) {
+      norm_out[0] = norm_in[0];
+    } else {
+      double tot = 0.0;
+      for (int b = 0; b < kQBlock; ++b) tot += sh[b];
+      norm_out[0] = (float)sqrt(tot);
+    }
+  }
+}
+
+template <typename CodeT>
+__global__ __launch_bounds__(kQBlock) void qsgd_global_encode_kernel(const float* __restrict__ x, int64_t n,
+                                                                    const float* __restrict__ norm_p, float qf,
+                                                                    const float* __restrict__ u, uint64_t seed,
+                                                                    CodeT* __restrict__ codes, int aligned) {
+  const float norm = norm_p[0];
+  const float scale = (1.0f / norm) * qf;   // q / norm as torch's __rdiv__: reciprocal(norm) * q
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    float v[4], uu[4];
+    load_quad(x, e, n, aligned != 0, v);
+    if (u) load_quad(u, e, n, aligned != 0, uu);
+    else uniform01x4(seed, (uint64_t)e, uu);
+    CodeT c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = qsgd_code<CodeT, 0>(v[j], scale * fabsf(v[j]), uu[j], norm);
+    store_codes4(codes, e, n, aligned != 0, c);
+  }
+}
+
 }  // namespace grace
 
 using namespace grace;
@@ -1141,6 +1213,36 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
                                                            reinterpret_cast<__half*>(codes));
   }
   GRACE_CHECK_LAUNCH("grace_qsgd_compress");
+  return GRACE_OK;
+}
+
+size_t grace_qsgd_global_workspace_bytes(void) { return sizeof(double) * kQgBlocks; }
+
+grace_status_t grace_qsgd_global_compress(const float* x, int64_t n, int32_t quantum_num, const float* u,
+                                          uint64_t seed, const float* norm_in, float* norm_out, void* codes,
+                                          void* ws, void* stream) {
+  GRACE_REQUIRE(x && n >= 1 && quantum_num >= 1 && norm_out && codes && ws,
+                "grace_qsgd_global_compress: bad arguments");
+  hipStream_t st = as_stream(stream);
+  double* part = reinterpret_cast<double*>(ws);
+  int nparts = 0;
+  if (!norm_in) {
+    nparts = (int)stream_grid((n + 3) / 4, kQBlock, kQgBlocks);
+    qsgd_global_sumsq_kernel<<<nparts, kQBlock, 0, st>>>(x, n, part);
+    GRACE_CHECK_LAUNCH("grace_qsgd_global_compress");
+  }
+  qsgd_global_norm_kernel<<<1, kQBlock, 0, st>>>(part, nparts, norm_in, norm_out);
+  GRACE_CHECK_LAUNCH("grace_qsgd_global_compress");
+  const unsigned grid = stream_grid((n + 3) / 4, kQBlock, 4096);
+  const int aligned = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(u)) & 15) == 0 &&
+                      (reinterpret_cast<uintptr_t>(codes) & (quantum_num < 128 ? 3 : 7)) == 0;
+  if (quantum_num < 128)
+    qsgd_global_encode_kernel<int8_t><<<grid, kQBlock, 0, st>>>(x, n, norm_out, (float)quantum_num, u, seed,
+                                                                reinterpret_cast<int8_t*>(codes), aligned);
+  else
+    qsgd_global_encode_kernel<__half><<<grid, kQBlock, 0, st>>>(x, n, norm_out, (float)quantum_num, u, seed,
+                                                                reinterpret_cast<__half*>(codes), aligned);
+  GRACE_CHECK_LAUNCH("grace_qsgd_global_compress");
   return GRACE_OK;
 }
 

@@ -33,6 +33,40 @@ __global__ __launch_bounds__(kSBlock) void gather_kernel(const float* __restrict
     vals[j] = x[idx[j]];
 }
 
+// Random-k without replacement (grace_dl/torch/compressor/randomk.py:10, randperm(numel)[:k]):
+// j -> pi(j) for j < k, pi a keyed pseudorandom permutation of [0, numel): a balanced 4-round
+// Feistel network on 2h bits (2^(2h) >= numel, so at most 4x numel) restricted to [0, numel) by
+// cycle walking, which keeps it a bijection.  Distinct j give distinct indices with no sort and no
+// shared state; every rank derives the same indices from the same seed.
+__device__ __forceinline__ uint64_t feistel(uint64_t x, int h, uint64_t key) {
+  const uint64_t mask = (1ull << h) - 1ull;
+  uint64_t l = x >> h, r = x & mask;
+#pragma unroll
+  for (int round = 0; round < 4; ++round) {
+    const uint64_t f = mix64(r ^ mix64(key + 0x9E3779B97F4A7C15ull * (uint64_t)(round + 1))) & mask;
+    const uint64_t t = l ^ f;
+    l = r;
+    r = t;
+  }
+  return (l << h) | r;
+}
+
+__global__ __launch_bounds__(kSBlock) void randperm_idx_kernel(uint64_t seed, int64_t numel, int64_t k, int h,
+                                                              int64_t* __restrict__ idx) {
+  const uint64_t key = mix64(seed ^ 0xD1B54A32D192ED03ull);
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock) {
+    uint64_t y = feistel((uint64_t)j, h, key);
+    while (y >= (uint64_t)numel) y = feistel(y, h, key);   // cycle walk: terminates (finite cycle through j)
+    idx[j] = (int64_t)y;
+  }
+}
+
+__global__ __launch_bounds__(kSBlock) void widen_i32_kernel(const int32_t* __restrict__ src, int64_t n,
+                                                           int64_t* __restrict__ dst) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < n; j += (int64_t)gridDim.x * kSBlock)
+    dst[j] = (int64_t)src[j];
+}
+
 // ------------------------------------------------------------------------------------------------
 // threshold
 struct ThrPart { float mx; uint32_t nan; uint32_t cnt; uint32_t pad; };
@@ -92,7 +126,7 @@ __global__ __launch_bounds__(kSBlock) void thr_stats_kernel(const float* __restr
 // exclusive offsets of the chunk counts; meta = {bound bits, total, recount flag}
 __global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ part, int64_t nchunks, float thr,
                                                         uint32_t* __restrict__ offs, uint32_t* __restrict__ meta,
-                                                        int final_pass) {
+                                                        int final_pass, int fixed_bound) {
   __shared__ uint32_t s_w[1024 / kWave + 1];
   __shared__ float s_mx;
   __shared__ uint32_t s_nan;
@@ -118,7 +152,7 @@ __global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ p
   __syncthreads();
   // torch.max propagates NaN; Python min(thr, NaN) returns thr (NaN < thr is False)
   const float gmax = s_nan ? __int_as_float(0x7FC00000) : s_mx;
-  const bool use_max = !s_nan && gmax < thr;
+  const bool use_max = !fixed_bound && !s_nan && gmax < thr;
   const float bound = use_max ? gmax : thr;
   // chunk offsets (valid when the counts were taken at `bound`)
   uint32_t run = 0;
@@ -138,10 +172,11 @@ __global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ p
 }
 
 // pass 3: ordered compaction of |x| >= bound
+template <typename IdxT>
 __global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restrict__ x, int64_t n,
                                                            const uint32_t* __restrict__ offs,
                                                            const uint32_t* __restrict__ meta,
-                                                           float* __restrict__ vals, int32_t* __restrict__ idx) {
+                                                           float* __restrict__ vals, IdxT* __restrict__ idx) {
   __shared__ uint32_t s_w[kSBlock / kWave + 1];
   const float bound = __uint_as_float(meta[0]);
   const int64_t base = (int64_t)blockIdx.x * kThrChunk;
@@ -154,7 +189,7 @@ __global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restr
     if (i < end) { v = x[i]; sel = fabsf(v) >= bound; }
     uint32_t tot;
     const uint32_t ex = blk_excl_scan<kSBlock>(sel ? 1u : 0u, s_w, &tot);
-    if (sel) { vals[run + ex] = v; idx[run + ex] = (int32_t)i; }
+    if (sel) { vals[run + ex] = v; idx[run + ex] = (IdxT)i; }
     run += tot;
   }
 }
@@ -198,7 +233,7 @@ grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void*
   hipStream_t s = as_stream(stream);
   thr_stats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, thr, part);
   GRACE_CHECK_LAUNCH("grace_threshold_count");
-  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 0);
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 0, 0);
   GRACE_CHECK_LAUNCH("grace_threshold_count");
   return GRACE_OK;
 }
@@ -214,7 +249,7 @@ grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, v
   hipStream_t s = as_stream(stream);
   thr_stats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, bound, part);
   GRACE_CHECK_LAUNCH("grace_threshold_recount");
-  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, bound, offs, meta, 1);
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, bound, offs, meta, 1, 0);
   GRACE_CHECK_LAUNCH("grace_threshold_recount");
   return GRACE_OK;
 }
@@ -226,8 +261,57 @@ grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, 
   const char* p = reinterpret_cast<const char*>(ws);
   const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
   const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
-  thr_write_kernel<<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
+  thr_write_kernel<int32_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
   GRACE_CHECK_LAUNCH("grace_threshold_write");
+  return GRACE_OK;
+}
+
+grace_status_t grace_randomk_perm_indices(uint64_t seed, int64_t numel, int64_t k, int64_t* idx, void* stream) {
+  GRACE_REQUIRE(idx && numel >= 1 && k >= 0 && k <= numel && numel < ((int64_t)1 << 62),
+                "grace_randomk_perm_indices: bad arguments (0 <= k <= numel)");
+  if (k == 0) return GRACE_OK;
+  int h = 1;
+  while ((int64_t)1 << (2 * h) < numel) ++h;
+  randperm_idx_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(seed, numel, k, h, idx);
+  GRACE_CHECK_LAUNCH("grace_randomk_perm_indices");
+  return GRACE_OK;
+}
+
+grace_status_t grace_widen_i32(const int32_t* src, int64_t n, int64_t* dst, void* stream) {
+  GRACE_REQUIRE(n >= 0 && (n == 0 || (src && dst)), "grace_widen_i32: bad arguments");
+  if (n == 0) return GRACE_OK;
+  widen_i32_kernel<<<stream_grid(n, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(src, n, dst);
+  GRACE_CHECK_LAUNCH("grace_widen_i32");
+  return GRACE_OK;
+}
+
+// Horovod-flavour threshold (grace_dl/torch/compressor/threshold.py:17): |x| > thr, no max rule.
+// The caller passes bound = the smallest f32 above thr (|x| > thr <=> |x| >= bound for every
+// f32, NaN never selected), or NaN when thr is +inf (nothing selected).
+grace_status_t grace_threshold_count_fixed(const float* x, int64_t n, float bound, void* ws, void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_count_fixed: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(p);
+  ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
+  uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  hipStream_t s = as_stream(stream);
+  thr_stats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, bound, part);
+  GRACE_CHECK_LAUNCH("grace_threshold_count_fixed");
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, bound, offs, meta, 1, 1);
+  GRACE_CHECK_LAUNCH("grace_threshold_count_fixed");
+  return GRACE_OK;
+}
+
+grace_status_t grace_threshold_write_i64(const float* x, int64_t n, const void* ws, float* vals, int64_t* idx,
+                                         void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_write_i64: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  const char* p = reinterpret_cast<const char*>(ws);
+  const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  thr_write_kernel<int64_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
+  GRACE_CHECK_LAUNCH("grace_threshold_write_i64");
   return GRACE_OK;
 }
 

@@ -119,7 +119,7 @@ struct TopkWs {
   int2* cand;
   int2* bnd;
   int64_t cap;
-  uint32_t* xcnt;      // sharded mode: [n_sure, n_cand] of this rank, exchanged after the main pass
+  uint32_t* xcnt;      // sharded mode: [n_sure, n_cand, shard length] of this rank, exchanged after the main pass
 };
 
 static inline int64_t topk_cap(int64_t n, int64_t k) {
@@ -832,6 +832,9 @@ __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
   const int64_t nchunks = (a.n + kMainChunk - 1) / kMainChunk;
+  // sharded mode: this rank's shard length rides in the exchanged counters, so every rank can
+  // check the shard sizes it planned with (grace_amd/dist/sharded.py)
+  if (w.xcnt && blockIdx.x == 0 && tid == 0) w.xcnt[2] = (uint32_t)a.n;
   __syncthreads();
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end

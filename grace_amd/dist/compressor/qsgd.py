@@ -24,15 +24,15 @@ class _QSGDBase(Compressor):
         self.rng = rng
         self._step = 0
 
-    def _uniforms(self, n, name):
+    def _uniforms(self, n, name, device):
         self._step += 1
         if self.rng == "torch_cpu":
-            return torch.empty(n).uniform_().to("cuda"), 0
+            return torch.empty(n).uniform_().to(device), 0
         return None, ops.step_seed("qsgd", ops.rank_of_process(), name, self._step)
 
     def compress(self, tensor, name):
         flat = ops.dev_f32(tensor)
-        u, seed = self._uniforms(flat.numel(), name)
+        u, seed = self._uniforms(flat.numel(), name, flat.device)
         codes, norms = ops.qsgd_compress(flat, self.quantum_num, self.bucket_size, variant=self.variant,
                                          u=u, seed=seed)
         return (codes, norms), tensor.size()

@@ -65,13 +65,21 @@ class TopKCompressor(Compressor):
             if not self.average:
                 return out.view(tensor.shape)
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
-        buf, _, _ = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None)
+        buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None)
         mem.residuals[name] = res
+        divisor = world if self.average else 1
+        if n > ops.SORT_PAYLOAD_MAX_N:
+            # beyond the index-sorted grouping's range (payload.hip): gather as-is and decode with
+            # the rank-ordered scatter-accumulate instead
+            gathered = torch.empty(world * 2 * k, dtype=torch.float32, device=g.device)
+            dist.all_gather_into_tensor(gathered, buf)
+            out = ops.sparse_aggregate(gathered, gathered[k:].view(torch.int32), 2 * k, [k] * world, world, n,
+                                       divisor)
+            return out.view(tensor.shape)
         # sort the local payload by index, exchange, then decode all W payloads in one pass over the
         # output (grace_amd/csrc/payload.hip) instead of W random scatters
         sbuf = ops.sort_payload(buf, k, n)
         gathered = torch.empty(world * 2 * k, dtype=torch.float32, device=g.device)
         dist.all_gather_into_tensor(gathered, sbuf)
-        divisor = world if self.average else 1
         out = ops.sparse_aggregate_sorted(gathered, k, world, n, divisor)
         return out.view(tensor.shape)

@@ -17,8 +17,12 @@ class PowerSGDMemory(Memory):
         if tensor.dim() == 1:
             return tensor
         if name in self.q_memory:
+            # tensor += residual, in place on any layout (a non-contiguous tensor is compensated
+            # through a contiguous copy that is written back)
             flat = ops.dev_f32(tensor)
-            ops.axpby(self.residuals[name], flat, 1.0, 1.0, out=flat)   # tensor += residual, in place
+            ops.axpby(self.residuals[name], flat, 1.0, 1.0, out=flat)
+            if not tensor.is_contiguous():
+                tensor.copy_(flat.view(tensor.shape))
         shape = tensor.size()
         n = shape[0]
         m = 1

@@ -110,8 +110,12 @@ class ShardedTopK:
         return 1, 0
 
     def _shard_sizes(self, name, m, device, world):
+        """Shard sizes of `name` on every rank.  Exchanged on a name's first step only; every later
+        step re-checks them for free through the shard length each rank's main pass writes into
+        its exchanged counters (step 3), so a resize on any rank is seen by ALL ranks in the same
+        step and they take the same branch (no rank-local collective)."""
         sizes = self._sizes.get(name)
-        if sizes is None or sizes[dist.get_rank(self.group) if world > 1 else 0] != m:
+        if sizes is None:
             if world > 1:
                 mine = torch.tensor([m], dtype=torch.int64, device=device)
                 allm = self.k_ops.empty(world, torch.int64, device)
@@ -158,7 +162,16 @@ class ShardedTopK:
         out_len = m if self.dense == "shard" else n
         out = K.fill_zero(K.empty(out_len, torch.float32, dev))
         self._wait_host()
-        ok, B, need, cap_b, cap_p = plan_boundary(host.numpy(), k, world, K.cand_cap(m, k))
+        rows = host.numpy().reshape(world, -1)
+        seen = [int(v) for v in rows[:, HIST_BINS + 2]]
+        if seen != list(sizes):
+            # some rank's shard changed size: this pass ran on stale offsets.  Every rank sees the
+            # same gathered lengths, so all of them redo the step with the new sizes; the residuals
+            # belong to the old partition and are dropped (the main pass left t in them).
+            self._sizes[name] = seen
+            self.residuals.pop(name, None)
+            return self.step(shard, name)
+        ok, B, need, cap_b, cap_p = plan_boundary(rows, k, world, K.cand_cap(m, k))
         self.last_fallback = not ok
         if not ok:
             return self._fallback(res, base, n, k, sizes, world, vals, idx, dev, out)
@@ -213,9 +226,14 @@ class ShardedTopK:
         K = self.k_ops
         if world > 1:
             if len(set(sizes)) != 1:
-                parts = [K.empty(sz, torch.float32, dev) for sz in sizes]
-                dist.all_gather(parts, res, group=self.group)
-                t_all = torch.cat(parts)
+                # unequal shards: RCCL / gloo gathers need one size, so pad every shard to the
+                # largest and cut the padding out of the gathered rows
+                mx = max(sizes)
+                send = K.empty(mx, torch.float32, dev)
+                send[:res.numel()].copy_(res)
+                recv = K.empty(world * mx, torch.float32, dev)
+                dist.all_gather_into_tensor(recv, send, group=self.group)
+                t_all = torch.cat([recv[r * mx:r * mx + sz] for r, sz in enumerate(sizes)])
             else:
                 t_all = K.empty(n, torch.float32, dev)
                 dist.all_gather_into_tensor(t_all, res, group=self.group)

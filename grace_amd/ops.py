@@ -232,10 +232,11 @@ def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out
     """Rank-ordered decode+aggregate of W sparse payloads laid out rank-major with `stride`.
     With `out` given it must already be zero-filled (e.g. by a fill that overlapped the gather)."""
     dev = vals_base.device
-    tags = _tags.get(str(dev))
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)   # per stream, like workspace()
+    tags = _tags.get(key)
     if tags is None or tags.numel() < n:
         tags = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        _tags[str(dev)] = tags
+        _tags[key] = tags
     prefilled = out is not None
     if out is None:
         out = torch.empty(n, dtype=F32, device=dev)
@@ -244,6 +245,9 @@ def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out
     _lib.call("grace_sparse_aggregate_into" if prefilled else "grace_sparse_aggregate", _p(vals_base), _p(idx_base),
               int(stride), ctypes.addressof(arr), int(world), float(divisor), _p(out), _p(tags), n, _stream())
     return out
+
+
+SORT_PAYLOAD_MAX_N = 1 << 28   # payload.hip kMaxGroupChunks * chunk: largest bucket sort_payload groups
 
 
 def sort_payload(buf, k, n):
@@ -337,6 +341,24 @@ def qsgd_decompress(codes, norms, quantum_num, bucket_size, n, sizes=None, varia
     return out
 
 
+def qsgd_global_compress(x, quantum_num, u=None, seed=0, norm_in=None):
+    """Horovod-flavour QSGD (grace_dl/torch/compressor/qsgd.py:12-31): one norm over the tensor.
+    Returns (codes int8 | fp16 [n], norm f32[1])."""
+    x = dev_f32(x)
+    n = x.numel()
+    codes = torch.empty(n, dtype=torch.int8 if quantum_num < 128 else torch.float16, device=x.device)
+    norm = torch.empty(1, dtype=F32, device=x.device)
+    ws = workspace("qsgd_global", _lib.query("grace_qsgd_global_workspace_bytes"), x.device)
+    _lib.call("grace_qsgd_global_compress", _p(x), n, int(quantum_num), _opt(u), int(seed) & (2 ** 64 - 1),
+              _opt(norm_in), _p(norm), _p(codes), _p(ws), _stream())
+    return codes, norm
+
+
+def qsgd_global_decompress(codes, norm, quantum_num, n, world=1, aggregate=False, divisor=1.0):
+    """(norm / q) * code (qsgd.py:33-38): the bucketed decoder with one bucket of n elements."""
+    return qsgd_decompress(codes, norm, quantum_num, n, n, world=world, aggregate=aggregate, divisor=divisor)
+
+
 # ----------------------------------------------------------------------------- TernGrad
 def terngrad_compress(x, sizes=None, clip=None, u=None, seed=0):
     x = dev_f32(x)
@@ -421,6 +443,20 @@ def randomk_indices(seed, numel, k, device):
     return idx
 
 
+def randomk_perm_indices(seed, numel, k, device):
+    """k distinct indices of [0, numel) (Horovod-flavour randperm(numel)[:k] semantics)."""
+    idx = torch.empty(k, dtype=torch.int64, device=device)
+    _lib.call("grace_randomk_perm_indices", int(seed) & (2 ** 64 - 1), int(numel), int(k), _p(idx), _stream())
+    return idx
+
+
+def widen_i32(idx32):
+    idx32 = require_dev(idx32, "indices")
+    out = torch.empty(idx32.numel(), dtype=torch.int64, device=idx32.device)
+    _lib.call("grace_widen_i32", _p(idx32), idx32.numel(), _p(out), _stream())
+    return out
+
+
 def gather(x, idx):
     x = dev_f32(x)
     idx = require_dev(idx)
@@ -450,6 +486,24 @@ def threshold_compress(x, thr):
     return vals, idx
 
 
+def threshold_compress_strict(x, thr):
+    """Horovod flavour (grace_dl/torch/compressor/threshold.py:17): (vals f32[m], idx int64[m]) of
+    |x| > f32(thr) in ascending order; one host sync sizes the outputs."""
+    import numpy as np
+    x = dev_f32(x)
+    n = x.numel()
+    t32 = np.float32(thr)
+    bound = np.float32("nan") if t32 == np.inf else np.nextafter(t32, np.float32(np.inf))
+    ws = workspace("threshold", _lib.query("grace_threshold_workspace_bytes", n), x.device)
+    _lib.call("grace_threshold_count_fixed", _p(x), n, float(bound), _p(ws), _stream())
+    m = int(ws[:12].view(torch.int32).cpu()[1])
+    vals = torch.empty(m, dtype=F32, device=x.device)
+    idx = torch.empty(m, dtype=torch.int64, device=x.device)
+    if m:
+        _lib.call("grace_threshold_write_i64", _p(x), n, _p(ws), _p(vals), _p(idx), _stream())
+    return vals, idx
+
+
 # ----------------------------------------------------------------------------- PowerSGD
 def powersgd_p(M2d, q):
     n, m = M2d.shape
@@ -470,7 +524,11 @@ def powersgd_qt(M2d, P):
 
 
 def orthogonalize_(A):
-    A = require_dev(A)
+    """In place: A must be a contiguous (row-major) device matrix, or the result would land on a copy."""
+    if not isinstance(A, torch.Tensor) or A.device.type != "cuda":
+        raise GraceDeviceError(f"grace_amd: orthogonalize_ needs a GPU tensor; got {getattr(A, 'device', type(A))}")
+    if not A.is_contiguous() or A.dtype != F32 or A.dim() != 2:
+        raise ValueError("grace_amd: orthogonalize_ works in place on a contiguous 2-D float32 matrix")
     _lib.call("grace_orthogonalize", _p(A), A.shape[0], A.shape[1], _stream())
     return A
 

@@ -6,9 +6,11 @@ The reference's ``grace_dl.torch`` drives Horovod's ``*_async`` collectives from
 same split runs on ``torch.distributed`` work handles (``async_op=True``), which on RCCL are
 stream-ordered: the collectives overlap the rest of the backward pass on the GPU.
 
-Compressors and memories are the ``grace_amd.dist`` ones (the reference's torch copies differ
-only in their Horovod imports), re-exported here so ``grace_dl.torch.compressor.*`` imports map
-one-to-one onto ``grace_amd.torch.compressor.*``.
+``grace_amd.torch.compressor`` / ``.memory`` mirror ``grace_dl.torch.compressor`` / ``.memory``
+module for module.  Six codecs compute something different from their dist copies (qsgd,
+threshold, randomk, topk, powersgd, onebit's decode; DgcMemory's constructor) and have their own
+implementations there; the others are the dist codecs, whose reference files differ only in the
+base-class import.
 """
 from abc import ABC, abstractmethod
 

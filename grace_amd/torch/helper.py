@@ -1,26 +1,88 @@
 """grace_from_params for the Horovod flavour (grace_dl/torch/helper.py:1-90): same keys and
-defaults; the world size comes from torch.distributed instead of ``hvd.size()``."""
+defaults, Horovod-flavour codecs; the world size comes from torch.distributed instead of
+``hvd.size()``."""
 import torch.distributed as dist
 
 
 def grace_from_params(params):
-    from grace_amd.dist.helper import grace_from_params as dist_grace
+    """grace_dl/torch/helper.py:1-90 with the Horovod-flavour classes of grace_amd.torch (same keys and
+    defaults; powersgd takes no arguments and its rank comes from the memory's compress_rank)."""
     world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-    p = dict(params)
-    p.setdefault('world_size', world_size)
-    comm = p.get('communicator', 'allreduce')
-    p['communicator'] = 'allreduce'          # build compressor + memory through the shared factory
-    built = dist_grace(p)
-    compressor, memory = built.compressor, built.memory
+    comp = params.get('compressor', 'none')
+    mem = params.get('memory', 'none')
+    comm = params.get('communicator', 'allreduce')
+    if comp == 'dgc':
+        from grace_amd.torch.compressor.dgc import DgcCompressor
+        compressor = DgcCompressor(params.get('compress_ratio', 0.3))
+    elif comp == 'efsignsgd':
+        from grace_amd.torch.compressor.efsignsgd import EFSignSGDCompressor
+        compressor = EFSignSGDCompressor(params.get('lr', 0.1))
+    elif comp == 'fp16':
+        from grace_amd.torch.compressor.fp16 import FP16Compressor
+        compressor = FP16Compressor()
+    elif comp == 'natural':
+        from grace_amd.torch.compressor.natural import NaturalCompressor
+        compressor = NaturalCompressor()
+    elif comp == 'none':
+        from grace_amd.torch.compressor.none import NoneCompressor
+        compressor = NoneCompressor()
+    elif comp == 'onebit':
+        from grace_amd.torch.compressor.onebit import OneBitCompressor
+        compressor = OneBitCompressor()
+    elif comp == 'powersgd':
+        from grace_amd.torch.compressor.powersgd import PowerSGDCompressor
+        compressor = PowerSGDCompressor()
+    elif comp == 'qsgd':
+        from grace_amd.torch.compressor.qsgd import QSGDCompressor
+        compressor = QSGDCompressor(params.get('quantum_num', 127))
+    elif comp == 'randomk':
+        from grace_amd.torch.compressor.randomk import RandomKCompressor
+        compressor = RandomKCompressor(params.get('compress_ratio', 0.3))
+    elif comp == 'signsgd':
+        from grace_amd.torch.compressor.signsgd import SignSGDCompressor
+        compressor = SignSGDCompressor()
+    elif comp == 'signum':
+        from grace_amd.torch.compressor.signum import SignumCompressor
+        compressor = SignumCompressor(params.get('momentum', 0.9))
+    elif comp == 'terngrad':
+        from grace_amd.torch.compressor.terngrad import TernGradCompressor
+        compressor = TernGradCompressor()
+    elif comp == 'threshold':
+        from grace_amd.torch.compressor.threshold import ThresholdCompressor
+        compressor = ThresholdCompressor(params.get('threshold', 0.01))
+    elif comp == 'topk':
+        from grace_amd.torch.compressor.topk import TopKCompressor
+        compressor = TopKCompressor(params.get('compress_ratio', 0.3))
+    else:
+        raise NotImplementedError(comp)
+
+    if mem == 'dgc':
+        from grace_amd.torch.memory.dgc import DgcMemory
+        memory = DgcMemory(params.get('momentum', 0.9), params.get('gradient_clipping', False))
+    elif mem == 'none':
+        from grace_amd.torch.memory.none import NoneMemory
+        memory = NoneMemory()
+    elif mem == 'powersgd':
+        from grace_amd.torch.memory.powersgd import PowerSGDMemory
+        memory = PowerSGDMemory(compressor.q_memory, params.get('compress_rank', 1))
+    elif mem == 'residual':
+        from grace_amd.torch.memory.residual import ResidualMemory
+        memory = ResidualMemory()
+    elif mem == 'efsignsgd':
+        from grace_amd.torch.memory.efsignsgd import EFSignSGDMemory
+        memory = EFSignSGDMemory(params.get('lr', 0.1))
+    else:
+        raise NotImplementedError(mem)
+
     if comm == 'allreduce':
         from grace_amd.torch.communicator.allreduce import Allreduce
-        return Allreduce(compressor, memory, p['world_size'])
+        return Allreduce(compressor, memory, world_size)
     if comm == 'allgather':
         from grace_amd.torch.communicator.allgather import Allgather
-        return Allgather(compressor, memory, p['world_size'])
+        return Allgather(compressor, memory, world_size)
     if comm == 'broadcast':
         from grace_amd.torch.communicator.broadcast import Broadcast
-        return Broadcast(compressor, memory, p['world_size'])
+        return Broadcast(compressor, memory, world_size)
     raise NotImplementedError(comm)
 
 

@@ -7,7 +7,7 @@
  *   - cnat_cuda.compress / decompress   grace_dl/dist/compressor/cnat_cuda/cnat.cpp:25-29
  *   - rdxtopk.topk                      grace_dl/dist/compressor/radixtopk_cuda/rdxtopk.cpp:11-18
  *   - the torch ops inside Compressor.compress/decompress and Memory.compensate/update
- *     (grace_dl/dist/compressor/*.py, grace_dl/dist/memory/*.py).
+ *     (the grace_dl/dist/compressor and grace_dl/dist/memory modules).
  *
  * Rules for every entry point:
  *   - plain pointers to DEVICE memory allocated by the caller, element counts, and a hipStream_t
@@ -165,6 +165,14 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
                                      const int64_t* bkt_off, int32_t nseg, int64_t n, int32_t quantum_num,
                                      int32_t bucket_size, int32_t variant, int32_t aggregate, float divisor,
                                      float* out, void* stream);
+/* QSGD, Horovod flavour (grace_dl/torch/compressor/qsgd.py:12-31): ONE norm over the whole tensor
+ * (tensor.norm(); no buckets), same codeword rule.  norm_out[1] f32 (f64 accumulation), norm_in
+ * (optional) injects it; ws = grace_qsgd_global_workspace_bytes().  Decode with
+ * grace_qsgd_decompress, one segment of one bucket of n elements (qsgd.py:33-38: norm / q * code). */
+size_t grace_qsgd_global_workspace_bytes(void);
+grace_status_t grace_qsgd_global_compress(const float* x, int64_t n, int32_t quantum_num, const float* u,
+                                          uint64_t seed, const float* norm_in, float* norm_out, void* codes,
+                                          void* ws, void* stream);
 /* TernGrad (terngrad.py:7-30).  unit_off[nseg + 1] (device) = per-segment offsets of
  * grace_terngrad_unit()-element work units; ws = grace_terngrad_workspace_bytes(nunits).
  * clip_in[nseg] (optional) injects the clamp bound c = f32(2.5 * std). */
@@ -197,6 +205,13 @@ grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n,
  * device generator keyed by the reference's seed sum(bytes(name)) + step: identical on every
  * rank.  (Bit-parity with torch's CPU generator: draw on the host and pass the indices.) */
 grace_status_t grace_randomk_indices(uint64_t seed, int64_t numel, int64_t k, int64_t* idx, void* stream);
+/* Random-k, Horovod flavour (grace_dl/torch/compressor/randomk.py:10: randperm(numel)[:k], WITHOUT
+ * replacement): idx[j] = pi(j), pi a keyed pseudorandom permutation of [0, numel) (Feistel network
+ * + cycle walking), so the k indices are distinct; identical on every rank for the same seed. */
+grace_status_t grace_randomk_perm_indices(uint64_t seed, int64_t numel, int64_t k, int64_t* idx, void* stream);
+/* dst[j] = (int64)src[j]: int64 index payloads of the Horovod-flavour top-k
+ * (grace_dl/torch/compressor/topk.py:11 keeps torch.topk's int64 indices) */
+grace_status_t grace_widen_i32(const int32_t* src, int64_t n, int64_t* dst, void* stream);
 /* vals[j] = x[idx[j]]  (randomk.py:12 tensor[indices]) */
 grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float* vals, void* stream);
 /* Threshold (threshold.py:16-19): idx = where(|x| >= min(thr, max(x))) in ascending order.
@@ -207,6 +222,11 @@ grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void*
 grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, void* ws, void* stream);
 grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, float* vals, int32_t* idx,
                                      void* stream);
+/* Horovod flavour (grace_dl/torch/compressor/threshold.py:17): where(|x| > thr), int64 indices.
+ * bound = the smallest f32 above f32(thr) (|x| > thr <=> |x| >= bound), NaN for thr = +inf. */
+grace_status_t grace_threshold_count_fixed(const float* x, int64_t n, float bound, void* ws, void* stream);
+grace_status_t grace_threshold_write_i64(const float* x, int64_t n, const void* ws, float* vals, int64_t* idx,
+                                         void* stream);
 
 /* ---------------------------------------------------------------------------------- PowerSGD */
 /* PowerSGD (powersgd.py:30-65) on M[n x m] row-major, rank r <= 16, f32 MFMA contractions.

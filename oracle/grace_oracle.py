@@ -299,6 +299,40 @@ def qsgd_cuda_compress(x, u, quantum_num, bucket_size, norms=None):
     return codes, norms
 
 
+# ----------------------------------------------------------------------------- Horovod flavour
+def qsgd_global_compress(x, u, quantum_num, norm=None):
+    """grace_dl/torch/compressor/qsgd.py:12-31: ONE norm ``tensor.norm()`` over the whole tensor, then
+    the dist codeword rule.  Returns (codes, norm f32[1])."""
+    xf = _f32(x).ravel()
+    if norm is None:
+        norm = np.array([torch.from_numpy(xf.copy()).norm().item()], dtype=F32)
+    norm = _f32(norm).reshape(1)
+    codes, _ = qsgd_compress(xf, u, quantum_num, max(xf.size, 1), norms=norm)
+    return codes, norm
+
+
+def qsgd_global_decode(codes, norm, quantum_num, numel):
+    """norm / q * code (grace_dl/torch/compressor/qsgd.py:33-38)."""
+    return qsgd_decode(codes, _f32(norm).reshape(1), quantum_num, max(numel, 1), numel)
+
+
+def threshold_select_strict(x, thr):
+    """grace_dl/torch/compressor/threshold.py:17: where(|x| > thr) with thr rounded to f32 (torch
+    compares a float32 tensor with a Python scalar in float32); int64 indices."""
+    xf = _f32(x).ravel()
+    with np.errstate(invalid="ignore"):
+        idx = np.nonzero(np.abs(xf) > F32(thr))[0]
+    return xf[idx].copy(), idx.astype(np.int64)
+
+
+def randomk_perm_indices(name, step, numel, ratio):
+    """grace_dl/torch/compressor/randomk.py:6-29: manual_seed(sum(bytes(name)) + step), then
+    randperm(numel)[:k] (no replacement)."""
+    h = sum(bytes(name, encoding="utf8"), step)
+    torch.manual_seed(h)
+    return torch.randperm(numel)[:ratio_k(numel, ratio)].numpy(), h
+
+
 # ----------------------------------------------------------------------------- natural
 def natural_compress(x, rnd_int):
     """cupy NaturalCompressor restated bit-for-bit (grace_dl/dist/compressor/natural.py:12-29),

@@ -329,6 +329,29 @@ def gen_powersgd():
         b = a.clone()
         orthogonalize(b)
         st.add(f"orth_{n}x{r}", {"codec": "orthogonalize"}, a=a, out=b)
+    # ill-conditioned inputs: A = U diag(s) V^T with condition number kappa; two nearly collinear
+    # columns; P = M q of a rank-2 M at r = 4 (what real low-rank gradients hand the orthogonaliser)
+    for n, r, kappa in ((4096, 4, 1e4), (4096, 4, 1e7), (500, 3, 1e4)):
+        gen = torch.Generator().manual_seed(1600 + int(np.log10(kappa)) + r)
+        u, _ = torch.linalg.qr(torch.randn(n, r, generator=gen, dtype=torch.float64))
+        v, _ = torch.linalg.qr(torch.randn(r, r, generator=gen, dtype=torch.float64))
+        s = torch.logspace(0, -np.log10(kappa), r, dtype=torch.float64)
+        a = (u * s) @ v.t()
+        a = a.float()
+        b = a.clone()
+        orthogonalize(b)
+        st.add(f"orth_ill_{n}x{r}_k{kappa:g}", {"codec": "orthogonalize", "kappa": kappa}, a=a, out=b)
+    a = g_randn((4096, 4), 1700)
+    a[:, 2] = a[:, 1] + 1e-6 * g_randn(4096, 1701)
+    b = a.clone()
+    orthogonalize(b)
+    st.add("orth_collinear_4096x4", {"codec": "orthogonalize", "kappa": 0}, a=a, out=b)
+    m2 = g_randn((4096, 2), 1702) @ g_randn((2, 1024), 1703)     # rank-2 gradient
+    q = g_randn((1024, 4), 1704)
+    p = torch.mm(m2, q)
+    b = p.clone()
+    orthogonalize(b)
+    st.add("orth_rank2_4096x4", {"codec": "orthogonalize", "kappa": -1}, a=p, out=b)
     # use_memory=False path with seeded normal_ draw, plus PowerSGDMemory for two steps
     comp = PowerSGDCompressor(rank=2, use_memory=False, world_size=1)
     mem = PowerSGDMemory(comp.q_memory, compress_rank=2)
@@ -455,6 +478,79 @@ def gen_dgc():
     st.save()
 
 
+def gen_torchflav():
+    """The Horovod-flavour codecs whose semantics differ from grace_dl.dist (grace_dl/torch/
+    compressor/{qsgd,threshold,randomk,topk,terngrad}.py).  These modules import no Horovod, so they
+    run here on CPU; PowerSGD / DgcMemory / the communicators need horovod and are not pinned."""
+    from grace_dl.torch.compressor.qsgd import QSGDCompressor
+    from grace_dl.torch.compressor.threshold import ThresholdCompressor
+    from grace_dl.torch.compressor.randomk import RandomKCompressor
+    from grace_dl.torch.compressor.topk import TopKCompressor
+    from grace_dl.torch.compressor.terngrad import TernGradCompressor
+
+    st = Store("torchflav")
+    # QSGD: ONE norm over the whole tensor (qsgd.py:12-31), no buckets
+    for q in (127, 255):
+        comp = QSGDCompressor(q)
+        inputs = [(f"n{n}", g_randn(n, 6000 + n, 0.01)) for n in (1, 129, 4099, 16411, 100003)]
+        inputs += [("s64x33", g_randn((64, 33), 61, 0.01)), ("zeros", torch.zeros(300)),
+                   ("outlier", torch.cat([g_randn(5000, 62, 0.01), torch.tensor([3.0, -4.0])]))]
+        for case, x in inputs:
+            seed = 7000 + x.numel() + q
+            torch.manual_seed(seed)
+            (codes, norm), shape = comp.compress(x, "w")
+            torch.manual_seed(seed)
+            u = torch.empty(x.numel()).uniform_()
+            dec = comp.decompress((codes, norm), shape)
+            st.add(f"qsgd_q{q}_{case}", {"codec": "qsgd", "quantum_num": q, "seed": seed, "shape": list(x.shape)},
+                   x=x, u=u, codes=codes, norm=norm.reshape(1), dec=dec)
+    # threshold: strict |x| > thr, int64 indices, ctx (shape, numel) (threshold.py:12-27)
+    inputs = [(f"n{n}", g_randn(n, 6100 + n)) for n in (1, 129, 4099, 16411)]
+    inputs += [("ties", tied_vec(4099, 63)), ("special", special_vec()), ("s64x33", g_randn((64, 33), 64))]
+    for case, x in inputs:
+        for thr in (0.01, 0.5, 1.5, 100.0):
+            comp = ThresholdCompressor(thr)
+            (vals, idx), ctx = comp.compress(x, "w")
+            dec = comp.decompress([vals, idx], ctx)
+            st.add(f"threshold_{case}_t{thr}", {"codec": "threshold", "threshold": thr, "shape": list(x.shape)},
+                   x=x, vals=vals, idx=idx, dec=dec)
+    # random-k: randperm(numel)[:k] without replacement, seeded sum(bytes(name)) + step (randomk.py:6-34)
+    for ratio in (0.01, 0.3):
+        comp = RandomKCompressor(ratio)
+        for name, n in (("layer1.weight", 4099), ("fc.bias", 129), ("conv.w", 100003)):
+            for s in range(2):
+                x = g_randn(n, 6200 + s)
+                h = sum(bytes(name, encoding="utf8"), comp.global_step)
+                (vals,), ctx = comp.compress(x, name)
+                dec = comp.decompress([vals], ctx)
+                st.add(f"randomk_{name}_r{ratio}_s{s}",
+                       {"codec": "randomk", "ratio": ratio, "name": name, "seed": int(h), "n": n},
+                       x=x, vals=vals, idx=ctx[0], dec=dec)
+    # top-k: int64 indices, ctx (numel, shape) (topk.py:6-36)
+    inputs = [(f"n{n}", g_randn(n, 6300 + n)) for n in (1, 129, 4099, 16411)]
+    inputs += [("s16x3x3x3", g_randn((16, 3, 3, 3), 65)), ("zeros", torch.zeros(1000))]
+    for case, x in inputs:
+        for ratio in (0.01, 0.3):
+            comp = TopKCompressor(ratio)
+            (vals, idx), ctx = comp.compress(x, "w")
+            dec = comp.decompress([vals, idx], ctx)
+            st.add(f"topk_{case}_r{ratio}", {"codec": "topk", "ratio": ratio, "shape": list(x.shape)},
+                   x=x, vals=vals, idx=idx, dec=dec)
+    # TernGrad: rnd = uniform_(0, scalar) instead of uniform_(0, 1) * scalar (terngrad.py:19)
+    tg = TernGradCompressor()
+    for case, x in [(f"n{n}", g_randn(n, 6400 + n, 0.01)) for n in (1, 129, 4099, 16411)] + \
+                   [("outlier", torch.cat([g_randn(4000, 66, 0.01), torch.tensor([5.0, -7.0])]))]:
+        seed = 8000 + x.numel()
+        torch.manual_seed(seed)
+        (codes, scalar), shape = tg.compress(x, "w")
+        torch.manual_seed(seed)
+        u = torch.empty(x.numel()).uniform_()
+        dec = tg.decompress((codes, scalar), shape)
+        st.add(f"terngrad_{case}", {"codec": "terngrad", "seed": seed, "shape": list(x.shape)},
+               x=x, u=u, codes=codes, scalar=scalar, dec=dec)
+    st.save()
+
+
 def gen_world2():
     import torch.multiprocessing as mp
     st = Store("world2")
@@ -475,7 +571,8 @@ if __name__ == "__main__":
         with open(mpath) as f:
             MANIFEST.update(json.load(f))
     for name, fn in (("sign", gen_sign), ("sparse", gen_sparse), ("quant", gen_quant),
-                     ("powersgd", gen_powersgd), ("world2", gen_world2), ("dgc", gen_dgc)):
+                     ("powersgd", gen_powersgd), ("world2", gen_world2), ("dgc", gen_dgc),
+                     ("torchflav", gen_torchflav)):
         if not only or name in only:
             fn()
     with open(mpath, "w") as f:

@@ -43,11 +43,83 @@ def test_p_and_qt_vs_numpy(shape, r):
     assert _close(_np(res), M - _np(out), 1, scale=np.abs(M).max())
 
 
+def _exact_qr(a):
+    """f64 Householder QR of the (f32) input, columns signed like Gram-Schmidt (R_cc > 0)."""
+    q, r = np.linalg.qr(np.asarray(a, dtype=np.float64))
+    return q * np.where(np.diag(r) < 0, -1.0, 1.0)
+
+
 def test_orthogonalize_golden(golden):
-    for c in golden.cases("powersgd", codec="orthogonalize"):
+    """Well-conditioned reference cases: within 1e-4 of the reference's f32 MGS.  Ill-conditioned
+    ones (kappa 1e4 / 1e7, two nearly collinear columns, P of a rank-2 gradient): the reference's own
+    f32 MGS is only determined to ~kappa * eps32 in the late columns (its distance from the exact
+    factor is measured here), so each column must match the reference within 1e-4 OR within 4x the
+    reference's own error, whichever is larger; and the result must be finite and orthonormal (the
+    one-pass Cholesky-QR gave NaN / lost orthogonality there before the MGS2 fallback)."""
+    cases = golden.cases("powersgd", codec="orthogonalize")
+    assert {c.name for c in cases} >= {"orth_ill_4096x4_k10000", "orth_ill_4096x4_k1e+07", "orth_collinear_4096x4",
+                                       "orth_rank2_4096x4", "orth_ill_500x3_k10000"}
+    for c in cases:
         a = _t(c["a"])
         ops.orthogonalize_(a)
-        assert np.allclose(_np(a), c["out"], rtol=1e-4, atol=1e-5), c.name
+        out = _np(a)
+        ref = c["out"]
+        assert np.isfinite(out).all(), c.name
+        r = out.shape[1]
+        assert np.abs(out.T.astype(np.float64) @ out - np.eye(r)).max() < 1e-5, c.name
+        if "kappa" not in c.meta:
+            assert np.allclose(out, ref, rtol=1e-4, atol=1e-5), c.name
+            continue
+        qx = _exact_qr(c["a"])
+        ref_err = np.abs(ref - qx).max(axis=0)
+        ours = np.abs(out - ref).max(axis=0)
+        assert np.all(ours <= np.maximum(1e-4, 4 * ref_err)), (c.name, ours, ref_err)
+        assert np.abs(out - qx).max() < 1e-5, c.name           # and it IS the exact factor
+
+
+@pytest.mark.parametrize("n,r,kappa", [(9000, 4, 1e7), (4096, 4, 1e6), (3000, 3, 1e9), (600, 8, 1e7)])
+def test_orthogonalize_ill_conditioned_vs_exact_qr(n, r, kappa):
+    """Both kernels (rank-4 register path, generic chunked path) on inputs with condition number
+    up to 1e9: finite, orthonormal, equal to the exact QR factor of the f32 input."""
+    rng = np.random.default_rng(int(np.log10(kappa)) + n)
+    u, _ = np.linalg.qr(rng.standard_normal((n, r)))
+    v, _ = np.linalg.qr(rng.standard_normal((r, r)))
+    a = ((u * np.logspace(0, -np.log10(kappa), r)) @ v.T).astype(np.float32)
+    out = _np(ops.orthogonalize_(_t(a)))
+    assert np.isfinite(out).all()
+    assert np.abs(out.T.astype(np.float64) @ out - np.eye(r)).max() < 1e-5
+    qx = _exact_qr(a)
+    err = np.abs(out - qx).max(axis=0)
+    rows = 4 if r <= 4 else (2 if r <= 8 else 1)     # powersgd.hip kOrthRows
+    if n <= 1024 * rows:
+        assert err.max() < 1e-5, err        # register-resident f64 MGS2: the exact factor
+    else:                                   # tall: f32 storage between sweeps, still ahead of the reference
+        ref_err = np.abs(O.orthogonalize(a) - qx).max(axis=0)
+        assert np.all(err <= np.maximum(1e-5, ref_err)), (err, ref_err)
+
+
+def test_orthogonalize_degenerate_columns():
+    """A zero column (a layer whose gradient slice is zero): the reference's MGS divides 0 by 0 and
+    the NaN spreads to every later column, then to P, Q and the decompressed gradient.  Here the
+    zero column stays zero and the other columns are the exact factor.  An
+    exactly repeated column: f32 rounding leaves a noise residual in both implementations; ours
+    is still finite and orthonormal."""
+    rng = np.random.default_rng(5)
+    for n, r in ((4096, 4), (700, 3)):
+        a = rng.standard_normal((n, r)).astype(np.float32)
+        a[:, 1] = 0.0
+        assert np.isnan(O.orthogonalize(a)).any()        # what the reference does
+        out = _np(ops.orthogonalize_(_t(a)))
+        assert np.isfinite(out).all()
+        assert np.all(out[:, 1] == 0)
+        keep = [c for c in range(r) if c != 1]
+        assert np.abs(out[:, keep] - _exact_qr(a[:, keep])).max() < 1e-5
+        a = rng.standard_normal((n, r)).astype(np.float32)
+        a[:, 2] = a[:, 0]
+        out = _np(ops.orthogonalize_(_t(a)))
+        assert np.isfinite(out).all()
+        assert np.abs(out.T.astype(np.float64) @ out - np.eye(r)).max() < 1e-5
+        assert np.abs(out[:, :2] - _exact_qr(a[:, :2])).max() < 1e-5
 
 
 def test_powersgd_compressor_golden(golden):
@@ -85,10 +157,14 @@ def test_powersgd_memory_allreduce_sequence(golden):
         payload, ctx = comp.compress(t, "w")
         mem.update(t, "w", comp, payload, ctx)
         out = comm.send_receive(payload, "w", ctx)
-        assert np.allclose(_np(t), c[f"t{s}"], rtol=1e-5, atol=1e-5)
-        assert np.allclose(_np(ctx[0]), c[f"p{s}"], rtol=1e-3, atol=1e-4)
-        assert np.allclose(_np(mem.residuals["w"]), c[f"res{s}"], rtol=1e-3, atol=1e-3)
-        assert np.allclose(_np(out), c[f"dec{s}"], rtol=1e-3, atol=1e-3)
+        # the stated bar: rel 1e-5 * sqrt(m), m = 40 columns
+        m = c[f"g{s}"].shape[1]
+        tscale = np.abs(c[f"t{s}"]).max()
+        assert _close(_np(t), c[f"t{s}"], m), s
+        assert _close(_np(ctx[0]), c[f"p{s}"], m), s
+        assert _close(_np(ctx[1]), c[f"q{s}"], m), s
+        assert _close(_np(out), c[f"dec{s}"], m, scale=tscale), s
+        assert _close(_np(mem.residuals["w"]), c[f"res{s}"], m, scale=tscale), s
 
 
 def test_one_dim_passthrough():

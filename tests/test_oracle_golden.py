@@ -321,3 +321,48 @@ def test_dgc_memory_oracle_vs_reference(golden):
             assert same_bits(r, c[f"res{s}"]) and same_bits(a, c[f"grad{s}"]), (c.name, s)
     quirk = golden.case("dgc", "dgc_clipping_quirk")
     assert bool(quirk["flag"][0])   # the reference's gradient_clipping=True raises TypeError
+
+
+# ----------------------------------------------------------------------------- Horovod flavour
+def test_torchflav_qsgd_global_norm(golden):
+    cases = golden.cases("torchflav", codec="qsgd")
+    assert len(cases) >= 14
+    for c in cases:
+        q = c.meta["quantum_num"]
+        codes, norm = O.qsgd_global_compress(c["x"], c["u"], q)
+        assert same_bits(norm, c["norm"].ravel()), c.name
+        assert same_bits(codes, c["codes"].ravel()), c.name
+        assert same_bits(O.qsgd_global_decode(c["codes"].ravel(), c["norm"], q, c["x"].size), c["dec"].ravel()), c.name
+
+
+def test_torchflav_threshold_strict(golden):
+    for c in golden.cases("torchflav", codec="threshold"):
+        v, i = O.threshold_select_strict(c["x"], c.meta["threshold"])
+        assert np.array_equal(i, c["idx"]), c.name
+        assert same_bits(v, c["vals"]), c.name
+
+
+def test_torchflav_randomk_randperm(golden):
+    for c in golden.cases("torchflav", codec="randomk"):
+        idx, h = O.randomk_perm_indices(c.meta["name"], c.meta["seed"] - sum(bytes(c.meta["name"], "utf8")),
+                                        c.meta["n"], c.meta["ratio"])
+        assert h == c.meta["seed"]
+        assert np.array_equal(idx, c["idx"]), c.name
+        assert np.unique(idx).size == idx.size
+
+
+def test_torchflav_topk_int64(golden):
+    for c in golden.cases("torchflav", codec="topk"):
+        assert c["idx"].dtype == np.int64
+        k = O.ratio_k(c["x"].size, c.meta["ratio"])
+        v, i = O.topk_select(c["x"].ravel(), k)
+        assert topk_sets_match(c["x"].ravel(), i, c["idx"], k), c.name
+
+
+def test_torchflav_terngrad_equals_dist_rule(golden):
+    """uniform_(0, scalar) (torch flavour) == uniform_(0, 1) * scalar (dist flavour), bit for bit."""
+    for c in golden.cases("torchflav", codec="terngrad"):
+        codes, scal = O.terngrad_compress(c["x"], c["u"])
+        assert np.array_equal(codes, c["codes"].ravel()), c.name
+        assert same_bits(scal, c["scalar"].ravel()), c.name
+        assert same_bits(O.terngrad_decode(codes, scal), c["dec"].ravel()), c.name

@@ -88,6 +88,7 @@ class OracleShardKernels:
         xh[:HIST] = torch.from_numpy(np.bincount(bins, minlength=HIST)[:HIST].astype(np.int32))
         xh[HIST] = sure.size
         xh[HIST + 1] = cand.size
+        xh[HIST + 2] = t.size               # the shard length (sharded.py re-checks the partition)
         self.state.update(lo=lo, sh=sh, n_sure=ns, cand=cand, cand_t=t[cand], bins=bins, base=base)
 
     def route(self, res, base, k, B, vals, idx, bsend):
@@ -164,16 +165,17 @@ def _bucket(case, n, seed):
     return g
 
 
-def _worker(rank, world, path, outdir, sizes, case, ratio, dense):
+def _worker(rank, world, path, outdir, sizes, case, ratio, dense, sizes2=None):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded import ShardedTopK
-    n = sum(sizes)
-    base = sum(sizes[:rank])
     eng = ShardedTopK(ratio, dense=dense, kernels=OracleShardKernels())
     res = {}
     for s in range(2):
+        part = sizes2 if (s == 1 and sizes2 is not None) else sizes
+        n = sum(part)
+        base = sum(part[:rank])
         full = _bucket(case, n, 100 + s)
-        out = eng.step(torch.from_numpy(full[base:base + sizes[rank]].copy()), "bucket")
+        out = eng.step(torch.from_numpy(full[base:base + part[rank]].copy()), "bucket")
         v, i = eng.last_payload
         keep = i.numpy() >= 0
         res[f"out{s}"] = out.numpy().copy()
@@ -185,9 +187,9 @@ def _worker(rank, world, path, outdir, sizes, case, ratio, dense):
     dist.destroy_process_group()
 
 
-def _run(world, sizes, case, ratio, dense="replicated"):
+def _run(world, sizes, case, ratio, dense="replicated", sizes2=None):
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, dense),
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, dense, sizes2),
                  nprocs=world, join=True)
         outs = []
         for r in range(world):
@@ -206,6 +208,7 @@ def _bits(a, b):
     (2, [50000, 33333], "normal", 0.01),
     (2, [40000, 40000], "ties", 0.5),
     (2, [150000, 150000], "miss", 0.01),
+    (3, [150000, 120001, 99999], "miss", 0.01),      # fallback gather with unequal shards
 ])
 def test_sharded_topk_matches_single_bucket(world, sizes, case, ratio):
     outs = _run(world, sizes, case, ratio)
@@ -227,6 +230,28 @@ def test_sharded_topk_matches_single_bucket(world, sizes, case, ratio):
         assert all(o["fb0"][0] for o in outs)
     else:
         assert not any(o["fb0"][0] or o["fb1"][0] for o in outs)
+
+
+def test_sharded_resize_one_rank_between_steps():
+    """only rank 1's shard changes size at step 2.  Every rank must see it in the same
+    step (no rank-local collective, no hang), re-plan with the new partition and drop the residual
+    that belongs to the old one."""
+    sizes, sizes2 = [40000, 40000], [40000, 25000]
+    outs = _run(2, sizes, "normal", 0.01, sizes2=sizes2)
+    g0 = _bucket("normal", sum(sizes), 100)
+    _, _, i0, r0, out0 = O.topk_residual_step(g0, None, 0.01)
+    idx = np.sort(np.concatenate([o["idx0"] for o in outs]).astype(np.int64))
+    assert np.array_equal(idx, i0.astype(np.int64))
+    g1 = _bucket("normal", sum(sizes2), 101)
+    _, v1, i1, r1, out1 = O.topk_residual_step(g1, None, 0.01)      # residual dropped
+    idx = np.concatenate([o["idx1"] for o in outs]).astype(np.int64)
+    vals = np.concatenate([o["vals1"] for o in outs])
+    order = np.argsort(idx)
+    assert np.array_equal(idx[order], i1.astype(np.int64))
+    assert _bits(vals[order], v1)
+    assert _bits(np.concatenate([o["res1"] for o in outs]), r1)
+    for o in outs:
+        assert _bits(o["out1"], out1)
 
 
 def test_sharded_dense_shard_mode():
