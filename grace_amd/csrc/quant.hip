@@ -1019,20 +1019,56 @@ __global__ __launch_bounds__(kQBlock) void tern_decode_kernel(const int8_t* __re
 }
 
 // ================================================================================================
+// Elementwise byte codecs (natural, cnat, fp16).  Every thread handles quads of 4 consecutive
+// elements: one 16-B load of x (and of an injected random stream), one 4-B code store (8-B for
+// fp16), grid-stride over the quads; a ragged tail or unaligned views fall back to per-element
+// accesses inside the same quad.
+__device__ __forceinline__ bool quad_fast(int64_t e, int64_t n, bool aligned) { return aligned && e + 3 < n; }
+
 // natural compression, cupy flavour (grace_dl/dist/compressor/natural.py:12-40): exponent
 // rounded up when mantissa > randint(0, 2^23 - 1), clipped to [18, 145], code = sign | (E - 18).
+__device__ __forceinline__ uint32_t natural_code(float xv, int32_t r) {
+  const int32_t bits = __float_as_int(xv);
+  const int32_t sign = bits & (int32_t)0x80000000;
+  int32_t e = bits & 0x7F800000;
+  const int32_t mant = bits & 0x007FFFFF;
+  if (mant > r) e += 0x00800000;
+  e = min(max(e, (int32_t)0x09000000), (int32_t)0x48800000);
+  return (uint32_t)(uint8_t)((sign >> 24) | ((e >> 23) - 18));
+}
+
 __global__ __launch_bounds__(kQBlock) void natural_encode_kernel(const float* __restrict__ x, int64_t n,
                                                                 const int32_t* __restrict__ ri, uint64_t seed,
-                                                                uint8_t* __restrict__ codes) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock) {
-    const int32_t bits = __float_as_int(x[i]);
-    const int32_t sign = bits & (int32_t)0x80000000;
-    int32_t e = bits & 0x7F800000;
-    const int32_t mant = bits & 0x007FFFFF;
-    const int32_t r = ri ? ri[i] : (int32_t)(mix64(seed ^ mix64((uint64_t)i)) % 0x7FFFFFull);
-    if (mant > r) e += 0x00800000;
-    e = min(max(e, (int32_t)0x09000000), (int32_t)0x48800000);
-    codes[i] = (uint8_t)((sign >> 24) | ((e >> 23) - 18));
+                                                                uint8_t* __restrict__ codes, int aligned) {
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    const bool fast = quad_fast(e, n, aligned != 0);
+    float v[4];
+    int32_t r[4];
+    load_quad(x, e, n, fast, v);
+    if (ri) {
+      if (fast) {
+        const int4 t = *reinterpret_cast<const int4*>(ri + e);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = e + j < n ? ri[e + j] : 0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = (int32_t)(mix64(seed ^ mix64((uint64_t)(e + j))) % 0x7FFFFFull);
+    }
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = natural_code(v[j], r[j]);
+    if (fast) {
+      *reinterpret_cast<uint32_t*>(codes + e) = c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < n) codes[e + j] = (uint8_t)c[j];
+    }
   }
 }
 
@@ -1045,20 +1081,46 @@ __device__ __forceinline__ float natural_dec(uint32_t c) {
 
 // cnat_cuda flavour (cnat_cuda.cu:68-134): frexp mantissa m in [0.5, 1); exponent kept w.p.
 // 2|m| - 1; LUT: biased E <= 17 -> 0, E -> E - 17 saturating at 127, +128 if negative.
+__device__ __forceinline__ uint32_t cnat_code(float v, float r) {
+  if (v == 0.f) return 0u;
+  int ex;
+  const float prob = fabsf(frexpf(v, &ex)) / 0.5f - 1.0f;
+  if (r >= prob) ex -= 1;
+  const int biased = ex + 127;
+  int code = biased <= 17 ? 0 : min(biased - 17, 127);
+  if (v < 0.f) code += 128;
+  return (uint32_t)code;
+}
+
 __global__ __launch_bounds__(kQBlock) void cnat_encode_kernel(const float* __restrict__ x, int64_t n,
                                                              const float* __restrict__ rnd, int deterministic,
-                                                             uint64_t seed, uint8_t* __restrict__ codes) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock) {
-    const float v = x[i];
-    if (v == 0.f) { codes[i] = 0; continue; }
-    int ex;
-    const float prob = fabsf(frexpf(v, &ex)) / 0.5f - 1.0f;
-    const float r = deterministic ? 0.5f : (rnd ? rnd[i] : uniform01(seed, (uint64_t)i));
-    if (r >= prob) ex -= 1;
-    const int biased = ex + 127;
-    int code = biased <= 17 ? 0 : min(biased - 17, 127);
-    if (v < 0.f) code += 128;
-    codes[i] = (uint8_t)code;
+                                                             uint64_t seed, uint8_t* __restrict__ codes,
+                                                             int aligned) {
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    const bool fast = quad_fast(e, n, aligned != 0);
+    float v[4], r[4];
+    load_quad(x, e, n, fast, v);
+    if (deterministic) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = 0.5f;
+    } else if (rnd) {
+      load_quad(rnd, e, n, fast, r);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = uniform01(seed, (uint64_t)(e + j));
+    }
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = cnat_code(v[j], r[j]);
+    if (fast) {
+      *reinterpret_cast<uint32_t*>(codes + e) = c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < n) codes[e + j] = (uint8_t)c[j];
+    }
   }
 }
 
@@ -1068,33 +1130,87 @@ __device__ __forceinline__ float cnat_dec(uint32_t c) {
   return __uint_as_float(((c >> 7) << 31) | (e << 23));
 }
 
+// decode (+ rank-ordered aggregate of W payloads at `stride`): 4 codes per 4-B load per rank,
+// one 16-B store
 template <int FLAVOUR>   // 0 = cupy natural, 1 = cnat
 __global__ __launch_bounds__(kQBlock) void natural_decode_kernel(const uint8_t* __restrict__ codes,
                                                                 int64_t stride, int world, int64_t n,
                                                                 float divisor, int aggregate,
-                                                                float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock) {
-    float acc = 0.f;
+                                                                float* __restrict__ out, int aligned) {
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    const bool fast = quad_fast(e, n, aligned != 0);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int w = 0; w < world; ++w) {
-      const uint32_t c = codes[w * stride + i];
-      const float d = FLAVOUR == 0 ? natural_dec(c) : cnat_dec(c);
-      acc = (aggregate || w > 0) ? acc + d : d;
+      const uint8_t* c = codes + w * stride + e;
+      uint32_t wd;
+      if (fast) {
+        wd = *reinterpret_cast<const uint32_t*>(c);
+      } else {
+        wd = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (e + j < n) wd |= (uint32_t)c[j] << (8 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t cj = (wd >> (8 * j)) & 0xFFu;
+        const float d = FLAVOUR == 0 ? natural_dec(cj) : cnat_dec(cj);
+        acc[j] = (aggregate || w > 0) ? acc[j] + d : d;
+      }
     }
-    out[i] = divisor == 1.0f ? acc : acc / divisor;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = divisor == 1.0f ? acc[j] : acc[j] / divisor;
+    if (fast) {
+      *reinterpret_cast<f4v*>(out + e) = f4v{acc[0], acc[1], acc[2], acc[3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < n) out[e + j] = acc[j];
+    }
   }
 }
 
 // ================================================================================================
-// fp16 (grace_dl/dist/compressor/fp16.py): round-to-nearest-even cast and back
+// fp16 (grace_dl/dist/compressor/fp16.py): round-to-nearest-even cast and back, 4 per quad
 __global__ __launch_bounds__(kQBlock) void f32_to_f16_kernel(const float* __restrict__ x, __half* __restrict__ h,
-                                                            int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock)
-    h[i] = __float2half_rn(x[i]);
+                                                            int64_t n, int aligned) {
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    const bool fast = quad_fast(e, n, aligned != 0);
+    float v[4];
+    load_quad(x, e, n, fast, v);
+    if (fast) {
+      uint2 wd;
+      wd.x = (uint32_t)__half_as_ushort(__float2half_rn(v[0])) | ((uint32_t)__half_as_ushort(__float2half_rn(v[1])) << 16);
+      wd.y = (uint32_t)__half_as_ushort(__float2half_rn(v[2])) | ((uint32_t)__half_as_ushort(__float2half_rn(v[3])) << 16);
+      *reinterpret_cast<uint2*>(h + e) = wd;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < n) h[e + j] = __float2half_rn(v[j]);
+    }
+  }
 }
 __global__ __launch_bounds__(kQBlock) void f16_to_f32_kernel(const __half* __restrict__ h, float* __restrict__ x,
-                                                            int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQBlock)
-    x[i] = __half2float(h[i]);
+                                                            int64_t n, int aligned) {
+  const int64_t nq = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
+    const int64_t e = q << 2;
+    if (quad_fast(e, n, aligned != 0)) {
+      const uint2 wd = *reinterpret_cast<const uint2*>(h + e);
+      *reinterpret_cast<f4v*>(x + e) = f4v{__half2float(__ushort_as_half((unsigned short)wd.x)),
+                                           __half2float(__ushort_as_half((unsigned short)(wd.x >> 16))),
+                                           __half2float(__ushort_as_half((unsigned short)wd.y)),
+                                           __half2float(__ushort_as_half((unsigned short)(wd.y >> 16)))};
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < n) x[e + j] = __half2float(h[e + j]);
+    }
+  }
 }
 
 // ================================================================================================
@@ -1335,8 +1451,10 @@ grace_status_t grace_natural_compress(const float* x, int64_t n, const int32_t* 
                                       uint8_t* codes, void* stream) {
   GRACE_REQUIRE(x && codes && n >= 0, "grace_natural_compress: bad arguments");
   if (n == 0) return GRACE_OK;
-  natural_encode_kernel<<<stream_grid(n, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(x, n, rand_int, seed,
-                                                                                        codes);
+  const int al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(rand_int)) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
+  natural_encode_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      x, n, rand_int, seed, codes, al);
   GRACE_CHECK_LAUNCH("grace_natural_compress");
   return GRACE_OK;
 }
@@ -1345,8 +1463,10 @@ grace_status_t grace_cnat_compress(const float* x, int64_t n, const float* rand,
                                    uint64_t seed, uint8_t* codes, void* stream) {
   GRACE_REQUIRE(x && codes && n >= 0, "grace_cnat_compress: bad arguments");
   if (n == 0) return GRACE_OK;
-  cnat_encode_kernel<<<stream_grid(n, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(x, n, rand, deterministic,
-                                                                                     seed, codes);
+  const int al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(rand)) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
+  cnat_encode_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      x, n, rand, deterministic, seed, codes, al);
   GRACE_CHECK_LAUNCH("grace_cnat_compress");
   return GRACE_OK;
 }
@@ -1357,13 +1477,15 @@ grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, in
   GRACE_REQUIRE(codes && out && world >= 1 && n >= 0 && (flavour == 0 || flavour == 1),
                 "grace_natural_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
-  const unsigned grid = stream_grid(n, kQBlock, 4096);
+  const unsigned grid = stream_grid((n + 3) / 4, kQBlock, 4096);
+  const int al = (reinterpret_cast<uintptr_t>(codes) & 3) == 0 && (stride % 4 == 0 || world == 1) &&
+                 (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   if (flavour == 0)
     natural_decode_kernel<0><<<grid, kQBlock, 0, as_stream(stream)>>>(codes, stride, world, n, divisor,
-                                                                      aggregate, out);
+                                                                      aggregate, out, al);
   else
     natural_decode_kernel<1><<<grid, kQBlock, 0, as_stream(stream)>>>(codes, stride, world, n, divisor,
-                                                                      aggregate, out);
+                                                                      aggregate, out, al);
   GRACE_CHECK_LAUNCH("grace_natural_decompress");
   return GRACE_OK;
 }
@@ -1371,8 +1493,9 @@ grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, in
 grace_status_t grace_fp16_compress(const float* x, void* half_out, int64_t n, void* stream) {
   GRACE_REQUIRE(x && half_out && n >= 0, "grace_fp16_compress: bad arguments");
   if (n == 0) return GRACE_OK;
-  f32_to_f16_kernel<<<stream_grid(n, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      x, reinterpret_cast<__half*>(half_out), n);
+  const int al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(half_out) & 7) == 0;
+  f32_to_f16_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      x, reinterpret_cast<__half*>(half_out), n, al);
   GRACE_CHECK_LAUNCH("grace_fp16_compress");
   return GRACE_OK;
 }
@@ -1380,8 +1503,9 @@ grace_status_t grace_fp16_compress(const float* x, void* half_out, int64_t n, vo
 grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n, void* stream) {
   GRACE_REQUIRE(half_in && out && n >= 0, "grace_fp16_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
-  f16_to_f32_kernel<<<stream_grid(n, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      reinterpret_cast<const __half*>(half_in), out, n);
+  const int al = (reinterpret_cast<uintptr_t>(half_in) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  f16_to_f32_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      reinterpret_cast<const __half*>(half_in), out, n, al);
   GRACE_CHECK_LAUNCH("grace_fp16_decompress");
   return GRACE_OK;
 }

@@ -80,7 +80,7 @@ struct TopkCtl {
   uint32_t bticket;    // bracket kernel arrival counter (reset by its last workgroup)
   uint32_t bar_count;  // finalize grid barrier (parallel exact fallback): arrivals
   uint32_t bar_gen;    //   and generation
-  uint32_t pad;
+  uint32_t thr_mid;    // provisional selection threshold of the fused main pass (key > thr_mid)
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 
@@ -519,8 +519,8 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   __shared__ uint32_t lh[kBracketBins];
   __shared__ uint32_t lc[kCoarseBins];
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_fc[4];
-  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_fc[6];
+  __shared__ uint32_t s_res[3];
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
   STAMP(w.ctl, 0);
@@ -568,17 +568,20 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
   const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
   const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
-  const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
-                          (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1)};
-  // coarse: thread t owns bins top, top-1 (descending); one block scan finds both coarse bins
+  // third target: the sample's estimate of the k-th rank itself, for the provisional selection
+  const int64_t rank_mid = (int64_t)floor(mu);
+  const uint32_t r1[3] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
+                          (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1),
+                          (uint32_t)((rank_mid < 0 ? 0 : (rank_mid >= S ? S - 1 : rank_mid)) + 1)};
+  // coarse: thread t owns bins top, top-1 (descending); one block scan finds the three coarse bins
   static_assert(kCoarseBins == 2 * kSampleBlock, "two coarse bins per thread");
   const int top = kCoarseBins - 1 - 2 * tid;
   const uint32_t h0 = __hip_atomic_load(w.chist + top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t h1 = __hip_atomic_load(w.chist + top - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid < 4) s_fc[tid] = 0;
+  if (tid < 6) s_fc[tid] = 0;
   const uint32_t ex = block_excl_scan<kSelBlock>(h0 + h1, s_w, nullptr);
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < 3; ++q)
     if (ex < r1[q] && r1[q] <= ex + h0 + h1) {
       const bool first = r1[q] <= ex + h0;
       s_fc[2 * q] = (uint32_t)(first ? top : top - 1);
@@ -588,17 +591,19 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   // fine: one 16-lane group per target rank, inclusive scan of the coarse bin's 16 fine bins
   // (descending) and the first lane whose running count reaches the rank
   if (tid < 64) {
-    const int q = (tid >> 4) & 1, j = tid & 15;
-    const uint32_t bin = s_fc[2 * q] * 16 + (15 - j);
-    uint32_t v = tid < 32 ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const int q = tid >> 4, j = tid & 15;
+    const bool act = q < 3;
+    const uint32_t bin = act ? s_fc[2 * q] * 16 + (15 - j) : 0u;
+    uint32_t v = act ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) {
       const uint32_t u = __shfl_up(v, o, 16);
       if (j >= o) v += u;
     }
-    const uint64_t bal = __ballot(tid < 32 && s_fc[2 * q + 1] + v >= r1[q]);
+    const int qc = act ? q : 0;
+    const uint64_t bal = __ballot(act && s_fc[2 * qc + 1] + v >= r1[qc]);
     const uint32_t hm = (uint32_t)(bal >> (16 * q)) & 0xFFFFu;
-    if (tid < 32 && j == __ffs(hm) - 1) s_res[q] = bin;
+    if (act && j == __ffs(hm) - 1) s_res[q] = bin;
   }
   __syncthreads();
   STAMP_IF(true, w.ctl, 4);
@@ -613,9 +618,14 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
     uint32_t sh = 0;
     const uint64_t span = (uint64_t)hi - (uint64_t)lo;   // keys lo..hi -> bins 0..span>>sh
     while ((span >> sh) >= (uint64_t)kHistBins) ++sh;
+    // provisional threshold: the middle of the fine bin holding the sample's k-th estimate,
+    // clamped into the candidate band (the fused main pass writes candidates above it as selected)
+    uint32_t mid = (s_res[2] << 16) | 0x8000u;
+    mid = mid < lo ? lo : (mid > hi ? hi : mid);
     w.ctl->thr_lo = lo;
     w.ctl->thr_hi = hi;
     w.ctl->shift = sh;
+    w.ctl->thr_mid = mid;
     w.ctl->bticket = 0u;
   }
   STAMP_IF(true, w.ctl, 5);
@@ -690,7 +700,7 @@ struct MainShared {
 // from the staged entries at the flush instead of a masked ds_add per element in the stream.
 template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
-                                               uint32_t hi, uint32_t sh, int64_t gbase,
+                                               uint32_t hi, uint32_t sh, uint32_t mid, int64_t gbase,
                                                const float4 (&rc)[kGroup], const float4 (&gc)[kGroup]) {
   const int64_t n = a.n;
   float4 t[kGroup];
@@ -721,7 +731,9 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
       msure |= (uint32_t)sure << (u * 4 + j);
       mcand |= (uint32_t)cand << (u * 4 + j);
       if constexpr (MODE == kDenseFused) {
-        if (sure) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
+        // sure elements, and candidates above the provisional threshold, are written as selected;
+        // the finalize fixes up only the candidates whose final decision differs
+        if (sure || (cand && key > mid)) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
       }
     }
     if constexpr (MODE == kDenseRes || MODE == kDenseFused) st4<FAST>(a.r, i0, n, rout);
@@ -772,7 +784,7 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
 
 template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
-                                              uint32_t lo, uint32_t hi, uint32_t sh, int64_t chunk) {
+                                              uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
   constexpr int NG = kMainVec / kGroup;
   const int64_t cbase = chunk * kMainChunk + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
@@ -782,7 +794,7 @@ __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w
     const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
     float4 rn[kGroup], gn[kGroup];
     if (q + 1 < NG) load_group<HAS_RES, FAST>(a, gbase + kGroup * (kMainBlock * 4), rn, gn);
-    classify_group<HAS_RES, MODE, FAST>(a, w, sm, lo, hi, sh, gbase, rc, gc);
+    classify_group<HAS_RES, MODE, FAST>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc);
 #pragma unroll
     for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
   }
@@ -825,12 +837,12 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
 }
 
 template <bool HAS_RES, int MODE, bool VEC>
-__global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
+__global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w) {   // <= 128 VGPRs: 4 WGs/CU
   __shared__ MainShared sm;
   const int tid = threadIdx.x;
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   if (tid < 4) sm.cnt[tid] = 0;
-  const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift;
+  const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   const int64_t nchunks = (a.n + kMainChunk - 1) / kMainChunk;
   // sharded mode: this rank's shard length rides in the exchanged counters, so every rank can
   // check the shard sizes it planned with (grace_amd/dist/sharded.py)
@@ -840,9 +852,9 @@ __global__ __launch_bounds__(kMainBlock) void topk_main(StepArgs a, TopkWs w) {
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     if (VEC && (chunk + 1) * kMainChunk <= a.n)
-      main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, chunk);
+      main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
     else
-      main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, chunk);
+      main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
     flush_staged(a, w, sm, lo, sh);
   }
   __syncthreads();
@@ -941,9 +953,32 @@ struct MainTs {
   }
 };
 
+// the boundary list into LDS (pairwise-ranking case); issued by the last workgroup BEFORE its own
+// deferred scattered writes, so the in-order vmcnt wait for these loads does not also wait for them
+template <int BLOCK>
+__device__ __forceinline__ bool boundary_preload(const TopkWs& w, bool ok, uint32_t need, uint32_t nb,
+                                                 FinShared<BLOCK>& fs) {
+  if (!ok || need == 0 || nb > (uint32_t)kPairCap) return false;
+  for (int j = threadIdx.x; j < (int)nb; j += BLOCK) {
+    const int2 e = ld_agent_i2(w.bnd + j);
+    fs.s_ent[j] = e;
+    fs.s_comp[j] = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
+  }
+  return true;
+}
+
+// boundary-bin entry not selected: in the fused mode undo a provisional selection (key > mid)
+template <int MODE>
+__device__ __forceinline__ void unselect(const StepArgs& a, int2 e, uint32_t mid) {
+  if constexpr (MODE == kDenseFused) {
+    const float v = u2f((uint32_t)e.y);
+    if (abs_key(v) > mid) { a.r[e.x] = v; a.out[e.x] = 0.f; }
+  }
+}
+
 template <int MODE, int BLOCK, bool AG>
 __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint32_t need, uint32_t nb,
-                              FinShared<BLOCK>& fs) {
+                              FinShared<BLOCK>& fs, bool preloaded, uint32_t mid) {
   const uint32_t k = (uint32_t)a.k;
   if (ok) {
     if (need == 0) return;
@@ -952,11 +987,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
       // rank by pairwise comparison of unique composites; G adjacent lanes share one entry's
       // comparisons and combine their counts with xor-shuffles
       const int nbi = (int)nb;
-      for (int j = threadIdx.x; j < nbi; j += BLOCK) {
-        const int2 e = ld_agent_i2(w.bnd + j);
-        fs.s_ent[j] = e;
-        fs.s_comp[j] = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
-      }
+      if (!preloaded) boundary_preload<BLOCK>(w, ok, need, nb, fs);
       int G = 1;
       while (G < 16 && nbi * (G * 2) <= BLOCK) G *= 2;
       __syncthreads();
@@ -966,9 +997,10 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
         uint32_t rank = 0;
         for (int q = part; q < nbi; q += G) rank += fs.s_comp[q] > me;
         for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
-        if (part == 0 && rank < need) {
+        if (part == 0) {
           const int2 e = fs.s_ent[el];
-          emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
+          if (rank < need) emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
+          else unselect<MODE>(a, e, mid);
         }
       }
       return;
@@ -986,6 +1018,8 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
       if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) {
         const uint32_t p = atomicAdd(&fs.s_pos, 1u);
         emit<MODE>(a, pos0 + p, e.x, u2f((uint32_t)e.y));
+      } else {
+        unselect<MODE>(a, e, mid);
       }
     }
     return;
@@ -998,19 +1032,27 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
   block_write_selected<MODE, BLOCK>(a, f, a.n, T, 0u, fs.s_w);
 }
 
-// payload + dense writes of a round's above-boundary candidates (bits of fsel), from slot ps on
+// One round of routed candidates: payload writes of the above-boundary ones (bits of fsel) from
+// slot ps on, and their residual / dense writes -- in the fused mode only where the main pass's
+// provisional decision (key > mid) was wrong, in both directions (fbelow: below the boundary bin).
 template <int MODE>
-__device__ __forceinline__ void write_selected(const StepArgs& a, const int2 (&e)[kFinPer], uint32_t fsel,
-                                               uint32_t ps) {
+__device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[kFinPer], uint32_t fsel,
+                                            uint32_t fbelow, uint32_t ps, uint32_t mid) {
 #pragma unroll
   for (int u = 0; u < kFinPer; ++u) {
+    const float v = u2f((uint32_t)e[u].y);
+    const bool above_mid = abs_key(v) > mid;
     if ((fsel >> u) & 1u) {
-      const float v = u2f((uint32_t)e[u].y);
       a.vals[ps] = v;
       a.idx[ps] = e[u].x;
-      if constexpr (MODE != kDenseNone) a.r[e[u].x] = v - v;
-      if constexpr (MODE == kDenseFused) a.out[e[u].x] = 0.f + v;
+      if constexpr (MODE == kDenseRes) a.r[e[u].x] = v - v;
+      if constexpr (MODE == kDenseFused) {
+        if (!above_mid) { a.r[e[u].x] = v - v; a.out[e[u].x] = 0.f + v; }
+      }
       ++ps;
+    } else if (MODE == kDenseFused && ((fbelow >> u) & 1u) && above_mid) {
+      a.r[e[u].x] = v;
+      a.out[e[u].x] = 0.f;
     }
   }
 }
@@ -1159,11 +1201,12 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
 
 // finalize workgroup `fi` of `fcnt`; returns true in the workgroup that ran the boundary step
 template <int MODE, int BLOCK, bool AG>
-__device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
+__device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs,
+                             bool coresident) {
   constexpr int PER = kHistBins / BLOCK;
   const int t = threadIdx.x;
   const uint32_t n_sure = ld_u32<AG>(&w.ctl->n_sure), n_cand = ld_u32<AG>(&w.ctl->n_cand);
-  const uint32_t thr_lo = w.ctl->thr_lo, shift = w.ctl->shift;   // written by the bracket launch
+  const uint32_t thr_lo = w.ctl->thr_lo, shift = w.ctl->shift, mid = w.ctl->thr_mid;   // bracket launch
   const uint32_t k = (uint32_t)a.k;
   const bool ok = n_sure <= k && (uint64_t)n_sure + n_cand >= k && n_cand <= (uint64_t)w.cap;
   {  // the bracket's sample histograms are free again: zero them for the next step.  Write-through
@@ -1180,14 +1223,17 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
       else __builtin_amdgcn_raw_buffer_store_b128(zero, rc, (z - kBracketBins / 4) * 16, 0, 16);
     }
   }
-  if (!ok && fcnt > 1 && fcnt <= kFinBlocks) {   // every finalize workgroup: the parallel fallback
+  // every finalize workgroup: the parallel fallback -- only when the launch checked that all of
+  // them are resident at once (its grid barriers spin); otherwise the last workgroup alone runs
+  // the single-workgroup exact select below (same result, slower)
+  if (!ok && coresident && fcnt > 1 && fcnt <= kFinBlocks) {
     parallel_exact<MODE, BLOCK, AG>(a, w, fi, fcnt, fs);
     return fi == 0;
   }
   int B = -1;
   uint32_t need = 0, nb = 0;
   int2 e[kFinPer];
-  uint32_t fsel = 0, ps = 0;
+  uint32_t fsel = 0, fbelow = 0, ps = 0;
   bool defer = false;
   if (ok) {
     const uint32_t target = k - n_sure;
@@ -1215,6 +1261,9 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
       w.ctl->n_bnd = nb;
     }
     STAMP_IF(fi == 0, w.ctl, 9);
+    // fused mode, no candidate needed (k sure elements): every candidate is unselected, but the
+    // provisionally selected ones still need their fix-ups -> route with the boundary above all bins
+    if (MODE == kDenseFused && B < 0) B = kHistBins;
     // residual-only mode: sure entries still hold t in r; zero them now
     if constexpr (MODE == kDenseRes) {
       for (uint32_t j = fi * BLOCK + t; j < n_sure; j += fcnt * BLOCK) {
@@ -1233,6 +1282,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
       for (uint32_t r0 = b0; r0 < b1; r0 += BLOCK * kFinPer) {
         uint32_t fb = 0;
         fsel = 0;
+        fbelow = 0;
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u) {
           const uint32_t j = r0 + u * BLOCK + t;
@@ -1240,6 +1290,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
           const int bin = j < b1 ? (int)((abs_key(u2f((uint32_t)e[u].y)) - thr_lo) >> shift) : -1;
           fsel |= (uint32_t)(bin > B) << u;
           fb |= (uint32_t)(bin == B) << u;
+          fbelow |= (uint32_t)(j < b1 && bin < B) << u;
         }
         const uint32_t packed = (uint32_t)__popc(fsel) | ((uint32_t)__popc(fb) << 16);
         uint32_t tot;
@@ -1255,7 +1306,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u)
           if ((fb >> u) & 1u) st_agent_i2(w.bnd + pb++, e[u]);
-        if (!defer) write_selected<MODE>(a, e, fsel, ps);
+        if (!defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid);
       }
     }
   }
@@ -1266,20 +1317,43 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   __syncthreads();
   if (t == 0) fs.s_last = atomicAdd(&w.ctl->ticket, 1u) == (uint32_t)fcnt - 1;
   __syncthreads();
-  if (defer) write_selected<MODE>(a, e, fsel, ps);
-  if (!fs.s_last) return false;
+  const bool last = fs.s_last;
+  const bool preloaded = last && boundary_preload<BLOCK>(w, ok, need, nb, fs);
+  if (defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid);
+  if (!last) return false;
   STAMP_IF(true, w.ctl, 11);
-  boundary_work<MODE, BLOCK, AG>(a, w, ok, need, nb, fs);
+  boundary_work<MODE, BLOCK, AG>(a, w, ok, need, nb, fs, preloaded, mid);
   __syncthreads();
   STAMP_IF(true, w.ctl, 12);
   return true;
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
+__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w, int coresident) {
   __shared__ FinShared<kSelBlock> fs;
   STAMP(w.ctl, 8);
-  finalize_run<MODE, kSelBlock, false>(a, w, blockIdx.x, gridDim.x, fs);
+  finalize_run<MODE, kSelBlock, false>(a, w, blockIdx.x, gridDim.x, fs, coresident != 0);
+}
+
+// Whether all kFinBlocks finalize workgroups are resident at once on this device (the parallel
+// exact fallback's grid barriers need it): the occupancy API's blocks per CU times the CU count,
+// with a 2x margin (the guide's occupancy caveats: the API can be one block per CU high).  Cached
+// per device; the plain launch itself never checks residency.
+template <int MODE>
+static int finalize_coresident() {
+  static int cached[64];
+  static bool init[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!init[dev]) {
+    int per_cu = 0, cus = 0;
+    const bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, topk_finalize<MODE>, kSelBlock, 0) ==
+                        hipSuccess &&
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+    cached[dev] = ok && (int64_t)per_cu * cus >= 2 * (int64_t)kFinBlocks ? 1 : 0;
+    init[dev] = true;
+  }
+  return cached[dev];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1342,7 +1416,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   else
     launch_timed(topk_main<HAS_RES, MODE, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
   GRACE_CHECK_LAUNCH("topk_main");
-  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
+  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w, finalize_coresident<MODE>());
   GRACE_CHECK_LAUNCH("topk_finalize");
   return GRACE_OK;
 }

@@ -53,6 +53,6 @@ class SignSGDCompressor(Compressor):
         if (isinstance(communicator, Allgather) and type(communicator.memory) is NoneMemory
                 and int(communicator.world_size) == 1 and isinstance(tensor, torch.Tensor)
                 and tensor.is_cuda and tensor.dtype == torch.float32):
-            _, out = ops.sign_step_w1(tensor, want_codes=False)
-            return out.view(tensor.shape)
+            _, out = ops.sign_step_w1(tensor, want_codes=False, reuse_out=True)
+            return out if out.shape == tensor.shape else out.view(tensor.shape)
         return None

@@ -64,6 +64,26 @@ def workspace(slot, nbytes, device):
     return buf
 
 
+_reuse = {}
+
+
+def reusable_output(slot, shape, dtype, device):
+    """An output tensor for a per-step codec result, reused across calls when nobody outside this
+    cache still holds the previous one (CPython refcount: dict + local + argument = 3) and the call
+    runs on the stream it was made on, so reuse is stream-ordered behind every earlier use.  A
+    caller that keeps its results gets a fresh tensor each call, exactly as the reference's new
+    allocations; one that consumes and drops them (``grad.copy_(grc.step(grad, name))``,
+    examples/dist/CIFAR10-dawndist/core.py:204-206) skips the allocator on launch-bound steps."""
+    import sys
+    key = (slot, tuple(shape), dtype, str(device), _stream())
+    buf = _reuse.get(key)
+    if buf is not None and sys.getrefcount(buf) == 3:
+        return buf
+    buf = torch.empty(shape, dtype=dtype, device=device)
+    _reuse[key] = buf
+    return buf
+
+
 # ----------------------------------------------------------------------------- elementwise
 def axpby(r, g, beta, gamma, out=None):
     r, g = dev_f32(r, "residual"), dev_f32(g, "gradient")
@@ -134,11 +154,11 @@ def signum_encode(g, momentum_buf, has_prev, momentum):
     return codes
 
 
-def sign_step_w1(x, want_codes=True):
+def sign_step_w1(x, want_codes=True, reuse_out=False):
     if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == F32 and x.is_contiguous()):
         x = dev_f32(x)   # (the checks dev_f32 would make, without its reshape on the common path)
     codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device) if want_codes else None
-    out = torch.empty_like(x)
+    out = reusable_output("sign_w1", x.shape, F32, x.device) if reuse_out else torch.empty_like(x)
     _lib.call("grace_sign_step_w1", x.data_ptr(), _p(codes), out.data_ptr(), x.numel(), _stream())
     return codes, out
 

@@ -303,3 +303,24 @@ def test_terngrad_workspace_reuse_across_shapes():
             assert same_bits(_np(codes[off:off + s]), _np(c1)), (sizes, i)
             assert same_bits(_np(scal[i:i + 1]), _np(s1)), (sizes, i)
             off += s
+
+
+@pytest.mark.parametrize("n,off", [(1, 0), (5, 1), (4099, 0), (4099, 3), (1 << 20, 1)])
+def test_byte_codecs_vectorised_edges(n, off):
+    """natural / cnat / fp16 quad kernels: ragged tails and unaligned views (offset slices)."""
+    rng = np.random.default_rng(n + off)
+    base = rng.standard_normal(n + off).astype(np.float32) * 3
+    x = base[off:]
+    xd = _t(base)[off:]
+    ri = rng.integers(0, 0x7FFFFF, n + off, dtype=np.int32)
+    rd = _t(ri)[off:]
+    codes = ops.natural_compress(xd, rand_int=rd)
+    assert np.array_equal(_np(codes), O.natural_compress(x, ri[off:]))
+    assert same_bits(_np(ops.natural_decompress(codes, n, 0)), O.natural_decode(O.natural_compress(x, ri[off:])))
+    u = rng.random(n + off, dtype=np.float32)
+    cc = ops.cnat_compress(xd, rand=_t(u)[off:])
+    assert np.array_equal(_np(cc), O.cnat_compress(x, u[off:]))
+    assert same_bits(_np(ops.natural_decompress(cc, n, 1)), O.cnat_decode(O.cnat_compress(x, u[off:])))
+    h = ops.fp16_compress(xd)
+    assert np.array_equal(_np(h).view(np.uint16), O.fp16_compress(x).view(np.uint16))
+    assert same_bits(_np(ops.fp16_decompress(h)), O.fp16_decode(O.fp16_compress(x)))

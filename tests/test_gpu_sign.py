@@ -7,6 +7,7 @@ from oracle import grace_oracle as O
 from tests.golden_util import same_bits
 
 pytestmark = pytest.mark.gpu
+ROWS_COLS = (4099, 1)
 DEV = "cuda"
 
 
@@ -106,3 +107,23 @@ def test_no_cpu_path():
     from grace_amd.ops import GraceDeviceError
     with pytest.raises(GraceDeviceError):
         SignSGDCompressor().compress(torch.zeros(8), "w")
+
+
+def test_w1_step_output_reuse_never_clobbers_a_held_result():
+    """The W=1 fused sign step reuses its output buffer only when the caller dropped the previous
+    result (ops.reusable_output); results the caller keeps stay intact."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.signsgd import SignSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    comm = Allgather(SignSGDCompressor(), NoneMemory(), 1)
+    rng = np.random.default_rng(9)
+    xs = [rng.standard_normal(4099).astype(np.float32) for _ in range(4)]
+    kept = [comm.step(_t(x), "w") for x in xs]                  # all held: four distinct buffers
+    assert len({k.data_ptr() for k in kept}) == 4
+    for k, x in zip(kept, xs):
+        assert np.array_equal(_np(k), np.where(x >= 0, 1.0, -1.0).astype(np.float32))
+    p1 = comm.step(_t(xs[0]), "w").data_ptr()                    # dropped at once -> reused
+    p2 = comm.step(_t(xs[1]), "w").data_ptr()
+    assert p1 == p2
+    out = comm.step(_t(xs[2]).view(ROWS_COLS), "w")             # 2-D input keeps its shape
+    assert out.shape == ROWS_COLS

@@ -62,6 +62,50 @@ __global__ __launch_bounds__(B) void r2w2_nt_k(f4* __restrict__ r, const f4* __r
     else { r[i] = x; o[i] = z; }
   }
 }
+// the top-k main pass's layout without its classification: one 16384-element chunk per workgroup,
+// groups of G float4 per lane per array, the next group's nt loads issued before the current group
+// is added and stored (nt); dynamic LDS pins the workgroups per CU (occupancy)
+template <int G>
+__global__ __launch_bounds__(B) void r2w2_nt_chunk_k(f4* __restrict__ r, const f4* __restrict__ g,
+                                                    f4* __restrict__ o, int64_t n4) {
+  extern __shared__ float pin[];
+  if (n4 < 0) pin[threadIdx.x] = 0.f;   // never: keeps the LDS allocation
+  constexpr int NG = 16 / G;
+  const int64_t base = (int64_t)blockIdx.x * (B * 16) + threadIdx.x;
+  f4 a[G], b[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) { a[u] = __builtin_nontemporal_load(r + base + u * B); b[u] = __builtin_nontemporal_load(g + base + u * B); }
+#pragma unroll 1
+  for (int q = 0; q < NG; ++q) {
+    f4 an[G], bn[G];
+    if (q + 1 < NG) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        an[u] = __builtin_nontemporal_load(r + base + ((q + 1) * G + u) * B);
+        bn[u] = __builtin_nontemporal_load(g + base + ((q + 1) * G + u) * B);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      __builtin_nontemporal_store(a[u] + b[u], r + base + (q * G + u) * B);
+      __builtin_nontemporal_store(z, o + base + (q * G + u) * B);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) { a[u] = an[u]; b[u] = bn[u]; }
+  }
+}
+__global__ __launch_bounds__(B) void r2w2_nt_gs_lds_k(f4* __restrict__ r, const f4* __restrict__ g,
+                                                     f4* __restrict__ o, int64_t n4) {
+  extern __shared__ float pin[];
+  if (n4 < 0) pin[threadIdx.x] = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * B + threadIdx.x; i < n4; i += (int64_t)gridDim.x * B) {
+    f4 a = __builtin_nontemporal_load(r + i), b = __builtin_nontemporal_load(g + i);
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    __builtin_nontemporal_store(a + b, r + i);
+    __builtin_nontemporal_store(z, o + i);
+  }
+}
 __global__ void scatter_k(const int* __restrict__ idx, int64_t k, float* __restrict__ o) {
   for (int64_t j = (int64_t)blockIdx.x * B + threadIdx.x; j < k; j += (int64_t)gridDim.x * B) o[idx[j]] = 1.f;
 }
@@ -111,6 +155,16 @@ int main() {
     printf("{\"probe\": \"r2w2 chunk16384 U4\", \"gbps\": %.1f, \"us\": %.1f}\n", 16.0 * n / ms / 1e6, ms * 1e3);
     ms = time_ms([&] { r2w2_chunk_k<8><<<n / 4096 / 4, B>>>((float4*)r, (float4*)g, (float4*)o, n4); });
     printf("{\"probe\": \"r2w2 chunk16384 U8\", \"gbps\": %.1f, \"us\": %.1f}\n", 16.0 * n / ms / 1e6, ms * 1e3);
+  }
+  for (int lds : {0, 20 * 1024, 40 * 1024}) {   // 8+ / 8 / 4 workgroups per CU
+    float ms = time_ms([&] { r2w2_nt_chunk_k<4><<<n / 4096 / 4, B, lds>>>((f4*)r, (f4*)g, (f4*)o, n4); });
+    printf("{\"probe\": \"r2w2 nt chunk16384 G4 lds %d\", \"gbps\": %.1f, \"us\": %.1f}\n", lds, 16.0 * n / ms / 1e6, ms * 1e3);
+    ms = time_ms([&] { r2w2_nt_chunk_k<2><<<n / 4096 / 4, B, lds>>>((f4*)r, (f4*)g, (f4*)o, n4); });
+    printf("{\"probe\": \"r2w2 nt chunk16384 G2 lds %d\", \"gbps\": %.1f, \"us\": %.1f}\n", lds, 16.0 * n / ms / 1e6, ms * 1e3);
+    for (int grid : {1024, 2048}) {
+      ms = time_ms([&] { r2w2_nt_gs_lds_k<<<grid, B, lds>>>((f4*)r, (f4*)g, (f4*)o, n4); });
+      printf("{\"probe\": \"r2w2 nt grid-stride grid %d lds %d\", \"gbps\": %.1f, \"us\": %.1f}\n", grid, lds, 16.0 * n / ms / 1e6, ms * 1e3);
+    }
   }
   for (int64_t k : {100000ll, 227000ll, 671088ll}) {
     std::vector<int> h(k);
