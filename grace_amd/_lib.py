@@ -101,6 +101,7 @@ SIGNATURES = {
     "grace_threshold_write": (ST, [P, I64, P, P, P, P]),
     "grace_powersgd_p": (ST, [P, I64, I64, P, I32, P, P, P]),
     "grace_powersgd_workspace_bytes": (SZ, [I64, I64, I32]),
+    "grace_powersgd_p_draw": (ST, [P, I64, I64, U64, I32, P, P, P]),
     "grace_powersgd_qt": (ST, [P, I64, I64, P, I32, P, P, P]),
     "grace_orthogonalize": (ST, [P, I64, I32, P]),
     "grace_normal_orthogonal": (ST, [P, I64, I32, U64, P]),
@@ -149,6 +150,20 @@ def call(name, *args):
         msg = load().grace_last_error()
         raise GraceNativeError(f"{name} failed ({st}): {msg.decode() if msg else ''}")
     return st
+
+
+def fn(name):
+    """The resolved ctypes function (for launch-bound callers that check the status themselves)."""
+    f = _fns.get(name)
+    if f is None:
+        f = _fns[name] = getattr(load(), name)
+    return f
+
+
+def check(name, st):
+    if st != 0:
+        msg = load().grace_last_error()
+        raise GraceNativeError(f"{name} failed ({st}): {msg.decode() if msg else ''}")
 
 
 def query(name, *args):

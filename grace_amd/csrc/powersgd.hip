@@ -128,6 +128,26 @@ __device__ __forceinline__ bool last_arrival(uint32_t* ticket, uint32_t expected
   return s_last != 0;
 }
 
+// standard normal draws: Box-Muller on the counter-based generator, one (cos, sin) pair per two
+// consecutive elements; element e is component e & 1 of pair e >> 1 (normal_kernel, the generic and
+// the rank-4 fused draws all produce the same stream)
+__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t pair, float& z0, float& z1) {
+  const uint64_t h = mix64(seed ^ mix64(pair * 2 + 1));
+  const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);   // (0, 1]
+  const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
+  // hardware transcendentals (v_log_f32 = log2, v_sin/v_cos_f32 take revolutions, v_sqrt_f32):
+  // a few ulp, irrelevant for a random draw, and ~5x fewer instructions than the correctly
+  // rounded libm calls -- the fused draw runs on one workgroup, so they were 4 us of its 9
+  const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));   // -2 ln 2 log2(u1)
+  z0 = rad * __builtin_amdgcn_cosf(u2);
+  z1 = rad * __builtin_amdgcn_sinf(u2);
+}
+__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t i) {
+  float z0, z1;
+  normal_pair(seed, i >> 1, z0, z1);
+  return (i & 1) ? z1 : z0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Both contractions stream M through LDS in tiles of 16 rows x 256·CPL columns: every global load
 // is one row's 1 KB contiguous run (64 lanes x 16 B) and a lane's CPL loads of a row
@@ -227,6 +247,29 @@ __device__ __forceinline__ void fac_load_r4(const float* __restrict__ F, int64_t
     pre[c] = row < rhi ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
   }
 }
+// the same rows of a fresh standard-normal [rows x 4] factor, drawn instead of loaded: entry
+// (row, c) = element row * 4 + c of the normal_kernel stream, i.e. Box-Muller pairs 2 row, 2 row + 1
+template <int CPL>
+__device__ __forceinline__ void fac_draw_r4(uint64_t seed, int64_t row0, int64_t rhi, f32x4v (&pre)[CPL]) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int64_t row = row0 + threadIdx.x + 256 * c;
+    float z0, z1, z2, z3;
+    normal_pair(seed, (uint64_t)row * 2, z0, z1);
+    normal_pair(seed, (uint64_t)row * 2 + 1, z2, z3);
+    pre[c] = row < rhi ? f32x4v{z0, z1, z2, z3} : f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+}
+template <int PER>
+__device__ __forceinline__ void fac_draw(uint64_t seed, int r, int64_t row0, int64_t rhi, int cnt, float (&pre)[PER]) {
+  const int64_t total = (int64_t)cnt * r;
+  const int64_t lim = (rhi - row0) * r;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int64_t e = threadIdx.x + (int64_t)j * kPBlockT;
+    pre[j] = (e < total && e < lim) ? normal_at(seed, (uint64_t)(row0 * r + e)) : 0.f;
+  }
+}
 constexpr int kPPer = kTileR * kMaxRank / kPBlockT;   // 1: P rows of one row tile
 
 // ------------------------------------------------------------------------------------------------
@@ -237,11 +280,13 @@ constexpr int kPPer = kTileR * kMaxRank / kPBlockT;   // 1: P rows of one row ti
 // instead of being serialised behind in-loop loads.  The 4 waves and the K chunks are reduced
 // deterministically (LDS, then the last workgroup of the row tile).  R4: q staged as 16-B rows,
 // wide tiles; otherwise one 1-KB run per row and flat scalar q staging.
-template <bool VEC, bool R4>
+// DRAWQ: q is not read but drawn on the fly (standard normal, counter-based, keyed by `seed`; the
+// same values grace_normal_fill writes), so PowerSGD's fresh q needs no buffer and no launch.
+template <bool VEC, bool R4, bool DRAWQ = false>
 __global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_p_kernel(const float* __restrict__ M, int64_t n, int64_t m,
                                                          const float* __restrict__ q, int r,
                                                          float* __restrict__ P, float* __restrict__ part,
-                                                         uint32_t* __restrict__ tickets) {
+                                                         uint32_t* __restrict__ tickets, uint64_t seed = 0) {
   constexpr int CPL = R4 ? kCPL : 1;
   constexpr int TC = Tile<CPL>::C;
   constexpr int QPER = TC * kMaxRank / kPBlockT;
@@ -261,10 +306,18 @@ __global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_p_kernel(const float* __
   f32x4v pre[4 * CPL];
   float qpre[R4 ? 1 : QPER];
   f32x4v q4[CPL];
+  auto q_tile = [&](int64_t row0) {
+    if constexpr (R4) {
+      if constexpr (DRAWQ) fac_draw_r4<CPL>(seed, row0, m, q4);
+      else fac_load_r4<CPL>(q, row0, m, q4);
+    } else {
+      if constexpr (DRAWQ) fac_draw(seed, r, row0, m, TC, qpre);
+      else fac_load(q, r, row0, m, TC, qpre);
+    }
+  };
   if (kt0 < kt1) {
     tile_load<CPL, VEC>(M, n, m, i0, i0 + kTileR, i0, kt0 * TC, pre);
-    if constexpr (R4) fac_load_r4<CPL>(q, kt0 * TC, m, q4);
-    else fac_load(q, r, kt0 * TC, m, TC, qpre);
+    q_tile(kt0 * TC);
   }
   for (int64_t kt = kt0; kt < kt1; ++kt) {
     tile_store<CPL>(tile, pre);
@@ -277,8 +330,7 @@ __global__ __launch_bounds__(kPBlockT) PS_OCC void psgd_p_kernel(const float* __
     __syncthreads();
     if (kt + 1 < kt1) {
       tile_load<CPL, VEC>(M, n, m, i0, i0 + kTileR, i0, (kt + 1) * TC, pre);
-      if constexpr (R4) fac_load_r4<CPL>(q, (kt + 1) * TC, m, q4);
-      else fac_load(q, r, (kt + 1) * TC, m, TC, qpre);
+      q_tile((kt + 1) * TC);
     }
 #pragma unroll
     for (int st = 0; st < 4 * CPL; ++st) {
@@ -693,26 +745,6 @@ __device__ void orth_mgs2(float* __restrict__ A, int64_t n, int r) {
     for (int64_t i = threadIdx.x; i < n; i += kOrthBlock) A[i * r + c] = (float)((double)A[i * r + c] * inv);
     __syncthreads();
   }
-}
-
-// standard normal draws: Box-Muller on the counter-based generator, one (cos, sin) pair per two
-// consecutive elements; element e is component e & 1 of pair e >> 1 (normal_kernel, the generic and
-// the rank-4 fused draws all produce the same stream)
-__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t pair, float& z0, float& z1) {
-  const uint64_t h = mix64(seed ^ mix64(pair * 2 + 1));
-  const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);   // (0, 1]
-  const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
-  // hardware transcendentals (v_log_f32 = log2, v_sin/v_cos_f32 take revolutions, v_sqrt_f32):
-  // a few ulp, irrelevant for a random draw, and ~5x fewer instructions than the correctly
-  // rounded libm calls -- the fused draw runs on one workgroup, so they were 4 us of its 9
-  const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));   // -2 ln 2 log2(u1)
-  z0 = rad * __builtin_amdgcn_cosf(u2);
-  z1 = rad * __builtin_amdgcn_sinf(u2);
-}
-__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t i) {
-  float z0, z1;
-  normal_pair(seed, i >> 1, z0, z1);
-  return (i & 1) ? z1 : z0;
 }
 
 // R = r rounded up to a power of two (the Gram accumulators live in registers: R(R+1)/2 doubles).
@@ -1144,10 +1176,9 @@ size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r) {
   return kTicketBytes + align256(pp > qp ? pp : qp);
 }
 
-grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
-                                void* ws, void* stream) {
-  GRACE_REQUIRE(M && q && P && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
-                "grace_powersgd_p: bad arguments");
+extern "C++" template <bool DRAWQ>
+static grace_status_t launch_p(const float* M, int64_t n, int64_t m, const float* q, uint64_t seed, int32_t r,
+                               float* P, void* ws, hipStream_t st) {
   const bool vec = (m % 4 == 0) && ((reinterpret_cast<uintptr_t>(M) & 15u) == 0);
   const bool r4 = r == 4 &&
                   ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(ws)) & 15u) == 0 &&
@@ -1155,11 +1186,25 @@ grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const floa
   const dim3 grid((unsigned)p_ksplit(n, m, vec && r4 ? Tile<kCPL>::C : Tile<1>::C), (unsigned)((n + kTileR - 1) / kTileR));
   uint32_t* tickets = reinterpret_cast<uint32_t*>(ws);
   float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kTicketBytes);
-  if (vec && r4) psgd_p_kernel<true, true><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
-  else if (vec) psgd_p_kernel<true, false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
-  else psgd_p_kernel<false, false><<<grid, kPBlockT, 0, as_stream(stream)>>>(M, n, m, q, r, P, part, tickets);
+  if (vec && r4) psgd_p_kernel<true, true, DRAWQ><<<grid, kPBlockT, 0, st>>>(M, n, m, q, r, P, part, tickets, seed);
+  else if (vec) psgd_p_kernel<true, false, DRAWQ><<<grid, kPBlockT, 0, st>>>(M, n, m, q, r, P, part, tickets, seed);
+  else psgd_p_kernel<false, false, DRAWQ><<<grid, kPBlockT, 0, st>>>(M, n, m, q, r, P, part, tickets, seed);
   GRACE_CHECK_LAUNCH("grace_powersgd_p");
   return GRACE_OK;
+}
+
+grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
+                                void* ws, void* stream) {
+  GRACE_REQUIRE(M && q && P && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
+                "grace_powersgd_p: bad arguments");
+  return launch_p<false>(M, n, m, q, 0, r, P, ws, as_stream(stream));
+}
+
+grace_status_t grace_powersgd_p_draw(const float* M, int64_t n, int64_t m, uint64_t seed, int32_t r, float* P,
+                                     void* ws, void* stream) {
+  GRACE_REQUIRE(M && P && ws && n >= 1 && m >= 1 && r >= 1 && r <= kMaxRank,
+                "grace_powersgd_p_draw: bad arguments");
+  return launch_p<true>(M, n, m, nullptr, seed, r, P, ws, as_stream(stream));
 }
 
 grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const float* P, int32_t r, float* Q,

@@ -44,14 +44,18 @@ class PowerSGDCompressor(Compressor):
         n, m = matrix.size()
         r = min(n, m, self.rank)
         if self.use_memory and name in self.q_memory:
-            q = self.q_memory[name]
+            p = ops.powersgd_p(matrix, self.q_memory[name])
         elif self.rng == "torch_cpu":
             q = self._normal(m, r, matrix.device, name)
             orthogonalize(q)
-        else:   # device draw + orthogonalisation fused in one launch
+            p = ops.powersgd_p(matrix, q)
+        else:
+            # device draw inside the contraction.  The fresh q is not orthogonalised first: with
+            # q = q0 R^-1 (q0's own QR), orthogonalize(M q) = orthogonalize(M q0) because R^-1 is
+            # upper triangular with a positive diagonal, so P after the orthogonalisation below is
+            # the reference's (powersgd.py:40-49) up to rounding -- one launch and q's buffer saved
             self._step += 1
-            q = ops.normal_orthogonal((m, r), ops.step_seed("powersgd-q", name, self._step), matrix.device)
-        p = ops.powersgd_p(matrix, q)
+            p = ops.powersgd_p_draw(matrix, r, ops.step_seed("powersgd-q", name, self._step))
         if self.world_size > 1 or (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
             dist.all_reduce(p)
         if self.world_size != 1:

@@ -50,9 +50,18 @@ class SignSGDCompressor(Compressor):
         return ops.sign_majority(codes, world_size, n).view(shape)
 
     def fused_step(self, communicator, tensor, name):
-        if (isinstance(communicator, Allgather) and type(communicator.memory) is NoneMemory
-                and int(communicator.world_size) == 1 and isinstance(tensor, torch.Tensor)
-                and tensor.is_cuda and tensor.dtype == torch.float32):
+        """World-1 Allgather(SignSGD, NoneMemory).step as ONE launch: sign encode -> decode ->
+        majority of one = +-1 (signsgd.py:12-30).  A 4 MiB step is launch-bound (the kernel is
+        ~1.5 us of HBM time), so this path keeps the host work to one checked ctypes launch."""
+        if not (communicator.__class__ is Allgather and communicator.memory.__class__ is NoneMemory
+                and communicator.world_size == 1):
+            return None
+        if not (tensor.__class__ is torch.Tensor and tensor.is_cuda and tensor.dtype == torch.float32
+                and tensor.is_contiguous()):
+            if not (isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
+                return None
             _, out = ops.sign_step_w1(tensor, want_codes=False, reuse_out=True)
-            return out if out.shape == tensor.shape else out.view(tensor.shape)
-        return None
+            return out.view(tensor.shape)
+        out = ops.reusable_output("sign_w1", tensor.shape, torch.float32, tensor.device)
+        ops.launch_sign_step_w1(tensor, out)
+        return out

@@ -20,10 +20,13 @@ class GraceDeviceError(TypeError):
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
+_current_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
     """The current HIP stream of the current device, as a raw pointer (no Stream object)."""
-    if _raw_stream is not None:
-        return _raw_stream(torch.cuda.current_device())
+    if _raw_stream is not None and _current_device is not None:
+        return _raw_stream(_current_device())
     return torch.cuda.current_stream().cuda_stream
 
 
@@ -65,6 +68,21 @@ def workspace(slot, nbytes, device):
 
 
 _reuse = {}
+_getrefcount = __import__("sys").getrefcount
+
+
+_sign_w1 = None
+
+
+def launch_sign_step_w1(x, out):
+    """grace_sign_step_w1 on a contiguous f32 device tensor into `out`: the launch-bound W=1 path."""
+    global _sign_w1
+    f = _sign_w1
+    if f is None:
+        f = _sign_w1 = _lib.fn("grace_sign_step_w1")
+    st = f(x.data_ptr(), None, out.data_ptr(), x.numel(), _stream())
+    if st:
+        _lib.check("grace_sign_step_w1", st)
 
 
 def reusable_output(slot, shape, dtype, device):
@@ -74,10 +92,9 @@ def reusable_output(slot, shape, dtype, device):
     caller that keeps its results gets a fresh tensor each call, exactly as the reference's new
     allocations; one that consumes and drops them (``grad.copy_(grc.step(grad, name))``,
     examples/dist/CIFAR10-dawndist/core.py:204-206) skips the allocator on launch-bound steps."""
-    import sys
-    key = (slot, tuple(shape), dtype, str(device), _stream())
+    key = (slot, shape, dtype, device, _stream())
     buf = _reuse.get(key)
-    if buf is not None and sys.getrefcount(buf) == 3:
+    if buf is not None and _getrefcount(buf) == 3:
         return buf
     buf = torch.empty(shape, dtype=dtype, device=device)
     _reuse[key] = buf
@@ -531,6 +548,15 @@ def powersgd_p(M2d, q):
     P = torch.empty(n, r, dtype=F32, device=M2d.device)
     ws = workspace("powersgd", _lib.query("grace_powersgd_workspace_bytes", n, m, r), M2d.device)
     _lib.call("grace_powersgd_p", _p(M2d), n, m, _p(require_dev(q)), r, _p(P), _p(ws), _stream())
+    return P
+
+
+def powersgd_p_draw(M2d, r, seed):
+    """P = M q with q = ops.normal((m, r), seed), drawn inside the contraction (no q buffer)."""
+    n, m = M2d.shape
+    P = torch.empty(n, r, dtype=F32, device=M2d.device)
+    ws = workspace("powersgd", _lib.query("grace_powersgd_workspace_bytes", n, m, r), M2d.device)
+    _lib.call("grace_powersgd_p_draw", _p(M2d), n, m, int(seed) & (2 ** 64 - 1), int(r), _p(P), _p(ws), _stream())
     return P
 
 

@@ -236,6 +236,13 @@ grace_status_t grace_threshold_write_i64(const float* x, int64_t n, const void* 
 grace_status_t grace_powersgd_p(const float* M, int64_t n, int64_t m, const float* q, int32_t r, float* P,
                                 void* ws, void* stream);
 size_t grace_powersgd_workspace_bytes(int64_t n, int64_t m, int32_t r);
+/* P = M q with q = standard normal draws keyed by `seed` (the grace_normal_fill stream of an [m x r]
+ * tensor), drawn inside the contraction: no q buffer, no draw launch.  PowerSGD's fresh q
+ * (powersgd.py:41-43) is orthogonalised before P = M q; since orthogonalize(M q R^-1) =
+ * orthogonalize(M q) for the upper-triangular R of q's own QR, orthogonalize(P) is the same
+ * either way, so the caller orthogonalises P only. */
+grace_status_t grace_powersgd_p_draw(const float* M, int64_t n, int64_t m, uint64_t seed, int32_t r, float* P,
+                                     void* ws, void* stream);
 grace_status_t grace_powersgd_qt(const float* M, int64_t n, int64_t m, const float* P, int32_t r, float* Q,
                                  void* ws, void* stream);
 grace_status_t grace_orthogonalize(float* A, int64_t n, int32_t r, void* stream);

@@ -192,3 +192,27 @@ def test_orthogonalize_shapes_and_fused_draw(n, r):
     ref = _np(ops.orthogonalize_(ops.normal((n, r), 77, "cuda")))
     assert np.allclose(fused, ref, rtol=1e-5, atol=1e-6)
     assert np.allclose(fused.T.astype(np.float64) @ fused, np.eye(r), atol=1e-4)
+
+
+@pytest.mark.parametrize("shape,r", [((4096, 4096), 4), ((256, 300), 4), ((100, 1000), 2), ((64, 48), 1), ((33, 17), 3)])
+def test_p_with_q_drawn_in_the_contraction(shape, r):
+    """grace_powersgd_p_draw == M @ normal((m, r), seed) (the grace_normal_fill stream), and the
+    compressor's device path equals the reference's algorithm on that draw: orthogonalize(M q) with
+    q = orthogonalize(draw) (powersgd.py:40-52) -- the same P, Q because orthogonalising q first only
+    right-multiplies M q by an upper-triangular matrix."""
+    from grace_amd.dist.compressor.powersgd import PowerSGDCompressor
+    rng = np.random.default_rng(shape[0] * r)
+    M = rng.standard_normal(shape).astype(np.float32)
+    n, m = shape
+    seed = 4242
+    q0 = _np(ops.normal((m, r), seed, DEV))
+    P = _np(ops.powersgd_p_draw(_t(M), r, seed))
+    Pe = M.astype(np.float64) @ q0.astype(np.float64)
+    assert _close(P, Pe, m)
+    comp = PowerSGDCompressor(rank=r)
+    payload, (p, q, shp) = comp.compress(_t(M), "w")
+    seed_used = ops.step_seed("powersgd-q", "w", 1)
+    q0 = _np(ops.normal((m, min(n, m, r)), seed_used, DEV))
+    p_or, q_or = O.powersgd_compress(M, O.orthogonalize(q0))
+    assert _close(_np(p), p_or, m, scale=1.0)
+    assert _close(_np(q), q_or, m)
