@@ -20,9 +20,10 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   topk_sharded  ONE 256 MiB bucket sharded over the N ranks, top-k 0.1 % + residual, exact global
              selection (histogram exchange + boundary lists + payload allgather), replicated dense
              decode (configs[4]); value = 4n / step time (strong scaling: the bucket is fixed)
-  ddp_params / ddp_bucket  the DDP loopback harness (grace_amd/harness.py) on ResNet-50's 161
-             gradient tensors, top-k 1 % + residual: per-parameter grc.step loop
-             (examples/dist/CIFAR10-dawndist/core.py:204-208) vs one flat bucket
+  ddp_params / ddp_segmented / ddp_bucket  the DDP loopback harness (grace_amd/harness.py) on
+             ResNet-50's 161 gradient tensors, top-k 1 % + residual: the per-parameter grc.step loop
+             (examples/dist/CIFAR10-dawndist/core.py:204-208), the same per-tensor semantics in one
+             launch sequence (SegmentedTopK), and one flat bucket with a single global top-k
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
 
 Launch: ``python bench.py`` (N=1) or
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
                     choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd",
-                             "ddp_params", "ddp_bucket"])
+                             "ddp_params", "ddp_bucket", "ddp_segmented"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -118,7 +119,7 @@ def main():
         else:
             dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
-           "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+           "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
     line = run(args, world, rank, dev)
     if args.workload == "topk" and world > 1 and not args.no_sharded:
@@ -131,6 +132,20 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(workload, alg_bytes):
+    """HBM bytes per step of a secondary workload's kernels from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (tools/prof_r02.sh -> tools/pmc_all.py), with the ratio to the algorithmic
+    bytes; None when that workload was not profiled."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_secondary.json")
+    try:
+        with open(path) as f:
+            wl = json.load(f)["workloads"][workload]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    t = wl["hbm_bytes_per_step"]
+    return t, round(t / alg_bytes, 3)
 
 
 def base_line(args, world, elapsed, nbytes_per_rank, metric=METRIC):
@@ -290,7 +305,8 @@ def bench_topk_sharded(args, world, rank, dev):
 
 def bench_ddp(args, world, rank, dev):
     from grace_amd.dist.helper import grace_from_params
-    from grace_amd.harness import GradBucket, ShapeModel, step_bucketed, step_parameters
+    from grace_amd.dist.segmented import SegmentedTopK
+    from grace_amd.harness import GradBucket, ShapeModel, step_bucketed, step_parameters, step_segmented
     model = ShapeModel(resnet50_shapes(), dev)
     bucket = GradBucket(model)
     grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
@@ -298,6 +314,9 @@ def bench_ddp(args, world, rank, dev):
     bucket.flat.normal_()
     if args.workload == "ddp_params":
         fn = lambda i: step_parameters(model, grc)   # noqa: E731
+    elif args.workload == "ddp_segmented":
+        eng = SegmentedTopK(0.01, world_size=world)
+        fn = lambda i: step_segmented(bucket, eng)   # noqa: E731
     else:
         fn = lambda i: step_bucketed(bucket, grc)    # noqa: E731
     fn(0)
@@ -305,8 +324,10 @@ def bench_ddp(args, world, rank, dev):
     total = bucket.flat.numel()
     line = base_line(args, world, elapsed, 4.0 * total,
                      metric=f"grad-codec GB/s, ResNet-50 gradients through the DDP loopback harness ({args.workload})")
-    line["config"] = {"workload": f"{'per-parameter grc.step loop' if args.workload == 'ddp_params' else 'one flat bucket'}"
-                                  f", Allgather(TopK 1 %, Residual), 161 ResNet-50 tensors", "numel": total,
+    kind = {"ddp_params": "per-parameter grc.step loop (core.py:204-208)",
+            "ddp_segmented": "per-tensor k and residual, all tensors in one launch sequence (SegmentedTopK)",
+            "ddp_bucket": "one flat bucket, ONE global top-k (a different algorithm)"}[args.workload]
+    line["config"] = {"workload": f"{kind}, Allgather(TopK 1 %, Residual), 161 ResNet-50 tensors", "numel": total,
                       "tensors": len(bucket.params)}
     line["roofline"] = None
     return line
@@ -332,9 +353,12 @@ def bench_sign(args, world, rank, dev):
     line["config"] = {"workload": f"Allgather(SignSGD, NoneMemory).step, {4 * n >> 20} MiB fp32", "numel": n,
                       "rotated_buffers": nbuf}
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic(args.workload, 10.0 * n)
     line["roofline"] = {"bound": "hbm", "achieved": round(10.0 * n / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(10.0 * n / t / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "note": "10n algorithmic bytes per step (SURVEY.md §8d config 1)"}
+                        "traffic": traffic, "traffic_over_algorithmic": ratio,
+                        "note": "10n algorithmic bytes per step (SURVEY.md §8d config 1); the world-1 fused step "
+                                "never materialises the u8 codes, so it moves 8n"}
     return line
 
 
@@ -365,9 +389,10 @@ def bench_quant(args, world, rank, dev):
                      metric=f"grad-codec GB/s (device-resident encode+decode), ResNet-50 set {args.workload}")
     line["config"] = {"workload": f"{args.workload} compress+decompress, 161 ResNet-50 tensors in one segmented "
                                   "launch per stage (BASELINE configs[2])", "numel": total, "tensors": len(sizes)}
+    traffic, ratio = pmc_traffic(args.workload, alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes_per_step": alg}
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
     return line
 
 
@@ -388,8 +413,10 @@ def bench_powersgd(args, world, rank, dev):
                      metric="grad-codec GB/s (device-resident encode+decode), PowerSGD rank 4, 4096x4096")
     line["config"] = {"workload": "Allreduce(PowerSGD rank 4, NoneMemory).step, 4096x4096 fp32 (BASELINE configs[3])",
                       "numel": n * m, "rank": r}
+    traffic, ratio = pmc_traffic("powersgd", 12.0 * n * m)
     line["roofline"] = {"bound": "hbm", "achieved": round(12 * n * m / t / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio,
                         "mfma_tflops": round(flops / t / 1e12, 3),
                         "mfma_util": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 5),
                         "note": "12n algorithmic bytes, 6nmr flops (SURVEY.md §8d config 4; AI = 2 flop/B)"}

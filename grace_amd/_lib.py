@@ -42,6 +42,9 @@ SIGNATURES = {
     "grace_topk_workspace_bytes": (SZ, [I64, I64]),
     "grace_topk_compress": (ST, [P, I64, I64, P, P, P, SZ, P]),
     "grace_topk_residual_step": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, SZ, P]),
+    "grace_topk_segmented_workspace_bytes": (SZ, [I64, I32]),
+    "grace_topk_segmented_chunk": (I32, []),
+    "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]),
     "grace_topk_shard_xs_words": (SZ, []),
     "grace_topk_shard_xh_words": (SZ, []),
     "grace_topk_shard_sample": (ST, [P, P, I32, F32, F32, I64, I64, P, P]),

@@ -35,6 +35,7 @@
 #include <hip/hip_ext.h>
 
 #include "common.h"
+#include "select.h"
 
 namespace grace {
 
@@ -178,128 +179,6 @@ static void launch_timed(void (*kern)(KArgs...), dim3 grid, dim3 block, hipStrea
 }
 
 // ------------------------------------------------------------------------------------------------
-// block-wide exclusive scan of one uint32 per thread (BLOCK threads, wave64)
-template <int BLOCK>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
-  constexpr int NW = BLOCK / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
-  if (lane == 63) s_w[w] = inc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < NW; ++i) {
-      uint32_t t = s_w[i];
-      s_w[i] = acc;
-      acc += t;
-    }
-    s_w[NW] = acc;
-  }
-  __syncthreads();
-  const uint32_t r = s_w[w] + inc - v;
-  if (total) *total = s_w[NW];
-  __syncthreads();
-  return r;
-}
-
-// Given a histogram hist[NBINS] (in LDS or global) find, scanning from the top, the bin d where
-// the running count reaches `rank` (1-based): sum_{b>d} < rank <= sum_{b>=d}, for NR ranks at
-// once (one block scan).  Returns d[q] and above[q] = sum_{b>d[q]}.  All BLOCK threads must call;
-// NBINS % BLOCK == 0; s_res needs 2*NR words.
-template <int BLOCK, int NBINS, int NR>
-__device__ void find_bins_desc(const uint32_t* hist, const uint32_t (&rank)[NR], uint32_t* s_w,
-                               uint32_t* s_res, int (&d)[NR], uint32_t (&above)[NR]) {
-  constexpr int PER = NBINS / BLOCK;
-  const int t = threadIdx.x;
-  const int top = NBINS - 1 - t * PER;  // this thread covers bins top, top-1, ..., top-PER+1
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) s += hist[top - j];
-  if (t < 2 * NR) s_res[t] = 0;
-  const uint32_t ex = block_excl_scan<BLOCK>(s, s_w, nullptr);
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    if (ex < rank[q] && rank[q] <= ex + s) {
-      uint32_t acc = ex;
-      for (int j = 0; j < PER; ++j) {
-        const uint32_t h = hist[top - j];
-        if (acc + h >= rank[q]) {
-          s_res[2 * q] = (uint32_t)(top - j);
-          s_res[2 * q + 1] = acc;
-          break;
-        }
-        acc += h;
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    d[q] = (int)s_res[2 * q];
-    above[q] = s_res[2 * q + 1];
-  }
-  __syncthreads();
-}
-
-template <int BLOCK, int NBINS>
-__device__ int find_bin_desc(const uint32_t* hist, uint32_t rank, uint32_t* s_w, uint32_t* s_res,
-                             uint32_t* above_out) {
-  const uint32_t r[1] = {rank};
-  int d[1];
-  uint32_t ab[1];
-  find_bins_desc<BLOCK, NBINS, 1>(hist, r, s_w, s_res, d, ab);
-  if (above_out) *above_out = ab[0];
-  return d[0];
-}
-
-// composite selection key: larger |t| first, then lower index first; unique per element
-__device__ __forceinline__ uint64_t comp_key(uint32_t key, uint32_t idx) {
-  return ((uint64_t)key << 32) | (uint64_t)(0xFFFFFFFFu - idx);
-}
-
-// Boundary-list entries cross workgroups (and XCDs, whose L2s are not coherent with each other):
-// they are written with agent-scope (sc1, write-through) stores and read back with agent-scope
-// loads, so the arrival protocol needs no L2 writeback / invalidate fences.
-__device__ __forceinline__ void st_agent_i2(int2* p, int2 v) {
-  const uint64_t u = (uint64_t)(uint32_t)v.x | ((uint64_t)(uint32_t)v.y << 32);
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int2 ld_agent_i2(const int2* p) {
-  const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return make_int2((int)(uint32_t)u, (int)(uint32_t)(u >> 32));
-}
-
-// Exact single-workgroup radix select: returns T such that exactly `need` items of src have
-// composite >= T (composites are unique).  6 passes of 11/11/11/11/11/9 bits.
-template <int BLOCK = kSelBlock, typename Src>
-__device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, uint32_t* hist,
-                                      uint32_t* s_w, uint32_t* s_res) {
-  uint64_t prefix = 0, pmask = 0;
-  uint32_t rem = need;
-  for (int p = 0; p < 6; ++p) {
-    const int shift = p < 5 ? 53 - 11 * p : 0;
-    const uint32_t dmask = p < 5 ? 2047u : 511u;
-    for (int b = threadIdx.x; b < 2048; b += BLOCK) hist[b] = 0;
-    __syncthreads();
-    for (int64_t j = threadIdx.x; j < N; j += BLOCK) {
-      const uint64_t c = src(j);
-      if ((c & pmask) == prefix) atomicAdd(&hist[(c >> shift) & dmask], 1u);
-    }
-    __syncthreads();
-    uint32_t above;
-    const int d = find_bin_desc<BLOCK, 2048>(hist, rem, s_w, s_res, &above);
-    rem -= above;
-    prefix |= (uint64_t)d << shift;
-    pmask |= (uint64_t)dmask << shift;
-  }
-  return prefix;
-}
-
 // ------------------------------------------------------------------------------------------------
 // Streaming accesses of the bucket are non-temporal (touched once per step): on gfx950 the
 // nt 16-B loads+stores lift the 2-read/2-write stream from ~5.1 to ~6.4 TB/s (tools/hbm_probe).

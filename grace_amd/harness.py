@@ -2,12 +2,13 @@
 examples/dist/CIFAR10-dawndist/core.py:195-209 -- after backward, every parameter's gradient goes
 through ``grc.step(grad, name)`` and is copied back before the optimizer step.
 
-``step_parameters(model, grc)`` is that loop verbatim.  ``step_bucketed(model, grc)`` is the
-MI355X-friendly alternative: all gradients are viewed as ONE flat bucket (allocated once, the
-parameters' .grad tensors become views into it), so a step is one codec launch sequence and one
-collective instead of one per parameter -- at ResNet-50's 161 tensors the per-parameter loop is
-launch-bound (most tensors are a few KB).  Both run the same compressors / memories /
-communicators (grace_amd.dist)."""
+``step_parameters(model, grc)`` is that loop verbatim.  All gradients can also be viewed as ONE
+flat bucket (GradBucket: allocated once, the parameters' .grad tensors become views into it):
+  * ``step_segmented(bucket, engine)`` keeps the loop's semantics -- per-tensor k_i and residual --
+    in one launch sequence for all tensors (grace_amd.dist.segmented.SegmentedTopK);
+  * ``step_bucketed(bucket, grc)`` runs ONE grc.step over the concatenation, i.e. a single global
+    top-k: a different algorithm (one k for the whole model), listed for comparison.
+At ResNet-50's 161 tensors the per-parameter loop is launch-bound (most tensors are a few KB)."""
 import torch
 
 
@@ -34,6 +35,14 @@ class GradBucket:
             p.grad = self.flat[off:off + n].view_as(p)
             off += n
         self.params = params
+        self.sizes = [p.numel() for p in params]
+
+
+def step_segmented(bucket, engine, name="bucket"):
+    """The per-parameter loop's semantics (every tensor its own k_i and residual) for all tensors in
+    one launch sequence: grace_amd.dist.segmented.SegmentedTopK over the bucket's segments, the
+    result written back into the .grad views in place."""
+    engine.step(bucket.flat, bucket.sizes, name, out=bucket.flat)
 
 
 def step_bucketed(bucket, grc, name="bucket"):

@@ -200,6 +200,22 @@ grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, in
 grace_status_t grace_fp16_compress(const float* x, void* half_out, int64_t n, void* stream);
 grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n, void* stream);
 
+/* Per-tensor top-k + residual over many tensors in one launch sequence (grace_amd/csrc/segtopk.hip):
+ * the reference's per-parameter DDP loop (examples/dist/CIFAR10-dawndist/core.py:203-206, one
+ * TopKCompressor(ratio) + ResidualMemory step per tensor, k_i = max(1, int(n_i * ratio)),
+ * grace_dl/dist/compressor/topk.py:34).  The tensors are segments of one flat buffer; device tables:
+ * seg_off[nseg + 1] (elements), k_off[nseg + 1] (payload), chk_off[nseg + 1] (chunks of
+ * grace_topk_segmented_chunk() elements, per segment), chunk_seg[nchunks].  Payload
+ * (vals f32, idx i32 GLOBAL indices)[k_off[nseg]]; out (dense world-1 result, may alias g) or NULL.
+ * The workspace is zeroed once; keep one per segment table (its layout depends on nseg). */
+size_t grace_topk_segmented_workspace_bytes(int64_t n_total, int32_t nseg);
+int32_t grace_topk_segmented_chunk(void);
+grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_t has_residual, float beta,
+                                         float gamma, const int64_t* seg_off, const int64_t* k_off,
+                                         const int64_t* chk_off, const int32_t* chunk_seg, int32_t nseg,
+                                         int64_t n_total, int64_t nchunks, float* vals, int32_t* idx, float* out,
+                                         void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------- random-k / threshold */
 /* Random-k indices (randomk.py:11: randint(numel, [k]), WITH replacement) from a counter-based
  * device generator keyed by the reference's seed sum(bytes(name)) + step: identical on every

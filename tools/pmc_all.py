@@ -1,0 +1,61 @@
+"""Per-step HBM traffic of a workload's grace kernels from two separate rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE), with MI355X_MICROARCH.md's gfx950 corrections: FETCH_SIZE is in KB and a
+wide (16-B per lane) streaming read is tallied at half its bytes (x2); WRITE_SIZE is in KB and
+exact for 16-B-per-lane stores.  Other access widths (the codecs' 4-B code stores, 8-B loads) are
+uncalibrated, so the per-kernel figures are reported raw-corrected and flagged.
+usage: python tools/pmc_all.py OUT_JSON WORKLOAD=FETCH_DIR,WRITE_DIR [...]"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(d):
+    """{kernel: [per-dispatch counter totals]} for the grace:: kernels of one pass."""
+    disp = collections.defaultdict(float)
+    name = {}
+    path = None
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                path = os.path.join(root, f)
+    if path is None:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = r["Kernel_Name"]
+            if "grace::" not in k:
+                continue
+            disp[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            name[r["Dispatch_Id"]] = k.split("(")[0].replace("void ", "")
+    out = collections.defaultdict(list)
+    for did, v in disp.items():
+        out[name[did]].append(v)
+    return out
+
+
+def main():
+    res = {"correction": "FETCH_SIZE KB x1024 x2 (gfx950 16-B streaming reads), WRITE_SIZE KB x1024",
+           "workloads": {}}
+    for arg in sys.argv[2:]:
+        wl, dirs = arg.split("=", 1)
+        fdir, wdir = dirs.split(",")
+        fk, wk = per_kernel(fdir), per_kernel(wdir)
+        kern = {}
+        step = 0.0
+        for k in sorted(set(fk) | set(wk)):
+            f = sum(fk.get(k, [0])) / max(len(fk.get(k, [])), 1) * 1024 * 2
+            w = sum(wk.get(k, [0])) / max(len(wk.get(k, [])), 1) * 1024
+            kern[k] = {"launches": [len(fk.get(k, [])), len(wk.get(k, []))], "fetch_bytes": round(f),
+                       "write_bytes": round(w), "hbm_bytes": round(f + w)}
+            step += f + w
+        res["workloads"][wl] = {"kernels": kern, "hbm_bytes_per_step": round(step),
+                                "source": [fdir, wdir]}
+    with open(sys.argv[1], "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({w: v["hbm_bytes_per_step"] for w, v in res["workloads"].items()}))
+
+
+if __name__ == "__main__":
+    main()
