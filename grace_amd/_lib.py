@@ -86,6 +86,8 @@ SIGNATURES = {
     "grace_randomk_perm_indices": (ST, [U64, I64, I64, P, P]),
     "grace_widen_i32": (ST, [P, I64, P, P]),
     "grace_threshold_count_fixed": (ST, [P, I64, F32, P, P]),
+    "grace_threshold_count_dev": (ST, [P, I64, F32, P, P]),
+    "grace_sparse_sub": (ST, [P, P, I64, P, P]),
     "grace_threshold_write_i64": (ST, [P, I64, P, P, P, P]),
     "grace_terngrad_unit": (I32, []),
     "grace_terngrad_workspace_bytes": (SZ, [I64]),

@@ -171,6 +171,56 @@ __global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ p
   }
 }
 
+// device-side recount (the host-free variant): only when pass 2 flagged max(x) < thr, count again at
+// the bound it chose; the bound kernel then runs as the final pass and clears the flag
+__global__ __launch_bounds__(kSBlock) void thr_restats_kernel(const float* __restrict__ x, int64_t n,
+                                                             const uint32_t* __restrict__ meta,
+                                                             ThrPart* __restrict__ part) {
+  if (meta[2] == 0u) return;
+  const float bound = __uint_as_float(meta[0]);
+  const int64_t base = (int64_t)blockIdx.x * kThrChunk;
+  const int64_t end = min(base + (int64_t)kThrChunk, n);
+  uint32_t cnt = 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += kSBlock) cnt += fabsf(x[i]) >= bound;
+  __shared__ uint32_t sc[kSBlock / kWave];
+  cnt = wave_sum(cnt);
+  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int j = 0; j < kSBlock / kWave; ++j) c += sc[j];
+    part[blockIdx.x].cnt = c;
+  }
+}
+__global__ __launch_bounds__(1024) void thr_reoffset_kernel(ThrPart* __restrict__ part, int64_t nchunks,
+                                                           uint32_t* __restrict__ offs, uint32_t* __restrict__ meta) {
+  __shared__ uint32_t s_w[1024 / kWave + 1];
+  if (meta[2] == 0u) return;
+  uint32_t run = 0;
+  for (int64_t j0 = 0; j0 < nchunks; j0 += 1024) {
+    const int64_t j = j0 + threadIdx.x;
+    const uint32_t c = j < nchunks ? part[j].cnt : 0u;
+    uint32_t tot;
+    const uint32_t ex = blk_excl_scan<1024>(c, s_w, &tot);
+    if (j < nchunks) offs[j] = run + ex;
+    run += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    meta[1] = run;
+    meta[2] = 0u;
+  }
+}
+
+// r[idx[j]] -= vals[j]: ResidualMemory.update's r = t - decompress(payload) (residual.py:16-20)
+// when r already holds t; the decompressed tensor is the scattered values and zeros elsewhere
+__global__ __launch_bounds__(kSBlock) void sparse_sub_kernel(const float* __restrict__ vals,
+                                                            const int32_t* __restrict__ idx, int64_t count,
+                                                            float* __restrict__ r) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < count; j += (int64_t)gridDim.x * kSBlock)
+    r[idx[j]] = r[idx[j]] - vals[j];
+}
+
 // pass 3: ordered compaction of |x| >= bound
 template <typename IdxT>
 __global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restrict__ x, int64_t n,
@@ -251,6 +301,33 @@ grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, v
   GRACE_CHECK_LAUNCH("grace_threshold_recount");
   thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, bound, offs, meta, 1, 0);
   GRACE_CHECK_LAUNCH("grace_threshold_recount");
+  return GRACE_OK;
+}
+
+// Stage 1 without any host decision: the recount (max(x) < thr) is decided on the device, so the
+// count (ws[4..8]) can be exchanged between ranks before anything is read on the host.
+grace_status_t grace_threshold_count_dev(const float* x, int64_t n, float thr, void* ws, void* stream) {
+  GRACE_REQUIRE(x && ws && n >= 1, "grace_threshold_count_dev: bad arguments");
+  grace_status_t st = grace_threshold_count(x, n, thr, ws, stream);
+  if (st != GRACE_OK) return st;
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(p);
+  ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
+  uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  hipStream_t s = as_stream(stream);
+  thr_restats_kernel<<<(unsigned)nch, kSBlock, 0, s>>>(x, n, meta, part);
+  GRACE_CHECK_LAUNCH("grace_threshold_count_dev");
+  thr_reoffset_kernel<<<1, 1024, 0, s>>>(part, nch, offs, meta);
+  GRACE_CHECK_LAUNCH("grace_threshold_count_dev");
+  return GRACE_OK;
+}
+
+grace_status_t grace_sparse_sub(const float* vals, const int32_t* idx, int64_t count, float* r, void* stream) {
+  GRACE_REQUIRE(count >= 0 && (count == 0 || (vals && idx && r)), "grace_sparse_sub: bad arguments");
+  if (count == 0) return GRACE_OK;
+  sparse_sub_kernel<<<stream_grid(count, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(vals, idx, count, r);
+  GRACE_CHECK_LAUNCH("grace_sparse_sub");
   return GRACE_OK;
 }
 

@@ -238,6 +238,11 @@ grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void*
 grace_status_t grace_threshold_recount(const float* x, int64_t n, float bound, void* ws, void* stream);
 grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, float* vals, int32_t* idx,
                                      void* stream);
+/* count with the max(x) < thr recount decided on the device (ws[4..8] = final count): the count can be
+ * exchanged between ranks before the host reads anything (one host read per variable-size step) */
+grace_status_t grace_threshold_count_dev(const float* x, int64_t n, float thr, void* ws, void* stream);
+/* r[idx[j]] -= vals[j] (ResidualMemory.update, residual.py:16-20, when r already holds t) */
+grace_status_t grace_sparse_sub(const float* vals, const int32_t* idx, int64_t count, float* r, void* stream);
 /* Horovod flavour (grace_dl/torch/compressor/threshold.py:17): where(|x| > thr), int64 indices.
  * bound = the smallest f32 above f32(thr) (|x| > thr <=> |x| >= bound), NaN for thr = +inf. */
 grace_status_t grace_threshold_count_fixed(const float* x, int64_t n, float bound, void* ws, void* stream);

@@ -101,6 +101,36 @@ def test_threshold_allgather_world1_variable_path():
     assert same_bits(res, O.residual_update(x, O.sparse_decode(ov, oi, x.size)))
 
 
+@pytest.mark.parametrize("n", [1, 5000, 16385, 1 << 20])
+@pytest.mark.parametrize("thr", [0.01, 1.5, 1e9])
+@pytest.mark.parametrize("memory", ["none", "residual"])
+def test_threshold_fused_one_read_step_sequence(n, thr, memory):
+    """threshold.fused_step (device recount, one host read): three steps bit-exact against the
+    oracle's compensate -> select -> decode -> residual sequence, including thresholds above the
+    signed max (recount at min(thr, max)), an all-negative step and the generic path."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    from grace_amd.dist.memory.residual import ResidualMemory
+    comp = ThresholdCompressor(thr)
+    comm = Allgather(comp, ResidualMemory() if memory == "residual" else NoneMemory(), 1)
+    assert comp.fused_step(comm, _t(np.zeros(4, np.float32)), "probe") is not None
+    rng = np.random.default_rng(n + int(thr))
+    res = None
+    for s in range(3):
+        x = rng.standard_normal(n).astype(np.float32)
+        if s == 1:
+            x = -np.abs(x)                                      # signed max < 0: threshold becomes max
+        out = _np(comm.step(_t(x), "w"))
+        t = O.residual_compensate(x, res) if memory == "residual" else x
+        ov, oi = O.threshold_select(t, thr)
+        dec = O.sparse_decode(ov, oi, n)
+        assert same_bits(out, (O.python_sum([dec]) / np.float32(1)).astype(np.float32)), s
+        if memory == "residual":
+            res = O.residual_update(t, dec)
+            assert same_bits(_np(comm.memory.residuals["w"]), res), s
+
+
 @pytest.mark.parametrize("world,n,k", [(1, 4099, 40), (2, 100003, 1000), (3, (1 << 20) + 17, 20000),
                                        (8, 5_000_000, 50000)])
 def test_sparse_aggregate_rank_ordered(world, n, k):

@@ -37,6 +37,14 @@ def _worker(rank, path, outdir, golden_path):
         res[f"big_g{s}"] = g
         res[f"big_out{s}"] = comm.step(torch.from_numpy(g).cuda(), "big").cpu().numpy()
         res[f"big_res{s}"] = comm.memory.residuals["big"].cpu().numpy()
+    # variable-size payloads: threshold + residual, one host read per step (threshold.fused_step)
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    comm = Allgather(ThresholdCompressor(1.5), ResidualMemory(), 2)
+    for s in range(3):
+        g = np.random.default_rng(2000 * rank + s).standard_normal(5003).astype(np.float32) * (1 + rank)
+        res[f"thr_g{s}"] = g
+        res[f"thr_out{s}"] = comm.step(torch.from_numpy(g).cuda(), "thr").cpu().numpy()
+        res[f"thr_res{s}"] = comm.memory.residuals["thr"].cpu().numpy()
     comm = Allgather(SignSGDCompressor(), NoneMemory(), 2)          # native majority decode
     res["sign_out"] = comm.step(torch.from_numpy(gold[pre + "sign_g"]).cuda(), "w").cpu().numpy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
@@ -67,3 +75,29 @@ def test_fused_topk_and_sign_world2(golden):
             exp = (O.python_sum(decs) / np.float32(2)).astype(np.float32)
             for r in range(2):
                 assert np.array_equal(zs[r][f"big_out{s}"].view(np.uint32), exp.view(np.uint32))
+
+
+def test_variable_size_threshold_world2_one_read():
+    """Threshold + ResidualMemory through Allgather at W = 2 with different payload sizes per rank
+    (the fused one-host-read exchange): outputs and residuals bit-exact against the oracle's
+    reference semantics (threshold.py:12-27, residual.py:10-20, allgather.py:15-45)."""
+    from oracle import grace_oracle as O
+    from tests.golden_util import GOLDEN_DIR
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(os.path.join(tmp, "rdv"), tmp, os.path.join(GOLDEN_DIR, "world2.npz")),
+                 nprocs=2, join=True)
+        zs = [dict(np.load(os.path.join(tmp, f"r{r}.npz"))) for r in range(2)]
+    res = [None, None]
+    for s in range(3):
+        decs = []
+        for r in range(2):
+            t = O.residual_compensate(zs[r][f"thr_g{s}"], res[r])
+            v, i = O.threshold_select(t, 1.5)
+            d = O.sparse_decode(v, i, t.size)
+            res[r] = O.residual_update(t, d)
+            decs.append(d)
+        sizes = [int((d != 0).sum()) for d in decs]
+        out = (O.python_sum(decs) / np.float32(2)).astype(np.float32)
+        for r in range(2):
+            assert np.array_equal(zs[r][f"thr_out{s}"].view(np.uint32), out.view(np.uint32)), (s, r, sizes)
+            assert np.array_equal(zs[r][f"thr_res{s}"].view(np.uint32), res[r].view(np.uint32)), (s, r)
