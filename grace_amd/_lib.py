@@ -88,6 +88,10 @@ SIGNATURES = {
     "grace_threshold_count_fixed": (ST, [P, I64, F32, P, P]),
     "grace_threshold_count_dev": (ST, [P, I64, F32, P, P]),
     "grace_sparse_sub": (ST, [P, P, I64, P, P]),
+    "grace_exchange_record_words": (SZ, [I64]),
+    "grace_threshold_write_capped": (ST, [P, I64, P, P, I64, P]),
+    "grace_sparse_aggregate_capped": (ST, [P, I64, I64, I32, F32, P, P, I64, P, P]),
+    "grace_sparse_sub_capped": (ST, [P, I64, P, P]),
     "grace_threshold_write_i64": (ST, [P, I64, P, P, P, P]),
     "grace_terngrad_unit": (I32, []),
     "grace_terngrad_workspace_bytes": (SZ, [I64]),

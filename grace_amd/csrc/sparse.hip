@@ -221,14 +221,22 @@ __global__ __launch_bounds__(kSBlock) void sparse_sub_kernel(const float* __rest
     r[idx[j]] = r[idx[j]] - vals[j];
 }
 
-// pass 3: ordered compaction of |x| >= bound
+// pass 3: ordered compaction of |x| >= bound.  Entries at positions >= cap are dropped (the
+// capacity-bounded exchange record); hdr, when given, receives {count, cap}.
 template <typename IdxT>
 __global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restrict__ x, int64_t n,
                                                            const uint32_t* __restrict__ offs,
                                                            const uint32_t* __restrict__ meta,
-                                                           float* __restrict__ vals, IdxT* __restrict__ idx) {
+                                                           float* __restrict__ vals, IdxT* __restrict__ idx,
+                                                           int64_t cap, uint32_t* __restrict__ hdr) {
   __shared__ uint32_t s_w[kSBlock / kWave + 1];
   const float bound = __uint_as_float(meta[0]);
+  if (hdr && blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr[0] = meta[1];
+    hdr[1] = (uint32_t)cap;
+    hdr[2] = 0u;
+    hdr[3] = 0u;
+  }
   const int64_t base = (int64_t)blockIdx.x * kThrChunk;
   const int64_t end = min(base + (int64_t)kThrChunk, n);
   uint32_t run = offs[blockIdx.x];
@@ -239,9 +247,68 @@ __global__ __launch_bounds__(kSBlock) void thr_write_kernel(const float* __restr
     if (i < end) { v = x[i]; sel = fabsf(v) >= bound; }
     uint32_t tot;
     const uint32_t ex = blk_excl_scan<kSBlock>(sel ? 1u : 0u, s_w, &tot);
-    if (sel) { vals[run + ex] = v; idx[run + ex] = (IdxT)i; }
+    if (sel && (int64_t)(run + ex) < cap) { vals[run + ex] = v; idx[run + ex] = (IdxT)i; }
     run += tot;
   }
+}
+
+// ---- capacity-bounded variable-size exchange -------------------------------------------------
+// One record per rank, `stride` = 4 + 2 cap words: {count, cap, 0, 0 | vals f32[cap] | idx i32[cap]}.
+// count may exceed cap (overflow): only the first cap entries (ascending index order) travel.
+constexpr int kRecHdr = 4;
+
+__device__ __forceinline__ int64_t rec_count(const uint32_t* rec, int64_t cap) {
+  return min((int64_t)rec[0], cap);
+}
+
+// rank w's entries, added in rank order (one launch per rank on one stream = the reference's
+// ((0 + d0) + d1) + ... order, allgather.py:40-45), tagging the last rank that touched each element
+__global__ __launch_bounds__(kSBlock) void rec_scatter_kernel(const uint32_t* __restrict__ rec, int64_t cap,
+                                                             int32_t w, float* __restrict__ out,
+                                                             int32_t* __restrict__ tags) {
+  const int64_t c = rec_count(rec, cap);
+  const float* vals = reinterpret_cast<const float*>(rec + kRecHdr);
+  const int32_t* idx = reinterpret_cast<const int32_t*>(rec + kRecHdr + cap);
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < c; j += (int64_t)gridDim.x * kSBlock) {
+    const int32_t i = idx[j];
+    out[i] = out[i] + vals[j];
+    tags[i] = w;
+  }
+}
+
+// divide each aggregated element once (by the entry of the last rank that touched it), and
+// stat = {max count over ranks, overflow flag} -- identical on every rank, so every rank takes the
+// same capacity decision without exchanging anything else
+__global__ __launch_bounds__(kSBlock) void rec_divide_kernel(const uint32_t* __restrict__ rec, int64_t stride,
+                                                            int64_t cap, int32_t world, float divisor,
+                                                            int32_t do_divide, float* __restrict__ out,
+                                                            const int32_t* __restrict__ tags,
+                                                            uint32_t* __restrict__ stat) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t mx = 0u;
+    for (int w = 0; w < world; ++w) mx = max(mx, rec[(int64_t)w * stride]);
+    stat[0] = mx;
+    stat[1] = (int64_t)mx > cap ? 1u : 0u;
+  }
+  if (!do_divide) return;
+  const int64_t total = (int64_t)world * cap;
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < total; j += (int64_t)gridDim.x * kSBlock) {
+    const int64_t w = j / cap, e = j - w * cap;
+    const uint32_t* r = rec + w * stride;
+    if (e >= rec_count(r, cap)) continue;
+    const int32_t i = reinterpret_cast<const int32_t*>(r + kRecHdr + cap)[e];
+    if (tags[i] == (int32_t)w) out[i] = out[i] / divisor;
+  }
+}
+
+// r[idx] -= vals over the entries that travelled (ResidualMemory.update, residual.py:16-20)
+__global__ __launch_bounds__(kSBlock) void rec_sub_kernel(const uint32_t* __restrict__ rec, int64_t cap,
+                                                         float* __restrict__ r) {
+  const int64_t c = rec_count(rec, cap);
+  const float* vals = reinterpret_cast<const float*>(rec + kRecHdr);
+  const int32_t* idx = reinterpret_cast<const int32_t*>(rec + kRecHdr + cap);
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < c; j += (int64_t)gridDim.x * kSBlock)
+    r[idx[j]] = r[idx[j]] - vals[j];
 }
 
 }  // namespace grace
@@ -338,7 +405,8 @@ grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, 
   const char* p = reinterpret_cast<const char*>(ws);
   const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
   const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
-  thr_write_kernel<int32_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
+  thr_write_kernel<int32_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx, n,
+                                                                           nullptr);
   GRACE_CHECK_LAUNCH("grace_threshold_write");
   return GRACE_OK;
 }
@@ -387,8 +455,57 @@ grace_status_t grace_threshold_write_i64(const float* x, int64_t n, const void* 
   const char* p = reinterpret_cast<const char*>(ws);
   const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
   const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
-  thr_write_kernel<int64_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx);
+  thr_write_kernel<int64_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx, n,
+                                                                           nullptr);
   GRACE_CHECK_LAUNCH("grace_threshold_write_i64");
+  return GRACE_OK;
+}
+
+size_t grace_exchange_record_words(int64_t cap) { return (size_t)(kRecHdr + 2 * cap); }
+
+// Writes this rank's capacity-bounded exchange record (after grace_threshold_count_dev).
+grace_status_t grace_threshold_write_capped(const float* x, int64_t n, const void* ws, uint32_t* rec, int64_t cap,
+                                            void* stream) {
+  GRACE_REQUIRE(x && ws && rec && n >= 1 && cap >= 1 && cap <= n && n < ((int64_t)1 << 31),
+                "grace_threshold_write_capped: bad arguments (1 <= cap <= n)");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  const char* p = reinterpret_cast<const char*>(ws);
+  const uint32_t* meta = reinterpret_cast<const uint32_t*>(p);
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  float* vals = reinterpret_cast<float*>(rec + kRecHdr);
+  int32_t* idx = reinterpret_cast<int32_t*>(rec + kRecHdr + cap);
+  thr_write_kernel<int32_t><<<(unsigned)nch, kSBlock, 0, as_stream(stream)>>>(x, n, offs, meta, vals, idx, cap, rec);
+  GRACE_CHECK_LAUNCH("grace_threshold_write_capped");
+  return GRACE_OK;
+}
+
+// Rank-ordered decode + aggregate of W gathered records (stride = grace_exchange_record_words(cap)
+// words apart) into out[n] (zero-filled here), each element divided once by `divisor`; stat
+// (device, u32[2]) = {max count over ranks, overflow = max count > cap}.
+grace_status_t grace_sparse_aggregate_capped(const uint32_t* recs, int64_t stride, int64_t cap, int32_t world,
+                                             float divisor, float* out, int32_t* tags, int64_t n, uint32_t* stat,
+                                             void* stream) {
+  GRACE_REQUIRE(recs && out && tags && stat && world >= 1 && cap >= 1 && stride == kRecHdr + 2 * cap && n >= 1,
+                "grace_sparse_aggregate_capped: bad arguments");
+  grace_status_t st = grace_fill(out, 0.f, n, stream);
+  if (st != GRACE_OK) return st;
+  hipStream_t s = as_stream(stream);
+  const unsigned g = stream_grid(cap, kSBlock, 1024);
+  for (int w = 0; w < world; ++w) {
+    rec_scatter_kernel<<<g, kSBlock, 0, s>>>(recs + (int64_t)w * stride, cap, w, out, tags);
+    GRACE_CHECK_LAUNCH("grace_sparse_aggregate_capped");
+  }
+  const int do_div = divisor != 1.0f;
+  rec_divide_kernel<<<do_div ? stream_grid((int64_t)world * cap, kSBlock, 2048) : 1u, kSBlock, 0, s>>>(
+      recs, stride, cap, world, divisor, do_div, out, tags, stat);
+  GRACE_CHECK_LAUNCH("grace_sparse_aggregate_capped");
+  return GRACE_OK;
+}
+
+grace_status_t grace_sparse_sub_capped(const uint32_t* rec, int64_t cap, float* r, void* stream) {
+  GRACE_REQUIRE(rec && r && cap >= 1, "grace_sparse_sub_capped: bad arguments");
+  rec_sub_kernel<<<stream_grid(cap, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(rec, cap, r);
+  GRACE_CHECK_LAUNCH("grace_sparse_sub_capped");
   return GRACE_OK;
 }
 

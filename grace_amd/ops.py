@@ -265,15 +265,20 @@ def sparse_decode(vals, idx, n):
 _tags = {}
 
 
-def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out=None):
-    """Rank-ordered decode+aggregate of W sparse payloads laid out rank-major with `stride`.
-    With `out` given it must already be zero-filled (e.g. by a fill that overlapped the gather)."""
-    dev = vals_base.device
+def _agg_tags(dev, n):
     key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)   # per stream, like workspace()
     tags = _tags.get(key)
     if tags is None or tags.numel() < n:
         tags = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         _tags[key] = tags
+    return tags
+
+
+def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out=None):
+    """Rank-ordered decode+aggregate of W sparse payloads laid out rank-major with `stride`.
+    With `out` given it must already be zero-filled (e.g. by a fill that overlapped the gather)."""
+    dev = vals_base.device
+    tags = _agg_tags(dev, n)
     prefilled = out is not None
     if out is None:
         out = torch.empty(n, dtype=F32, device=dev)
@@ -281,6 +286,23 @@ def sparse_aggregate(vals_base, idx_base, stride, counts, world, n, divisor, out
     arr = (ctypes.c_int64 * world)(*[int(c) for c in counts])
     _lib.call("grace_sparse_aggregate_into" if prefilled else "grace_sparse_aggregate", _p(vals_base), _p(idx_base),
               int(stride), ctypes.addressof(arr), int(world), float(divisor), _p(out), _p(tags), n, _stream())
+    return out
+
+
+def exchange_record_words(cap):
+    return int(_lib.query("grace_exchange_record_words", int(cap)))
+
+
+def sparse_aggregate_capped(recs, cap, world, n, divisor, stat):
+    """Rank-ordered decode+aggregate of W gathered capacity-bounded records (counts read from the
+    record headers on the device); stat (int32[2] on the device) <- {max count, overflow flag}."""
+    require_dev(recs, "records")
+    stride = exchange_record_words(cap)
+    if recs.numel() != world * stride or recs.dtype != torch.int32 or stat.numel() < 2:
+        raise ValueError("sparse_aggregate_capped: records / stat do not match (world, cap)")
+    out = torch.empty(n, dtype=F32, device=recs.device)
+    _lib.call("grace_sparse_aggregate_capped", _p(recs), stride, int(cap), int(world), float(divisor), _p(out),
+              _p(_agg_tags(recs.device, n)), int(n), _p(stat), _stream())
     return out
 
 

@@ -243,6 +243,19 @@ grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, 
 grace_status_t grace_threshold_count_dev(const float* x, int64_t n, float thr, void* ws, void* stream);
 /* r[idx[j]] -= vals[j] (ResidualMemory.update, residual.py:16-20, when r already holds t) */
 grace_status_t grace_sparse_sub(const float* vals, const int32_t* idx, int64_t count, float* r, void* stream);
+/* Capacity-bounded variable-size exchange (allgather.py:15-38 without the size round trip): each rank
+ * writes one record of grace_exchange_record_words(cap) u32 words {count, cap, 0, 0 | vals f32[cap] |
+ * idx i32[cap]} (entries past cap are dropped: overflow), the records are all-gathered as one
+ * fixed-size buffer, and the aggregate reads the counts from the gathered headers on the device.
+ * stat (device u32[2]) = {max count over ranks, overflow flag}: the same on every rank. */
+size_t grace_exchange_record_words(int64_t cap);
+grace_status_t grace_threshold_write_capped(const float* x, int64_t n, const void* ws, uint32_t* rec, int64_t cap,
+                                            void* stream);
+grace_status_t grace_sparse_aggregate_capped(const uint32_t* recs, int64_t stride, int64_t cap, int32_t world,
+                                             float divisor, float* out, int32_t* tags, int64_t n, uint32_t* stat,
+                                             void* stream);
+/* r[idx] -= vals over the min(count, cap) entries of one record */
+grace_status_t grace_sparse_sub_capped(const uint32_t* rec, int64_t cap, float* r, void* stream);
 /* Horovod flavour (grace_dl/torch/compressor/threshold.py:17): where(|x| > thr), int64 indices.
  * bound = the smallest f32 above f32(thr) (|x| > thr <=> |x| >= bound), NaN for thr = +inf. */
 grace_status_t grace_threshold_count_fixed(const float* x, int64_t n, float bound, void* ws, void* stream);

@@ -131,6 +131,76 @@ def test_threshold_fused_one_read_step_sequence(n, thr, memory):
             assert same_bits(_np(comm.memory.residuals["w"]), res), s
 
 
+@pytest.mark.parametrize("memory", ["none", "residual"])
+def test_threshold_capacity_exchange_retry_bit_exact(memory):
+    """exchange='capacity', overflow='retry': the first step learns the capacity through the counts
+    exchange, later steps send fixed-size records; a step whose count outgrows the capacity is redone
+    exactly.  Every step bit-exact with the oracle sequence."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = 300_007
+    comp = ThresholdCompressor(2.0, exchange="capacity", capacity_margin=1.25)
+    comm = Allgather(comp, ResidualMemory() if memory == "residual" else NoneMemory(), 1)
+    rng = np.random.default_rng(77)
+    res = None
+    scales = [1.0, 1.0, 1.05, 2.0, 1.0, 0.1]      # step 3 overflows (count grows ~8x)
+    for s, sc in enumerate(scales):
+        x = (rng.standard_normal(n) * sc).astype(np.float32)
+        out = _np(comm.step(_t(x), "w"))
+        t = O.residual_compensate(x, res) if memory == "residual" else x
+        ov, oi = O.threshold_select(t, 2.0)
+        dec = O.sparse_decode(ov, oi, n)
+        assert same_bits(out, dec), s
+        if memory == "residual":
+            res = O.residual_update(t, dec)
+            assert same_bits(_np(comm.memory.residuals["w"]), res), s
+        assert comp.capacity["w"] >= 64
+    assert comp.overflows >= 1
+
+
+def test_threshold_capacity_exchange_defer_keeps_overflow_in_residual():
+    """overflow='defer' (ResidualMemory): no host read in the step.  Without overflow the step is
+    bit-exact; on overflow only the first `cap` selected entries (ascending index) are sent, the rest
+    stay in the residual, and the next step of the name runs with a grown capacity.  Inputs: small
+    noise plus c_s spikes of magnitude 5, so the selected count is controlled step by step."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n, margin = 200_003, 1.5
+    comp = ThresholdCompressor(2.0, exchange="capacity", capacity_margin=margin, overflow="defer")
+    comm = Allgather(comp, ResidualMemory(), 1)
+    rng = np.random.default_rng(5)
+    grow = lambda mx: int(min(n, max(64, int(np.ceil(mx * margin)))))
+    res, cap, prev = None, None, None      # mirror of the capacity policy (threshold._settle)
+    truncated = 0
+    for s, c in enumerate([1000, 1000, 5000, 1000, 1000]):
+        x = (rng.standard_normal(n) * 0.01).astype(np.float32)
+        x[rng.choice(n, c, replace=False)] = np.float32(5.0)
+        if prev is not None and (prev[0] > prev[1] or grow(prev[0]) * 4 < prev[1]):
+            cap = grow(prev[0])
+        out = _np(comm.step(_t(x), "w"))
+        t = O.residual_compensate(x, res)
+        ov, oi = O.threshold_select(t, 2.0)
+        if cap is None:
+            cap, prev = grow(oi.size), None                 # learned through the counts exchange
+        else:
+            prev = (oi.size, cap)
+            if oi.size > cap:
+                ov, oi = ov[:cap], oi[:cap]
+                truncated += 1
+        assert comp.capacity["w"] == cap or prev is not None, s
+        dec = O.sparse_decode(ov, oi, n)
+        res = O.residual_update(t, dec)
+        assert same_bits(out, dec), s
+        assert same_bits(_np(comm.memory.residuals["w"]), res), s
+    assert truncated == 1
+    torch.cuda.synchronize()
+    comp._settle("w", n)
+    assert comp.overflows == 1
+
+
 @pytest.mark.parametrize("world,n,k", [(1, 4099, 40), (2, 100003, 1000), (3, (1 << 20) + 17, 20000),
                                        (8, 5_000_000, 50000)])
 def test_sparse_aggregate_rank_ordered(world, n, k):

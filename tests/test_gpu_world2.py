@@ -45,6 +45,15 @@ def _worker(rank, path, outdir, golden_path):
         res[f"thr_g{s}"] = g
         res[f"thr_out{s}"] = comm.step(torch.from_numpy(g).cuda(), "thr").cpu().numpy()
         res[f"thr_res{s}"] = comm.memory.residuals["thr"].cpu().numpy()
+    # capacity-bounded records (the overflow step is retried exactly)
+    comm = Allgather(ThresholdCompressor(1.5, exchange="capacity"), ResidualMemory(), 2)
+    for s in range(4):
+        sc = 3.0 if s == 2 and rank == 1 else 1.0
+        g = (np.random.default_rng(3000 * rank + s).standard_normal(5003) * sc).astype(np.float32)
+        res[f"cap_g{s}"] = g
+        res[f"cap_out{s}"] = comm.step(torch.from_numpy(g).cuda(), "thr").cpu().numpy()
+        res[f"cap_res{s}"] = comm.memory.residuals["thr"].cpu().numpy()
+    res["cap_overflows"] = np.array([comm.compressor.overflows])
     comm = Allgather(SignSGDCompressor(), NoneMemory(), 2)          # native majority decode
     res["sign_out"] = comm.step(torch.from_numpy(gold[pre + "sign_g"]).cuda(), "w").cpu().numpy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
@@ -87,11 +96,18 @@ def test_variable_size_threshold_world2_one_read():
         mp.spawn(_worker, args=(os.path.join(tmp, "rdv"), tmp, os.path.join(GOLDEN_DIR, "world2.npz")),
                  nprocs=2, join=True)
         zs = [dict(np.load(os.path.join(tmp, f"r{r}.npz"))) for r in range(2)]
+    for pre, steps in (("thr", 3), ("cap", 4)):
+        _check_thr_sequence(O, zs, pre, steps)
+    # every rank takes the same capacity decisions (the stat comes from the gathered headers)
+    assert zs[0]["cap_overflows"][0] >= 1 and zs[0]["cap_overflows"][0] == zs[1]["cap_overflows"][0]
+
+
+def _check_thr_sequence(O, zs, pre, steps):
     res = [None, None]
-    for s in range(3):
+    for s in range(steps):
         decs = []
         for r in range(2):
-            t = O.residual_compensate(zs[r][f"thr_g{s}"], res[r])
+            t = O.residual_compensate(zs[r][f"{pre}_g{s}"], res[r])
             v, i = O.threshold_select(t, 1.5)
             d = O.sparse_decode(v, i, t.size)
             res[r] = O.residual_update(t, d)
@@ -99,5 +115,5 @@ def test_variable_size_threshold_world2_one_read():
         sizes = [int((d != 0).sum()) for d in decs]
         out = (O.python_sum(decs) / np.float32(2)).astype(np.float32)
         for r in range(2):
-            assert np.array_equal(zs[r][f"thr_out{s}"].view(np.uint32), out.view(np.uint32)), (s, r, sizes)
-            assert np.array_equal(zs[r][f"thr_res{s}"].view(np.uint32), res[r].view(np.uint32)), (s, r)
+            assert np.array_equal(zs[r][f"{pre}_out{s}"].view(np.uint32), out.view(np.uint32)), (pre, s, r, sizes)
+            assert np.array_equal(zs[r][f"{pre}_res{s}"].view(np.uint32), res[r].view(np.uint32)), (pre, s, r)
