@@ -15,6 +15,7 @@
 namespace grace {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxRank = 16;
 
@@ -1089,6 +1090,558 @@ __global__ __launch_bounds__(256) void psgd_outer4_kernel(const float* __restric
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// World-1 rank-4 compress in ONE pass over M (psgd_w1_pass + psgd_w1_fin).
+//
+// At world size 1 nothing is all-reduced between the contractions (powersgd.py:44-52), so
+//   P = orth(M q) = P_raw R^-1           (R = chol(P_raw^T P_raw), the R of the reference's MGS)
+//   Q = M^T P      = (M^T P_raw) R^-1
+// and both P_raw = M q and Qraw = M^T P_raw come out of a single read of M: P_raw's row i needs
+// only row i of M, which is still in registers when Qraw accumulates M[i, j] P_raw[i, :].  Qraw is
+// accumulated in f64 (f32 x f32 products are exact in f64), so the triangular solve by R^-1 does
+// not amplify rounding by kappa(R) the way an f32 Qraw would: Q matches M^T P to f32 accuracy.
+// M is read once instead of twice (8 nm bytes per step with the decompression instead of 12 nm).
+//
+// psgd_w1_pass: a 1024-thread workgroup owns a 1024-column group of a 64-row slab -- column wave
+// cw = w & 3 holds 256 columns (4 per lane), row wave rw = w >> 2 holds 16 rows, all 16 rows'
+// loads issued at once (the grid is sized to one workgroup per CU, so the whole of M is in
+// flight).  Per row the lane's 4 x 4 products are summed over its DPP row (16 lanes), the 16
+// (column wave, DPP row) partials of the group in LDS, and the G = ceil(m / 1024) column groups of
+// the slab exchange their 64 x 4 partials through write-through (sc1) 16-B records and one
+// arrival counter per slab; every group sums the G records in the same order, so they all hold
+// bit-identical P_raw rows.  Then Qraw[j, c] += M[i, j] P_raw[i, c] in f64 from the registers; the
+// row waves are summed in LDS and each workgroup writes one f64 [1024 x 4] partial.  Group 0 of
+// each slab writes P_raw and accumulates the slab's Gram matrix (f64).
+// psgd_w1_fin: every workgroup sums the Gram partials (fixed order), factors R = chol(G) and
+// solves its share of rows: P = P_raw R^-1 in place, Q = (sum of the Qraw partials) R^-1.  When the
+// pivots say P_raw is ill-conditioned (as psgd_orth4_kernel), workgroup 0 runs MGS2 on P_raw,
+// publishes its R (write-through + flag) and the others solve Q with that R.
+// Requirements (checked by grace_powersgd_w1_ok): r == 4, m % 4 == 0, m <= 16384, 16-B aligned M,
+// q, P, Q; the launch keeps the grid within one workgroup per CU (co-resident: the exchange waits).
+constexpr int kW1Block = 1024;
+constexpr int kW1Rows = 16;                   // rows per lane (per row wave)
+constexpr int kW1Slab = 4 * kW1Rows;          // 64 rows per slab
+constexpr int kW1Cols = 1024;                 // columns per workgroup
+constexpr int kW1MaxG = 16;                   // m <= 16384
+constexpr int kW1FinBlock = 1024;
+constexpr uint32_t kW1SpinMax = 1u << 22;     // bounded waits (never expected to run out)
+
+#ifdef GRACE_STAMPS   // diagnostic build only: s_memrealtime phase stamps of psgd_w1_pass
+#define W1_STAMP(ws, slot) do { if (threadIdx.x == 0) { if (blockIdx.x == 0 && blockIdx.y == 0) (ws).dbg[slot] = __builtin_amdgcn_s_memrealtime(); \
+    if ((slot) >= 1 && (slot) <= 4) (ws).dbg[8 + 4 * (blockIdx.y * gridDim.x + blockIdx.x) + (slot) - 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+#define W1_SPAN(ws) do { if (threadIdx.x == 0) { atomicMin((unsigned long long*)&(ws).dbg[6], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
+#define W1_END(ws) do { if (threadIdx.x == 0) { atomicMax((unsigned long long*)&(ws).dbg[7], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
+#define FIN_STAMP(ws, slot) do { if (threadIdx.x == 0 && blockIdx.x == 0) (ws).dbg[1800 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define FIN_SPAN(ws) do { if (threadIdx.x == 0) { atomicMin((unsigned long long*)&(ws).dbg[1810], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
+#define FIN_END(ws) do { if (threadIdx.x == 0) { atomicMax((unsigned long long*)&(ws).dbg[1811], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
+#else
+#define FIN_STAMP(ws, slot) do { } while (0)
+#define FIN_SPAN(ws) do { } while (0)
+#define FIN_END(ws) do { } while (0)
+#define W1_STAMP(ws, slot) do { } while (0)
+#define W1_SPAN(ws) do { } while (0)
+#define W1_END(ws) do { } while (0)
+#endif
+
+struct W1Ws {
+  uint32_t* arr;      // [S] exchange arrivals
+  uint32_t* done;     // [S] exchange reads
+  uint32_t* ctl;      // [0] robust-path flag, [1] its reads, [2] status (1 = a wait ran out)
+  uint64_t* dbg;      // diagnostic stamps (GRACE_STAMPS builds only)
+  f32x4v* xp;         // [S][G][64] partial P rows
+  double* qpart;      // [S][m][4] one f64 partial of Qraw per slab
+  double* gpart;      // [4 S][16] four Gram partials per slab
+};
+
+__device__ __forceinline__ float row16_sum_f32(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+__device__ __forceinline__ bool spin_until(const uint32_t* p, uint32_t target, uint32_t* status) {
+  uint32_t spins = 0;
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > kW1SpinMax) {
+      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+
+template <bool DRAWQ>
+__global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict__ M, int64_t n, int64_t m,
+                                                        const float* __restrict__ q, uint64_t seed,
+                                                        float* __restrict__ P, W1Ws ws, int S) {
+  __shared__ float pp[4][kW1Rows][4][4];       // [rw][d][cw][rank]: the column waves' partials
+  __shared__ double prow[kW1Slab][4];          // P_raw rows of the slab, f64
+  __shared__ double qred[2][16 * 256];         // row-wave pair sums, [e][column-wave lane]
+  __shared__ f32x4v qsh[kW1Cols];               // q rows of this column group
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cw = w & 3, rw = w >> 2;
+  const int G = gridDim.x, cg = blockIdx.x, SG = gridDim.y;
+  W1_STAMP(ws, 0);
+  W1_SPAN(ws);
+  const int64_t jc = (int64_t)cg * kW1Cols + 256 * cw + 4 * lane;
+  const bool colv = jc < m;                    // m % 4 == 0: all 4 columns or none
+  const uint32_t jo = colv ? (uint32_t)jc : 0u; // lane offset within a row (m <= 16384)
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc(ws.xp, (short)0, 0x7FFFFFFF, 0x00020000);
+  // Row interleave: slab s is row lanes 4 s + rw, and row lane l holds rows l + L d (L = 4 S), so at
+  // load step d every workgroup reads inside one contiguous band of L rows (a sequential sweep of M
+  // rather than 4 S scattered 16-row runs)
+  const int64_t L = 4 * (int64_t)S;
+  bool qstaged = false;
+  for (int s = blockIdx.y; s < S; s += SG) {
+    const int64_t lrow = 4 * (int64_t)s + rw;
+    f32x4v v[kW1Rows];
+#pragma unroll
+    for (int d = 0; d < kW1Rows; ++d) {        // every load issued before any is used
+      // wave-uniform row base (scalar) + 32-bit lane offset; a row past n re-reads row n - 1
+      const int64_t row = lrow + L * d;
+      const float* rowp = M + (row < n ? row : n - 1) * m;
+      v[d] = *reinterpret_cast<const f32x4v*>(rowp + jo);
+    }
+    if (!qstaged) {   // q rows of the group into LDS (drawn or loaded) while M's loads are in flight
+      qstaged = true;
+      const int64_t jq = (int64_t)cg * kW1Cols + threadIdx.x;
+      f32x4v qr = {0.f, 0.f, 0.f, 0.f};
+      if (jq < m) {
+        if constexpr (DRAWQ) {
+          float z0, z1, z2, z3;
+          normal_pair(seed, (uint64_t)jq * 2, z0, z1);
+          normal_pair(seed, (uint64_t)jq * 2 + 1, z2, z3);
+          qr = f32x4v{z0, z1, z2, z3};
+        } else {
+          qr = *reinterpret_cast<const f32x4v*>(q + 4 * jq);
+        }
+      }
+      qsh[threadIdx.x] = qr;
+    }
+    // no masking of v (a masked copy would double the rows' registers): a column past m has zero
+    // q rows (qsh), and a row past n re-reads row n - 1 but gets a zero P_raw row (prow) below
+    // partial P of each row over the lane's 4 columns, summed over the DPP row
+    __syncthreads();   // qsh written (first slab)
+    // Partial P over the wave's 256 columns, 4 rows (16 values: row dd, rank c at 4 dd + c) at a
+    // time, by a 64-lane reduce-scatter: permlane32 swap (+8), permlane16 swap (+4), row mirror
+    // (+2) and half-row mirror (+1) each halve the values a lane holds while summing over lane
+    // pairs, then a quad allreduce; lane l ends with value l >> 2 summed over all 64 lanes.
+    // ~40 VALU ops per 4 rows instead of 4 DPP stages for every value.
+    const f32x4v* qrow = &qsh[256 * cw + 4 * lane];   // the lane's 4 q rows (LDS)
+    const bool b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
+#pragma unroll
+    for (int b4 = 0; b4 < kW1Rows / 4; ++b4) {
+      const f32x4v q0 = qrow[0], q1 = qrow[1], q2 = qrow[2], q3 = qrow[3];
+      float u[16];
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {   // ranks in pairs: packed f32 FMAs
+        const f32x4v mv = v[4 * b4 + dd];
+#pragma unroll
+        for (int c = 0; c < 4; c += 2) {
+          f32x2v x = f32x2v{mv.x, mv.x} * f32x2v{q0[c], q0[c + 1]};
+          x = __builtin_elementwise_fma(f32x2v{mv.y, mv.y}, f32x2v{q1[c], q1[c + 1]}, x);
+          x = __builtin_elementwise_fma(f32x2v{mv.z, mv.z}, f32x2v{q2[c], q2[c + 1]}, x);
+          x = __builtin_elementwise_fma(f32x2v{mv.w, mv.w}, f32x2v{q3[c], q3[c + 1]}, x);
+          u[4 * dd + c] = x.x;
+          u[4 * dd + c + 1] = x.y;
+        }
+      }
+      float z[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(u[k]), __float_as_uint(u[k + 8]), false, false);
+        z[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      float y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(z[k]), __float_as_uint(z[k + 4]), false, false);
+        y[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      float x2[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float send = b3 ? y[k] : y[k + 2], keep = b3 ? y[k + 2] : y[k];
+        x2[k] = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x140, 0xF, 0xF, false));   // row_mirror
+      }
+      const float send = b2 ? x2[0] : x2[1], keep = b2 ? x2[1] : x2[0];
+      float w1 = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x141, 0xF, 0xF, false));   // half mirror
+      w1 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(w1), 0x4E, 0xF, 0xF, false));
+      w1 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(w1), 0xB1, 0xF, 0xF, false));
+      if ((lane & 3) == 0) pp[rw][4 * b4 + (lane >> 4)][cw][(lane >> 2) & 3] = w1;
+    }
+    __syncthreads();
+    W1_STAMP(ws, 1);
+    const int t = threadIdx.x;
+    f32x4v part = {0.f, 0.f, 0.f, 0.f};
+    if (t < kW1Slab) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) part += *reinterpret_cast<const f32x4v*>(pp[t >> 4][t & 15][k]);
+      if (G > 1) __builtin_amdgcn_raw_buffer_store_b128(part, xrs, (int)((((int64_t)s * G + cg) * kW1Slab + t) * 16), 0, kSc1);
+    }
+    if (G > 1) {
+      // every wave's write-through record stores complete, then one arrival per workgroup; wait
+      // for the slab's G groups (co-resident grid) and read all G records in group order
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        __hip_atomic_fetch_add(ws.arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(ws.arr + s, (uint32_t)G, ws.ctl + 2);
+      }
+      __syncthreads();
+      W1_STAMP(ws, 2);
+      if (t < kW1Slab) {   // the G records in group order, 4 loads in flight per round (clamped)
+        part = f32x4v{0.f, 0.f, 0.f, 0.f};
+        for (int g0 = 0; g0 < G; g0 += 4) {
+          f32x4v rec[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            rec[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                xrs, (int)((((int64_t)s * G + (g0 + u < G ? g0 + u : G - 1)) * kW1Slab + t) * 16), 0, kSc1);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (g0 + u < G) part += rec[u];
+        }
+      }
+    }
+    if (t < kW1Slab) {
+      const int64_t row = 4 * (int64_t)s + (t >> 4) + L * (t & 15);   // slab row t = (rw, d)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) prow[t][c] = row < n ? (double)part[c] : 0.0;
+      if (cg == 0) {
+        // group 0 writes P_raw and the slab's Gram partials: wave 0 holds the 64 slab rows, each
+        // DPP row of 16 sums its rows' products (f64, symmetric butterflies) -> 4 partials per slab
+        if (row < n) *reinterpret_cast<f32x4v*>(P + row * 4) = part;
+        double gv[10];
+        int e = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int c2 = c; c2 < 4; ++c2, ++e) gv[e] = row < n ? (double)part[c] * (double)part[c2] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) gv[k] = row16_sum(gv[k]);
+        if ((t & 15) == 0) {
+#pragma unroll
+          for (int k = 0; k < 10; ++k) ws.gpart[((int64_t)s * 4 + (t >> 4)) * 16 + k] = gv[k];
+        }
+      }
+    }
+    __syncthreads();
+    if (G > 1 && t == 0) {   // the last group to finish reading re-zeroes the slab's counters
+      if (__hip_atomic_fetch_add(ws.done + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)G - 1) {
+        __hip_atomic_store(ws.arr + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.done + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    W1_STAMP(ws, 3);
+    // Qraw += M[i, j] P_raw[i, :] in f64, rows in order
+    double acc[4][4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[s4][c] = 0.0;
+#ifdef GRACE_W1_NOQ   // diagnostic A/B build only: no Qraw FMAs (wrong Q)
+    for (int s4 = 0; s4 < 4; ++s4) acc[s4][0] = (double)v[s4][s4];
+#else
+#pragma unroll
+    for (int d = 0; d < kW1Rows; ++d) {
+      const double* pr = prow[rw * kW1Rows + d];   // wave-uniform: LDS broadcast
+      const double p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const double mv = (double)v[d][s4];
+        acc[s4][0] = fma(mv, p0, acc[s4][0]);
+        acc[s4][1] = fma(mv, p1, acc[s4][1]);
+        acc[s4][2] = fma(mv, p2, acc[s4][2]);
+        acc[s4][3] = fma(mv, p3, acc[s4][3]);
+      }
+    }
+#endif
+    // row waves summed as (rw0 + rw1) + (rw2 + rw3) through two LDS regions laid out element-major
+    // (qred[buf][e][256 cw-lanes]: consecutive lanes on consecutive banks), e = 4 s4 + rank
+    double* q16a = &qred[0][64 * cw + lane];
+    double* q16b = &qred[1][64 * cw + lane];
+    if (rw & 1) {
+      double* dst = rw == 1 ? q16a : q16b;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dst[e * 256] = acc[e >> 2][e & 3];
+    }
+    __syncthreads();
+    if (!(rw & 1)) {
+      const double* src = rw == 0 ? q16a : q16b;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e >> 2][e & 3] += src[e * 256];
+    }
+    __syncthreads();
+    if (rw == 2) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) q16a[e * 256] = acc[e >> 2][e & 3];
+    }
+    __syncthreads();
+    if (rw == 0) {   // the final sums, element-major, into the second region
+#pragma unroll
+      for (int e = 0; e < 16; ++e) q16b[e * 256] = acc[e >> 2][e & 3] + q16a[e * 256];
+    }
+    __syncthreads();
+    {
+      // the slab's f64 [columns x 4] partial of Qraw (psgd_w1_fin sums the S slabs in order),
+      // 32 KB stored by all 1024 threads as 16-B pieces contiguous across the workgroup:
+      // piece q = column q / 2 of the group, ranks 2 (q & 1) and 2 (q & 1) + 1
+      const int64_t gbase = ((int64_t)s * m + (int64_t)cg * kW1Cols) * 4;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int qp = threadIdx.x + 1024 * h, jl = qp >> 1;
+        if ((int64_t)cg * kW1Cols + jl < m) {
+          const int cwl = 64 * (jl >> 8) + ((jl & 255) >> 2), e0 = 4 * (jl & 3) + 2 * (qp & 1);
+          *reinterpret_cast<double2*>(ws.qpart + gbase + 2 * qp) =
+              make_double2(qred[1][e0 * 256 + cwl], qred[1][(e0 + 1) * 256 + cwl]);
+        }
+      }
+    }
+    __syncthreads();   // prow / pp / qred are rewritten by the next slab
+  }
+  W1_STAMP(ws, 4);
+  W1_END(ws);
+}
+
+// row solve x = a R^-1 (forward substitution, f64)
+__device__ __forceinline__ void w1_solve(const double (&a)[4], const double (&Rs)[4][4], const double (&Rinv)[4],
+                                         double (&x)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double t = a[c];
+#pragma unroll
+    for (int k = 0; k < c; ++k) t -= x[k] * Rs[k][c];
+    x[c] = t * Rinv[c];
+  }
+}
+
+// Q[j0 .. j1) = M^T P directly (robust path): thread (row lane rl = t >> 4, column quad cq = t & 15)
+// accumulates rows rl, rl + 64, ... of its 4 columns in f64; the 64 row lanes are summed in a fixed
+// order (cross-row shuffles, then the 16 waves in LDS).
+__device__ void w1_direct_q(const float* __restrict__ M, const float* __restrict__ P, int64_t n, int64_t m,
+                            int64_t j0, int64_t j1, float* __restrict__ Q) {
+  __shared__ double red[kW1FinBlock / kWave][16][16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rl = t >> 4, cq = t & 15;
+  for (int64_t jb = j0; jb < j1; jb += 64) {
+    const int64_t j = jb + 4 * cq;
+    const bool jv = j < j1;
+    double acc[4][4] = {};
+    for (int64_t i = rl; i < n; i += kW1FinBlock / 16) {
+      const f32x4v mv = *reinterpret_cast<const f32x4v*>(M + i * m + (jv ? j : j0));
+      const f32x4v pv = *reinterpret_cast<const f32x4v*>(P + i * 4);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[s4][c] = fma((double)mv[s4], (double)pv[c], acc[s4][c]);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double v = acc[s4][c];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) red[w][cq][s4 * 4 + c] = v;
+      }
+    __syncthreads();
+    if (t < 256) {
+      const int cq2 = t >> 4, e = t & 15;
+      double v = 0.0;
+      for (int ww = 0; ww < kW1FinBlock / kWave; ++ww) v += red[ww][cq2][e];
+      const int64_t jj = jb + 4 * cq2 + (e >> 2);
+      if (jj < j1) Q[jj * 4 + (e & 3)] = (float)v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kW1FinBlock) void psgd_w1_fin(const float* __restrict__ M, float* __restrict__ P,
+                                                          int64_t n, int64_t m, float* __restrict__ Q, W1Ws ws,
+                                                          int S) {
+  __shared__ double Gs[10];
+  __shared__ double Rs[4][4];
+  __shared__ double Rinv[4];
+  __shared__ int s_robust;
+  const int t = threadIdx.x, NB = gridDim.x, b = blockIdx.x;
+  FIN_STAMP(ws, 0);
+  FIN_SPAN(ws);
+  // this workgroup's Q rows (16 per round)
+  const int64_t qper = ((m + NB - 1) / NB + 15) / 16 * 16;
+  const int64_t q0 = min(m, (int64_t)b * qper), q1 = min(m, q0 + qper);
+  // This workgroup's P_raw rows and its first Q round's partials are loaded first: their latency
+  // overlaps the Gram sum and the factorisation below.  Q: wave w owns column q0 + w of a round
+  // (16 per round), lane sl sums slabs sl, sl + 64, ... in order; then a fixed-order butterfly
+  // over the 64 lanes.
+  const int64_t pper = (n + NB - 1) / NB;
+  const int64_t prow_i = (int64_t)b * pper + t;
+  const bool pv_ok = t < pper && prow_i < n;
+  const f32x4v pv = *reinterpret_cast<const f32x4v*>(P + (pv_ok ? prow_i : 0) * 4);
+  const int col = t >> 6, sl = t & 63;
+  double2 pre_lo[4], pre_hi[4];
+  {
+    const int64_t j = q0 + col < q1 ? q0 + col : 0;
+    if (S <= 64) {   // one slab per lane (the common case): no clamped duplicate loads
+      const double2* src = reinterpret_cast<const double2*>(ws.qpart + ((int64_t)(sl < S ? sl : 0) * m + j) * 4);
+      pre_lo[0] = src[0];
+      pre_hi[0] = src[1];
+#pragma unroll
+      for (int u = 1; u < 4; ++u) pre_lo[u] = pre_hi[u] = make_double2(0.0, 0.0);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int su = sl + 64 * u < S ? sl + 64 * u : 0;   // clamped to slab 0
+        const double2* src = reinterpret_cast<const double2*>(ws.qpart + ((int64_t)su * m + j) * 4);
+        pre_lo[u] = src[0];
+        pre_hi[u] = src[1];
+      }
+    }
+  }
+  FIN_STAMP(ws, 1);
+  // Gram partials: wave e < 10 sums slot e, lane k taking slabs k, k + 64, ... (loads in flight
+  // together), then a fixed-order butterfly over the lanes
+  {
+    const int e = t >> 6, k = t & 63;
+    if (e < 10) {
+      double g = 0.0;
+      const int NG = 4 * S;   // 4 Gram partials per slab
+      for (int s0 = k; s0 < NG; s0 += 4 * kWave) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int su = s0 + u * kWave;
+          v[u] = ws.gpart[(int64_t)(su < NG ? su : 0) * 16 + e];   // clamped to partial 0
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g += s0 + u * kWave < NG ? v[u] : 0.0;
+      }
+      g = wave_sum(g);
+      if (k == 0) Gs[e] = g;
+    }
+  }
+  __syncthreads();
+  FIN_STAMP(ws, 2);
+  if (t == 0) {   // Cholesky with the pivot check of psgd_orth4_kernel
+    auto gi = [](int c, int c2) { return c * 4 - c * (c - 1) / 2 + (c2 - c); };
+    int robust = 0;
+    for (int c = 0; c < 4; ++c) {
+      double d = Gs[gi(c, c)];
+      for (int k = 0; k < c; ++k) d -= Rs[k][c] * Rs[k][c];
+      if (!(d > kOrthPivotMin * Gs[gi(c, c)] && isfinite(d))) robust = 1;
+      const double rcc = sqrt(d);
+      const double inv = 1.0 / rcc;
+      Rs[c][c] = rcc;
+      Rinv[c] = inv;
+      for (int c2 = c + 1; c2 < 4; ++c2) {
+        double u = Gs[gi(c, c2)];
+        for (int k = 0; k < c; ++k) u -= Rs[k][c] * Rs[k][c2];
+        Rs[c][c2] = u * inv;
+      }
+    }
+    s_robust = robust;
+  }
+  __syncthreads();
+  if (s_robust) {
+    // ill-conditioned P_raw (kappa above ~1e4): Qraw R^-1 would amplify rounding by kappa, so
+    // workgroup 0 orthogonalises P_raw in place by MGS2 (psgd_orth4_kernel's robust path) and
+    // publishes it (release fence + flag); every workgroup then computes its Q rows as M^T P
+    // directly (a second read of M, on this rare path only)
+    if (b == 0) {
+      if (n <= (int64_t)kOrth4Rows) {
+        double x[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t i = t + (int64_t)j * kOrthBlock;
+          const f32x4v v = *reinterpret_cast<const f32x4v*>(P + (i < n ? i : 0) * 4);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[j][c] = i < n ? (double)v[c] : 0.0;
+        }
+        orth_mgs2_regs<4, 4>(x, 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t i = t + (int64_t)j * kOrthBlock;
+          if (i < n) *reinterpret_cast<f32x4v*>(P + i * 4) = f32x4v{(float)x[j][0], (float)x[j][1], (float)x[j][2], (float)x[j][3]};
+        }
+      } else {
+        orth_mgs2<4>(P, n, 4);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0 && NB > 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ws.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      if (t == 0) {
+        spin_until(ws.ctl, 1u, ws.ctl + 2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+    w1_direct_q(M, P, n, m, q0, q1, Q);
+    if (b != 0 && t == 0 &&
+        __hip_atomic_fetch_add(ws.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)NB - 2) {
+      __hip_atomic_store(ws.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // last reader
+      __hip_atomic_store(ws.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  FIN_STAMP(ws, 3);
+  // P = P_raw R^-1 in place: this workgroup's rows
+  for (int64_t i = prow_i; i < min(n, (int64_t)(b + 1) * pper); i += kW1FinBlock) {
+    const f32x4v v = i == prow_i ? pv : *reinterpret_cast<const f32x4v*>(P + i * 4);
+    const double a[4] = {(double)v.x, (double)v.y, (double)v.z, (double)v.w};
+    double x[4];
+    w1_solve(a, Rs, Rinv, x);
+    *reinterpret_cast<f32x4v*>(P + i * 4) = f32x4v{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+  }
+  // Q rows, 16 columns per round (wave = column, lane = slab lane), x = Qraw R^-1
+  for (int64_t jb = q0; jb < q1; jb += 16) {
+    const int64_t j = jb + col;
+    const bool jv = j < q1;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int s0 = sl; s0 < S; s0 += 4 * 64) {   // up to 4 slabs' loads in flight
+      double2 lo[4], hi[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (jb == q0 && s0 == sl) {   // prefetched at the top
+          lo[u] = pre_lo[u];
+          hi[u] = pre_hi[u];
+          continue;
+        }
+        const int su = s0 + 64 * u < S ? s0 + 64 * u : 0;   // clamped to slab 0
+        const double2* src = reinterpret_cast<const double2*>(ws.qpart + ((int64_t)su * m + (jv ? j : 0)) * 4);
+        lo[u] = src[0];
+        hi[u] = src[1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (s0 + 64 * u < S) { a[0] += lo[u].x; a[1] += lo[u].y; a[2] += hi[u].x; a[3] += hi[u].y; }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double v = row16_sum(a[c]);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      a[c] = v;
+    }
+    if (jv && sl == 0) {
+      double x[4];
+      w1_solve(a, Rs, Rinv, x);
+      *reinterpret_cast<f32x4v*>(Q + j * 4) = f32x4v{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    }
+  }
+  FIN_STAMP(ws, 4);
+  FIN_END(ws);
+}
+
 // standard normal draws (Box-Muller on the counter-based generator), for q (powersgd.py:41)
 __global__ __launch_bounds__(256) void normal_kernel(float* __restrict__ x, int64_t n, uint64_t seed) {
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; 2 * p < n; p += (int64_t)gridDim.x * 256) {
@@ -1271,6 +1824,97 @@ grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* strea
   if (n == 0) return GRACE_OK;
   normal_kernel<<<stream_grid(n, 256, 1024), 256, 0, as_stream(stream)>>>(x, n, seed);
   GRACE_CHECK_LAUNCH("grace_normal_fill");
+  return GRACE_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// world-1 rank-4 compress (psgd_w1_pass + psgd_w1_fin).  Workspace: [ctl 256 B | arrivals and
+// read counters for kW1MaxSlabs slabs | R 256 B] at fixed offsets (the counters are left zeroed,
+// whatever the shape of the call that shares the workspace), then the shape-sized data regions.
+namespace grace {
+constexpr int64_t kW1MaxSlabs = 16384;        // n <= 1 Mi rows
+constexpr int kW1MaxCUs = 256;                // partial slots sized for <= 256 CUs (MI355X)
+
+static int64_t w1_S(int64_t n) { return (n + kW1Slab - 1) / kW1Slab; }
+static int w1_G(int64_t m) { return (int)((m + kW1Cols - 1) / kW1Cols); }
+static int64_t w1_SG_max(int64_t n, int64_t m) {
+  const int64_t cap = kW1MaxCUs / w1_G(m);
+  return min(w1_S(n), cap < 1 ? 1 : cap);
+}
+static size_t w1_align(size_t x) { return (x + 255) & ~(size_t)255; }
+static size_t w1_bytes(int64_t n, int64_t m) {
+  const int64_t S = w1_S(n);
+  return 256 + 2 * w1_align(4 * kW1MaxSlabs) + 16384 + w1_align((size_t)S * w1_G(m) * kW1Slab * 16) +
+         w1_align((size_t)S * 4 * 16 * 8) + (size_t)S * m * 32;
+}
+static W1Ws w1_carve(void* base, int64_t n, int64_t m) {
+  char* p = reinterpret_cast<char*>(base);
+  W1Ws w;
+  w.ctl = reinterpret_cast<uint32_t*>(p); p += 256;
+  w.arr = reinterpret_cast<uint32_t*>(p); p += w1_align(4 * kW1MaxSlabs);
+  w.done = reinterpret_cast<uint32_t*>(p); p += w1_align(4 * kW1MaxSlabs);
+  w.dbg = reinterpret_cast<uint64_t*>(p); p += 16384;   // diagnostic stamps only
+  w.xp = reinterpret_cast<f32x4v*>(p); p += w1_align((size_t)w1_S(n) * w1_G(m) * kW1Slab * 16);
+  w.gpart = reinterpret_cast<double*>(p); p += w1_align((size_t)w1_S(n) * 4 * 16 * 8);
+  w.qpart = reinterpret_cast<double*>(p);
+  return w;
+}
+// CUs of the current device and whether both kernels fit one workgroup per CU (cached per device)
+static int w1_cus() {
+  static int cached[64];
+  static bool init[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!init[dev]) {
+    int a = 0, b = 0, c = 0, cus = 0;
+    const bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, psgd_w1_pass<true>, kW1Block, 0) == hipSuccess &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, psgd_w1_pass<false>, kW1Block, 0) == hipSuccess &&
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, psgd_w1_fin, kW1FinBlock, 0) == hipSuccess &&
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+    cached[dev] = ok && a >= 1 && b >= 1 && c >= 1 ? cus : 0;
+    init[dev] = true;
+  }
+  return cached[dev];
+}
+}  // namespace grace
+
+extern "C" {
+
+int32_t grace_powersgd_w1_ok(int64_t n, int64_t m, int32_t r) {
+  return r == 4 && n >= 1 && m >= 4 && m % 4 == 0 && m <= (int64_t)kW1Cols * kW1MaxG && w1_S(n) <= kW1MaxSlabs &&
+                 w1_cus() >= w1_G(m)
+             ? 1 : 0;
+}
+
+size_t grace_powersgd_w1_workspace_bytes(int64_t n, int64_t m) { return w1_bytes(n, m); }
+
+grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, const float* q, uint64_t seed,
+                                          float* P, float* Q, void* ws, size_t ws_bytes, void* stream) {
+  GRACE_REQUIRE(M && P && Q && ws && grace_powersgd_w1_ok(n, m, 4), "grace_powersgd_w1_compress: bad arguments");
+  GRACE_REQUIRE(((reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(P) |
+                  reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(ws)) & 15u) == 0,
+                "grace_powersgd_w1_compress: M, q, P, Q and the workspace must be 16-B aligned");
+  if (ws_bytes < w1_bytes(n, m)) {
+    set_error_msg("grace_powersgd_w1_compress: workspace too small");
+    return GRACE_ERR_WORKSPACE;
+  }
+  const hipStream_t st = as_stream(stream);
+  const W1Ws w = w1_carve(ws, n, m);
+  const int G = w1_G(m);
+  const int64_t S = w1_S(n);
+  int64_t SG = min((int64_t)w1_cus() / G, w1_SG_max(n, m));   // one workgroup per CU: co-resident
+  if (SG < 1) SG = 1;
+  const dim3 grid((unsigned)G, (unsigned)SG);
+  if (q) psgd_w1_pass<false><<<grid, kW1Block, 0, st>>>(M, n, m, q, seed, P, w, (int)S);
+  else psgd_w1_pass<true><<<grid, kW1Block, 0, st>>>(M, n, m, q, seed, P, w, (int)S);
+  GRACE_CHECK_LAUNCH("psgd_w1_pass");
+  int64_t nb = (max(n, m) + 15) / 16;
+  nb = min(nb, min((int64_t)256, (int64_t)w1_cus()));   // one per CU at most: co-resident (robust path)
+  if (nb < 1) nb = 1;
+  psgd_w1_fin<<<(unsigned)nb, kW1FinBlock, 0, st>>>(M, P, n, m, Q, w, (int)S);   // one partial per slab
+  GRACE_CHECK_LAUNCH("psgd_w1_fin");
   return GRACE_OK;
 }
 

@@ -21,8 +21,9 @@ def orthogonalize(matrix):
 
 class PowerSGDCompressor(Compressor):
 
-    def __init__(self, rank=1, use_memory=False, world_size=1, rng="device"):
+    def __init__(self, rank=1, use_memory=False, world_size=1, rng="device", one_pass=True):
         super().__init__()
+        self.one_pass = one_pass   # world size 1, rank 4: P and Q from one read of M (psgd_w1_pass)
         self.world_size = world_size
         self.q_memory = {}
         self.rank = rank
@@ -43,6 +44,22 @@ class PowerSGDCompressor(Compressor):
         matrix = ops.dev_f32(tensor).view(shape[0], -1)
         n, m = matrix.size()
         r = min(n, m, self.rank)
+        distributed = self.world_size > 1 or (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+        if self.one_pass and not distributed and self.world_size == 1 and ops.powersgd_w1_ok(matrix, r):
+            # world size 1: nothing is all-reduced between the contractions, so P = orth(M q) and
+            # Q = M^T P come out of ONE pass over M (Q = (M^T M q) R^-1, f64 accumulation; see
+            # powersgd.hip psgd_w1_pass).  q needs no orthogonalisation first, as below.
+            if self.use_memory and name in self.q_memory:
+                p, q = ops.powersgd_w1_compress(matrix, q=self.q_memory[name])
+            elif self.rng == "torch_cpu":
+                p, q = ops.powersgd_w1_compress(matrix, q=self._normal(m, r, matrix.device, name))
+            else:
+                self._step += 1
+                p, q = ops.powersgd_w1_compress(matrix, seed=ops.step_seed("powersgd-q", name, self._step))
+            ctx = p, q, shape
+            if self.use_memory:
+                self.q_memory[name] = q
+            return [], ctx
         if self.use_memory and name in self.q_memory:
             p = ops.powersgd_p(matrix, self.q_memory[name])
         elif self.rng == "torch_cpu":

@@ -591,6 +591,26 @@ def powersgd_qt(M2d, P):
     return Q
 
 
+def powersgd_w1_ok(M2d, r):
+    """Whether the one-pass world-1 compress (grace_powersgd_w1_compress) takes this matrix."""
+    n, m = M2d.shape
+    return (M2d.is_contiguous() and M2d.data_ptr() % 16 == 0 and
+            bool(_lib.query("grace_powersgd_w1_ok", n, m, r)))
+
+
+def powersgd_w1_compress(M2d, q=None, seed=0):
+    """World-size-1 rank-4 compress in one pass over M: (P, Q) with P = orthogonalize(M q) and
+    Q = M^T P; q is the given [m x 4] matrix, or drawn from `seed` (the ops.normal stream)."""
+    n, m = M2d.shape
+    dev = M2d.device
+    P = torch.empty(n, 4, dtype=F32, device=dev)
+    Q = torch.empty(m, 4, dtype=F32, device=dev)
+    ws = workspace("powersgd_w1", _lib.query("grace_powersgd_w1_workspace_bytes", n, m), dev)
+    _lib.call("grace_powersgd_w1_compress", _p(M2d), n, m, _p(require_dev(q)) if q is not None else None,
+              int(seed) & (2 ** 64 - 1), _p(P), _p(Q), _p(ws), ws.numel(), _stream())
+    return P, Q
+
+
 def orthogonalize_(A):
     """In place: A must be a contiguous (row-major) device matrix, or the result would land on a copy."""
     if not isinstance(A, torch.Tensor) or A.device.type != "cuda":

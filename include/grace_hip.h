@@ -284,6 +284,18 @@ grace_status_t grace_orthogonalize(float* A, int64_t n, int32_t r, void* stream)
 grace_status_t grace_normal_orthogonal(float* A, int64_t n, int32_t r, uint64_t seed, void* stream);
 grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, int64_t m, int32_t r, float* out,
                                     const float* M, float* residual, void* stream);
+/* World-size-1 rank-4 compress in one pass over M (replaces the P / orthogonalize / Qt sequence
+ * of PowerSGDCompressor.compress, powersgd.py:30-56, when nothing is all-reduced in between):
+ * P = orthogonalize(M q) and Q = M^T P, with q = `q` [m x 4] if non-null, else the standard normal
+ * draws keyed by `seed` (the grace_normal_fill stream; as for grace_powersgd_p_draw, q itself need
+ * not be orthogonalised).  Qraw = M^T (M q) is accumulated in f64 and solved by the R of P's QR.
+ * Eligibility (grace_powersgd_w1_ok): r == 4, m % 4 == 0, m <= 16384, n <= 1 Mi rows; 16-B aligned
+ * pointers.  The workspace (grace_powersgd_w1_workspace_bytes) is zeroed once at allocation and
+ * left with its counters zeroed by every call. */
+int32_t grace_powersgd_w1_ok(int64_t n, int64_t m, int32_t r);
+size_t grace_powersgd_w1_workspace_bytes(int64_t n, int64_t m);
+grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, const float* q, uint64_t seed,
+                                          float* P, float* Q, void* ws, size_t ws_bytes, void* stream);
 /* standard normal fill (q draws, powersgd.py:41 / memory/powersgd.py:27), device generator */
 grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* stream);
 
