@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
                     choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd",
-                             "ddp_params", "ddp_bucket", "ddp_segmented"])
+                             "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -120,7 +120,8 @@ def main():
             dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
-           "terngrad": bench_quant, "powersgd": bench_powersgd}[args.workload]
+           "terngrad": bench_quant, "powersgd": bench_powersgd, "natural": bench_cast, "cnat": bench_cast,
+           "fp16": bench_cast}[args.workload]
     line = run(args, world, rank, dev)
     if args.workload == "topk" and world > 1 and not args.no_sharded:
         # BASELINE configs[4] (one 256 MiB bucket sharded over the ranks, top-k 0.1 %) rides in the
@@ -393,6 +394,38 @@ def bench_quant(args, world, rank, dev):
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
+    return line
+
+
+# ------------------------------------------------------------------------------------------ natural / cnat / fp16
+def bench_cast(args, world, rank, dev):
+    """Allgather(NaturalCompressor | NaturalCompressor_CUDA | FP16Compressor, NoneMemory).step on a 256 MiB
+    bucket: element-wise codecs, u8 codes (natural, cnat) or f16 (fp16)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.fp16 import FP16Compressor
+    from grace_amd.dist.compressor.natural import NaturalCompressor, NaturalCompressor_CUDA
+    from grace_amd.dist.memory.none import NoneMemory
+    n = args.numel
+    comp = {"natural": NaturalCompressor, "cnat": NaturalCompressor_CUDA, "fp16": FP16Compressor}[args.workload]()
+    comm = Allgather(comp, NoneMemory(), world)
+    nbuf = 3
+    grads = [torch.randn(n, device=dev) for _ in range(nbuf)]
+    elapsed = timed(lambda i: comm.step(grads[i % nbuf], "w"), args.steps, args.warmup, world, dev)
+    t = elapsed / args.steps
+    code_bytes = 2 if args.workload == "fp16" else 1
+    # world 1 runs the fused step (grace_cast_step_w1: read x, write the decoded f32, the codes never
+    # stored) = 8n; otherwise encode + decode move the codes too
+    alg = 8 * n if world == 1 else (8 + 2 * code_bytes) * n
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric=f"grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 {args.workload}")
+    line["config"] = {"workload": f"Allgather({type(comp).__name__}, NoneMemory).step, 256 MiB fp32", "numel": n,
+                      "rotated_buffers": nbuf}
+    traffic, ratio = pmc_traffic(args.workload, alg)
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg,
+                        "note": "8n at world 1 (fused step: x read once, the f32 result written once); "
+                                f"{8 + 2 * code_bytes}n with the codes materialised (world > 1)"}
     return line
 
 

@@ -102,6 +102,8 @@ SIGNATURES = {
     "grace_natural_decompress": (ST, [P, I64, I32, I64, I32, I32, F32, P, P]),
     "grace_fp16_compress": (ST, [P, P, I64, P]),
     "grace_fp16_decompress": (ST, [P, P, I64, P]),
+    "grace_fp16_decompress_aggregate": (ST, [P, I64, I32, I64, F32, P, P]),
+    "grace_cast_step_w1": (ST, [P, I64, I32, U64, P, P]),
     "grace_randomk_indices": (ST, [U64, I64, I64, P, P]),
     "grace_gather": (ST, [P, P, I64, P, P]),
     "grace_threshold_workspace_bytes": (SZ, [I64]),

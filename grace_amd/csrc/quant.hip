@@ -1037,6 +1037,18 @@ __device__ __forceinline__ uint32_t natural_code(float xv, int32_t r) {
   return (uint32_t)(uint8_t)((sign >> 24) | ((e >> 23) - 18));
 }
 
+// device generator of the natural codec: one rand32 hash per quad plus xorshift32 steps
+// (uniform01x4's stream), mapped onto [0, 0x7FFFFF) by a high multiply (the reference's randint
+// range; the per-element 64-bit mixes and 64-bit modulo this replaced made the encoder ALU-bound)
+__device__ __forceinline__ void natural_rand4(uint64_t seed, int64_t e, int32_t (&r)[4]) {
+  uint32_t hq = rand32(seed, (uint64_t)e);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j) { hq = hq ? hq : 0x9E3779B9u; hq ^= hq << 13; hq ^= hq >> 17; hq ^= hq << 5; }
+    r[j] = (int32_t)__umulhi(hq, 0x7FFFFFu);
+  }
+}
+
 __global__ __launch_bounds__(kQBlock) void natural_encode_kernel(const float* __restrict__ x, int64_t n,
                                                                 const int32_t* __restrict__ ri, uint64_t seed,
                                                                 uint8_t* __restrict__ codes, int aligned) {
@@ -1056,8 +1068,7 @@ __global__ __launch_bounds__(kQBlock) void natural_encode_kernel(const float* __
         for (int j = 0; j < 4; ++j) r[j] = e + j < n ? ri[e + j] : 0;
       }
     } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = (int32_t)(mix64(seed ^ mix64((uint64_t)(e + j))) % 0x7FFFFFull);
+      natural_rand4(seed, e, r);
     }
     uint32_t c[4];
 #pragma unroll
@@ -1108,8 +1119,7 @@ __global__ __launch_bounds__(kQBlock) void cnat_encode_kernel(const float* __res
     } else if (rnd) {
       load_quad(rnd, e, n, fast, r);
     } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = uniform01(seed, (uint64_t)(e + j));
+      uniform01x4(seed, (uint64_t)e, r);   // one hash per quad (device generator)
     }
     uint32_t c[4];
 #pragma unroll
@@ -1194,22 +1204,79 @@ __global__ __launch_bounds__(kQBlock) void f32_to_f16_kernel(const float* __rest
     }
   }
 }
+// f16 -> f32; with `aggregate` the W rank-major payloads at `stride` are summed in rank order from
+// 0 (Python's sum: 0 + d0 + d1 ..., allgather.py:44) and divided by `divisor` unless it is 1 --
+// the Allgather step's decompress + aggregate + divide in one pass
 __global__ __launch_bounds__(kQBlock) void f16_to_f32_kernel(const __half* __restrict__ h, float* __restrict__ x,
-                                                            int64_t n, int aligned) {
+                                                            int64_t n, int aligned, int64_t stride, int world,
+                                                            int aggregate, float divisor) {
   const int64_t nq = (n + 3) >> 2;
   for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
     const int64_t e = q << 2;
-    if (quad_fast(e, n, aligned != 0)) {
-      const uint2 wd = *reinterpret_cast<const uint2*>(h + e);
-      *reinterpret_cast<f4v*>(x + e) = f4v{__half2float(__ushort_as_half((unsigned short)wd.x)),
-                                           __half2float(__ushort_as_half((unsigned short)(wd.x >> 16))),
-                                           __half2float(__ushort_as_half((unsigned short)wd.y)),
-                                           __half2float(__ushort_as_half((unsigned short)(wd.y >> 16)))};
+    const bool fast = quad_fast(e, n, aligned != 0);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < world; ++w) {
+      const __half* hw = h + w * stride;
+      float d[4];
+      if (fast) {
+        const uint2 wd = *reinterpret_cast<const uint2*>(hw + e);
+        d[0] = __half2float(__ushort_as_half((unsigned short)wd.x));
+        d[1] = __half2float(__ushort_as_half((unsigned short)(wd.x >> 16)));
+        d[2] = __half2float(__ushort_as_half((unsigned short)wd.y));
+        d[3] = __half2float(__ushort_as_half((unsigned short)(wd.y >> 16)));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = e + j < n ? __half2float(hw[e + j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = (aggregate || w > 0) ? acc[j] + d[j] : d[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = divisor == 1.0f ? acc[j] : acc[j] / divisor;
+    if (fast) {
+      *reinterpret_cast<f4v*>(x + e) = f4v{acc[0], acc[1], acc[2], acc[3]};
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (e + j < n) x[e + j] = __half2float(h[e + j]);
+        if (e + j < n) x[e + j] = acc[j];
     }
+  }
+}
+
+// World-1 Allgather(Natural | Natural_CUDA | FP16, NoneMemory).step in ONE pass: out = 0 + dec(enc(x))
+// (the division by world size 1 is exact and omitted), with the same codes as the separate encode
+// kernels on the device generator -- the codes never reach memory (8 B per element instead of 10 / 12).
+enum CastMode : int { kCastNatural = 0, kCastCnat = 1, kCastCnatDet = 2, kCastF16 = 3 };
+template <int MODE>
+__device__ __forceinline__ float cast_round_trip(float v, float u, int32_t ri) {
+  if constexpr (MODE == kCastNatural) return 0.f + natural_dec(natural_code(v, ri));
+  else if constexpr (MODE == kCastCnat || MODE == kCastCnatDet) return 0.f + cnat_dec(cnat_code(v, u));
+  else return 0.f + __half2float(__float2half_rn(v));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kQBlock) void cast_step_w1_kernel(const float* __restrict__ x, float* __restrict__ o,
+                                                              int64_t n, uint64_t seed) {
+  const int64_t n4 = n >> 2;
+  const int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x;
+  const int64_t qq = q < n4 ? q : (n4 > 0 ? n4 - 1 : 0);
+  const f4v v = n4 > 0 ? reinterpret_cast<const f4v*>(x)[qq] : f4v{0.f, 0.f, 0.f, 0.f};
+  const int64_t e = q << 2;
+  float u[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+  int32_t r[4] = {0, 0, 0, 0};
+  if constexpr (MODE == kCastNatural) natural_rand4(seed, e, r);
+  if constexpr (MODE == kCastCnat) uniform01x4(seed, (uint64_t)e, u);
+  if (q < n4) {
+    reinterpret_cast<f4v*>(o)[q] = f4v{cast_round_trip<MODE>(v.x, u[0], r[0]), cast_round_trip<MODE>(v.y, u[1], r[1]),
+                                       cast_round_trip<MODE>(v.z, u[2], r[2]), cast_round_trip<MODE>(v.w, u[3], r[3])};
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 3)) {   // the scalar tail: one quad's generator
+    const int64_t t0 = n4 << 2;
+    float ut[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+    int32_t rt[4] = {0, 0, 0, 0};
+    if constexpr (MODE == kCastNatural) natural_rand4(seed, t0, rt);
+    if constexpr (MODE == kCastCnat) uniform01x4(seed, (uint64_t)t0, ut);
+    for (int j = 0; j < (int)(n & 3); ++j) o[t0 + j] = cast_round_trip<MODE>(x[t0 + j], ut[j], rt[j]);
   }
 }
 
@@ -1505,8 +1572,39 @@ grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n,
   if (n == 0) return GRACE_OK;
   const int al = (reinterpret_cast<uintptr_t>(half_in) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   f16_to_f32_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      reinterpret_cast<const __half*>(half_in), out, n, al);
+      reinterpret_cast<const __half*>(half_in), out, n, al, 0, 1, 0, 1.0f);
   GRACE_CHECK_LAUNCH("grace_fp16_decompress");
+  return GRACE_OK;
+}
+
+grace_status_t grace_cast_step_w1(const float* x, int64_t n, int32_t mode, uint64_t seed, float* out,
+                                  void* stream) {
+  GRACE_REQUIRE(x && out && n >= 0 && mode >= 0 && mode <= 3 &&
+                ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) == 0,
+                "grace_cast_step_w1: bad arguments (16-B aligned x and out)");
+  if (n == 0) return GRACE_OK;
+  const unsigned grid = (unsigned)(((n >> 2) + kQBlock - 1) / kQBlock > 0 ? ((n >> 2) + kQBlock - 1) / kQBlock : 1);
+  const hipStream_t st = as_stream(stream);
+  switch (mode) {
+    case kCastNatural: cast_step_w1_kernel<kCastNatural><<<grid, kQBlock, 0, st>>>(x, out, n, seed); break;
+    case kCastCnat: cast_step_w1_kernel<kCastCnat><<<grid, kQBlock, 0, st>>>(x, out, n, seed); break;
+    case kCastCnatDet: cast_step_w1_kernel<kCastCnatDet><<<grid, kQBlock, 0, st>>>(x, out, n, seed); break;
+    default: cast_step_w1_kernel<kCastF16><<<grid, kQBlock, 0, st>>>(x, out, n, seed); break;
+  }
+  GRACE_CHECK_LAUNCH("grace_cast_step_w1");
+  return GRACE_OK;
+}
+
+grace_status_t grace_fp16_decompress_aggregate(const void* half_in, int64_t stride, int32_t world, int64_t n,
+                                               float divisor, float* out, void* stream) {
+  GRACE_REQUIRE(half_in && out && n >= 0 && world >= 1 && stride >= n && divisor != 0.0f,
+                "grace_fp16_decompress_aggregate: bad arguments");
+  if (n == 0) return GRACE_OK;
+  const int al = (reinterpret_cast<uintptr_t>(half_in) & 7) == 0 && (stride & 3) == 0 &&
+                 (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  f16_to_f32_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      reinterpret_cast<const __half*>(half_in), out, n, al, stride, world, 1, divisor);
+  GRACE_CHECK_LAUNCH("grace_fp16_decompress_aggregate");
   return GRACE_OK;
 }
 

@@ -29,6 +29,21 @@ class NaturalCompressor(Compressor):
     def compress(self, tensor, name):
         return [self._encode(ops.dev_f32(tensor), name)], tensor.size()
 
+    def _w1_mode(self):
+        return 0 if self.rng == "device" else None
+
+    def _w1_seed(self, name):
+        return ops.step_seed("natural", ops.rank_of_process(), name, self._step)
+
+    def fused_step(self, communicator, tensor, name):
+        """World-1 Allgather(Natural, NoneMemory).step as ONE pass (grace_cast_step_w1): the same
+        codes as compress() on the device generator, decoded as (0 + d) / 1, never stored."""
+        mode = self._w1_mode()
+        if mode is None or not ops.w1_elementwise_ok(communicator, tensor):
+            return None
+        self._step += 1
+        return ops.cast_step_w1(tensor, mode, self._w1_seed(name))
+
     def decompress(self, tensor_compressed, shape):
         codes, = tensor_compressed
         return ops.natural_decompress(codes, shape.numel(), self.flavour).view(shape)
@@ -57,6 +72,12 @@ class NaturalCompressor(Compressor):
 
 class NaturalCompressor_CUDA(NaturalCompressor):
     flavour = 1
+
+    def _w1_mode(self):
+        return {"device": 1, "deterministic": 2}.get(self.rng)
+
+    def _w1_seed(self, name):
+        return ops.step_seed("cnat", ops.rank_of_process(), name, self._step)
 
     def _encode(self, flat, name):
         self._step += 1

@@ -482,6 +482,34 @@ def fp16_decompress(h):
     return out
 
 
+def w1_elementwise_ok(communicator, tensor):
+    """Whether a world-1 Allgather(NoneMemory) step may run as one fused element-wise pass:
+    a contiguous 16-B aligned f32 device tensor (anything else takes the unfused path)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.memory.none import NoneMemory
+    return (communicator.__class__ is Allgather and communicator.memory.__class__ is NoneMemory
+            and int(communicator.world_size) == 1 and isinstance(tensor, torch.Tensor) and tensor.is_cuda
+            and tensor.dtype == F32 and tensor.is_contiguous() and tensor.data_ptr() % 16 == 0)
+
+
+def cast_step_w1(x, mode, seed):
+    """grace_cast_step_w1: out = 0 + decompress(compress(x)) for natural (0), cnat (1), cnat
+    deterministic (2) or fp16 (3), in one pass; same shape as x."""
+    out = torch.empty_like(x)
+    _lib.call("grace_cast_step_w1", _p(x), x.numel(), int(mode), int(seed) & (2 ** 64 - 1), _p(out), _stream())
+    return out
+
+
+def fp16_decompress_aggregate(h_all, n, world, divisor=1.0):
+    """Allgather-step decode of `world` rank-major f16 payloads of n elements each:
+    ((0 + d_0) + ... + d_{W-1}) / divisor in one pass (no division when divisor == 1)."""
+    h_all = require_dev(h_all)
+    out = torch.empty(n, dtype=F32, device=h_all.device)
+    _lib.call("grace_fp16_decompress_aggregate", _p(h_all), int(n), int(world), int(n), float(divisor), _p(out),
+              _stream())
+    return out
+
+
 # ----------------------------------------------------------------------------- seeds
 def step_seed(*parts):
     """Deterministic 64-bit seed for the device generator from (rank, name, step, ...)."""

@@ -199,6 +199,17 @@ grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, in
 /* fp16 (fp16.py): round-to-nearest-even cast and back */
 grace_status_t grace_fp16_compress(const float* x, void* half_out, int64_t n, void* stream);
 grace_status_t grace_fp16_decompress(const void* half_in, float* out, int64_t n, void* stream);
+/* World-1 Allgather(compressor, NoneMemory).step of an element-wise codec in one pass:
+ * out = 0 + decompress(compress(x)); mode 0 natural (device generator keyed by seed, the
+ * grace_natural_compress stream), 1 cnat (grace_cnat_compress's device stream), 2 cnat
+ * deterministic, 3 fp16.  The codes are the separate compress kernels' bit for bit. */
+grace_status_t grace_cast_step_w1(const float* x, int64_t n, int32_t mode, uint64_t seed, float* out,
+                                  void* stream);
+/* Allgather step's decode of W rank-major f16 payloads (rank r at half_in + r * stride):
+ * out = ((0 + d_0) + d_1 + ... + d_{W-1}) / divisor (no division when divisor == 1), one pass
+ * (allgather.py:40-45 with fp16.py's decompress) */
+grace_status_t grace_fp16_decompress_aggregate(const void* half_in, int64_t stride, int32_t world, int64_t n,
+                                               float divisor, float* out, void* stream);
 
 /* Per-tensor top-k + residual over many tensors in one launch sequence (grace_amd/csrc/segtopk.hip):
  * the reference's per-parameter DDP loop (examples/dist/CIFAR10-dawndist/core.py:203-206, one

@@ -324,3 +324,61 @@ def test_byte_codecs_vectorised_edges(n, off):
     h = ops.fp16_compress(xd)
     assert np.array_equal(_np(h).view(np.uint16), O.fp16_compress(x).view(np.uint16))
     assert same_bits(_np(ops.fp16_decompress(h)), O.fp16_decode(O.fp16_compress(x)))
+
+
+@pytest.mark.parametrize("world,average", [(1, True), (2, True), (3, False)])
+def test_fp16_allgather_fused_decode(world, average):
+    """FP16Compressor.decode_aggregate_gathered (grace_fp16_decompress_aggregate): the W gathered
+    f16 payloads decoded, summed from 0 in rank order and divided by W when averaging, in one pass
+    -- bit-exact against Python's sum of the per-rank decodes (allgather.py:40-45), including -0,
+    inf/NaN and an odd length (scalar tail)."""
+    from grace_amd.dist.compressor.fp16 import FP16Compressor
+    rng = np.random.default_rng(world)
+    n = 100003
+    xs = [rng.standard_normal(n).astype(np.float32) for _ in range(world)]
+    xs[0][:4] = [-0.0, np.inf, np.nan, 7e4]
+    hs = [O.fp16_compress(x) for x in xs]
+    comp = FP16Compressor()
+    comp.average = average
+    gathered = [_t(np.concatenate(hs))]
+    out = _np(comp.decode_aggregate_gathered(gathered, (torch.float32, torch.Size([n])), world))
+    exp = np.float32(0.0) + O.fp16_decode(hs[0])
+    for h in hs[1:]:
+        exp = (exp + O.fp16_decode(h)).astype(np.float32)
+    if average:
+        exp = (exp / np.float32(world)).astype(np.float32)
+    assert same_bits(out, exp)
+
+
+def test_fp16_allgather_step_world1():
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.fp16 import FP16Compressor
+    from grace_amd.dist.memory.none import NoneMemory
+    x = np.random.default_rng(9).standard_normal((33, 65)).astype(np.float32)
+    out = _np(Allgather(FP16Compressor(), NoneMemory(), 1).step(_t(x), "w"))
+    assert out.shape == x.shape
+    assert same_bits(out.ravel(), np.float32(0.0) + O.fp16_decode(O.fp16_compress(x.ravel())))
+
+
+@pytest.mark.parametrize("cls,rng", [("natural", "device"), ("cnat", "device"), ("cnat", "deterministic"),
+                                     ("fp16", None)])
+@pytest.mark.parametrize("n", [1, 7, 4096, 1000003])
+def test_cast_world1_fused_step_equals_unfused(cls, rng, n):
+    """grace_cast_step_w1 (one pass, codes never stored) == compress -> Allgather decode at world 1
+    -> (0 + d) / 1 through the separate kernels, bit for bit, on the same device generator draws
+    (two compressors stepped in lockstep: the fused one and one whose fused path is disabled)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.fp16 import FP16Compressor
+    from grace_amd.dist.compressor.natural import NaturalCompressor, NaturalCompressor_CUDA
+    from grace_amd.dist.memory.none import NoneMemory
+    mk = {"natural": lambda: NaturalCompressor(rng=rng), "cnat": lambda: NaturalCompressor_CUDA(rng=rng),
+          "fp16": FP16Compressor}[cls]
+    fused, plain = mk(), mk()
+    plain.fused_step = lambda *a: None
+    cf, cp = Allgather(fused, NoneMemory(), 1), Allgather(plain, NoneMemory(), 1)
+    x = np.random.default_rng(n).standard_normal(n).astype(np.float32)
+    x[: min(n, 3)] = [-0.0, 3e-39, -7e4][: min(n, 3)]
+    xd = _t(x)
+    for step in range(2):
+        a, b = _np(cf.step(xd, "w")), _np(cp.step(xd, "w"))
+        assert same_bits(a, b), (cls, rng, n, step)
