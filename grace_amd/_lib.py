@@ -79,6 +79,8 @@ SIGNATURES = {
     "grace_sort_payload": (ST, [P, P, I64, I64, P, P, P, SZ, P]),
     "grace_sorted_aggregate_workspace_bytes": (SZ, [I64, I32]),
     "grace_sparse_aggregate_sorted": (ST, [P, P, I64, I64, I32, F32, P, I64, P, P]),
+    "grace_qsgd_step_w1": (ST, [P, P, P, I32, I64, I32, I32, P, U64, P, P]),
+    "grace_qsgd_seg_max": (I32, []),
     "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
     "grace_qsgd_decompress": (ST, [P, P, I64, I64, I32, P, P, I32, I64, I32, I32, I32, I32, F32, P, P]),
     "grace_qsgd_global_workspace_bytes": (SZ, []),
@@ -96,6 +98,7 @@ SIGNATURES = {
     "grace_terngrad_unit": (I32, []),
     "grace_terngrad_workspace_bytes": (SZ, [I64]),
     "grace_terngrad_compress": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
+    "grace_terngrad_step_w1": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_decompress": (ST, [P, P, I64, I64, I32, P, I32, I64, I32, F32, P, P]),
     "grace_natural_compress": (ST, [P, I64, P, U64, P, P]),
     "grace_cnat_compress": (ST, [P, I64, P, I32, U64, P, P]),

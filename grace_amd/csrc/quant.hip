@@ -211,11 +211,15 @@ __device__ __forceinline__ void uniform01x4_k(uint64_t key, uint32_t i, float (&
 
 // A 16-lane row owns a bucket of 128: each lane two quads (l16, l16 + 16; two 16-B loads), the norm is
 // one DPP row reduction; kQNB buckets per row per iteration with every load issued first.
-template <typename CodeT, int VARIANT>
+// FUSED: the world-1 Allgather step (qsgd.py:41-51 decompress, allgather.py:44 sum from 0, division by
+// 1 omitted) in the same pass: out = 0 + (norm / q) * code, written instead of the codes and norms --
+// the same arithmetic as qsgd_decode_bkt_kernel, so the result is bit-identical to compress + decode.
+template <typename CodeT, int VARIANT, bool FUSED = false>
 __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
     int nseg, int32_t nbuckets, float qf, const float* __restrict__ u, uint64_t seed,
-    const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes) {
+    const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes,
+    float* __restrict__ fused_out = nullptr) {
   __shared__ SegTables32 tab;
   stage_tables32(tab, seg_off, bkt_off, nseg);
   const int l16 = threadIdx.x & 15;
@@ -275,8 +279,9 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
 #pragma unroll
     for (int h = 0; h < kQNB; ++h) {
       if (!ok[h]) continue;
-      if (l16 == 0) norms_out[bb[h]] = norm[h];
+      if (!FUSED && l16 == 0) norms_out[bb[h]] = norm[h];
       const float scale = VARIANT == 0 ? (1.0f / norm[h]) * qf : qf / norm[h];
+      const float dsc = norm[h] / qf;   // the decoder's scale
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int32_t eq = e[h][q];
@@ -297,7 +302,25 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
           const float level = VARIANT == 0 ? scale * fabsf(v[h][q][j]) : qf / norm[h] * fabsf(v[h][q][j]);
           c[j] = qsgd_code<CodeT, VARIANT>(v[h][q][j], level, uu[j], norm[h]);
         }
-        store_codes4(codes, eq, end[h], fast[h][q], c);
+        if constexpr (FUSED) {
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float cf = (float)c[j];
+            float d = dsc * cf;
+            if (VARIANT == 1 && cf == -128.0f) d = __int_as_float(0x7FC00000);
+            o[j] = 0.f + d;
+          }
+          if (fast[h][q]) {
+            __builtin_nontemporal_store(f4v{o[0], o[1], o[2], o[3]}, reinterpret_cast<f4v*>(fused_out + eq));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (eq + j < end[h]) fused_out[eq + j] = o[j];
+          }
+        } else {
+          store_codes4(codes, eq, end[h], fast[h][q], c);
+        }
       }
     }
   }
@@ -768,10 +791,13 @@ constexpr int kTernBlock = GRACE_TERN_BLOCK;
 #define GRACE_TERN_SUB 4
 #endif   // encode workgroup (A/B: 256 beats 512 and 1024)
 
+// FUSED: the world-1 Allgather step in the same pass -- out = 0 + code * scalar (the decoder's
+// arithmetic, division by 1 omitted) written instead of the codes: bit-identical to encode + decode.
+template <bool FUSED = false>
 __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
     int nseg, const TernSlot* __restrict__ w, const float* __restrict__ u, uint64_t seed,
-    int8_t* __restrict__ codes) {
+    int8_t* __restrict__ codes, float* __restrict__ out = nullptr) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
   const int64_t unit = blockIdx.x;
@@ -813,13 +839,17 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     }
     return code;
   };
+  auto put1 = [&](int64_t i, int8_t cd) {
+    if constexpr (FUSED) out[i] = 0.f + (float)cd * scalar;
+    else codes[i] = cd;
+  };
   if (base + t < qs.a0) {
     const int64_t i = base + t;
-    codes[i] = enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i));
+    put1(i, enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i)));
   }
   if (qs.a1 + t < end) {
     const int64_t i = qs.a1 + t;
-    codes[i] = enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i));
+    put1(i, enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i)));
   }
 #pragma unroll
   for (int st = 0; st < kTernSteps; ++st) {
@@ -838,9 +868,15 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
           uniform01x4(seed, (uint64_t)i, r4);
           uu = f4v{r4[0], r4[1], r4[2], r4[3]};
         }
-        const uint32_t cw = (uint32_t)(uint8_t)enc(v.x, uu.x) | ((uint32_t)(uint8_t)enc(v.y, uu.y) << 8) |
-                            ((uint32_t)(uint8_t)enc(v.z, uu.z) << 16) | ((uint32_t)(uint8_t)enc(v.w, uu.w) << 24);
-        *reinterpret_cast<uint32_t*>(codes + i) = cw;
+        if constexpr (FUSED) {
+          __builtin_nontemporal_store(f4v{0.f + (float)enc(v.x, uu.x) * scalar, 0.f + (float)enc(v.y, uu.y) * scalar,
+                                          0.f + (float)enc(v.z, uu.z) * scalar, 0.f + (float)enc(v.w, uu.w) * scalar},
+                                      reinterpret_cast<f4v*>(out + i));
+        } else {
+          const uint32_t cw = (uint32_t)(uint8_t)enc(v.x, uu.x) | ((uint32_t)(uint8_t)enc(v.y, uu.y) << 8) |
+                              ((uint32_t)(uint8_t)enc(v.z, uu.z) << 16) | ((uint32_t)(uint8_t)enc(v.w, uu.w) << 24);
+          *reinterpret_cast<uint32_t*>(codes + i) = cw;
+        }
       }
     }
     if (st + 1 < kTernSteps) {
@@ -1358,6 +1394,30 @@ using namespace grace;
 
 extern "C" {
 
+grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg,
+                                  int64_t nbuckets, int32_t quantum_num, int32_t variant, const float* u,
+                                  uint64_t seed, float* out, void* stream) {
+  GRACE_REQUIRE(x && seg_off && bkt_off && nseg >= 1 && nseg <= kSegLds && nbuckets >= 0 &&
+                    nbuckets < (int64_t(1) << 24) && quantum_num >= 1 && out &&
+                    (variant == 0 || (variant == 1 && quantum_num < 128)),
+                "grace_qsgd_step_w1: bad arguments (bucket 128, <= kSegLds segments)");
+  if (nbuckets == 0) return GRACE_OK;
+  hipStream_t st = as_stream(stream);
+  const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
+#define GRACE_QSTEP128(CT, V)                                                                        \
+  qsgd_encode128_kernel<CT, V, true><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
+                                                              (float)quantum_num, u, seed, nullptr, nullptr, \
+                                                              nullptr, out)
+  if (variant == 1) GRACE_QSTEP128(int8_t, 1);
+  else if (quantum_num < 128) GRACE_QSTEP128(int8_t, 0);
+  else GRACE_QSTEP128(__half, 0);
+#undef GRACE_QSTEP128
+  GRACE_CHECK_LAUNCH("grace_qsgd_step_w1");
+  return GRACE_OK;
+}
+
+int32_t grace_qsgd_seg_max(void) { return kSegLds; }
+
 grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const int64_t* bkt_off,
                                    int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
                                    int32_t variant, const float* u, uint64_t seed, const float* norms_in,
@@ -1490,6 +1550,22 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
   tern_encode_kernel<<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w,
                                                                          u, seed, codes);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
+  return GRACE_OK;
+}
+
+grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, const int64_t* unit_off, int32_t nseg,
+                                     int64_t nunits, const float* clip_in, const float* u, uint64_t seed,
+                                     float* scalars, void* ws, float* out, void* stream) {
+  GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && nunits >= 1 && scalars && ws && out &&
+                    ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) == 0,
+                "grace_terngrad_step_w1: bad arguments (16-B aligned x and out)");
+  TernSlot* const w = reinterpret_cast<TernSlot*>(ws);
+  tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
+                                                                       scalars);
+  GRACE_CHECK_LAUNCH("grace_terngrad_step_w1");
+  tern_encode_kernel<true><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w,
+                                                                               u, seed, nullptr, out);
+  GRACE_CHECK_LAUNCH("grace_terngrad_step_w1");
   return GRACE_OK;
 }
 

@@ -37,6 +37,15 @@ class _QSGDBase(Compressor):
                                          u=u, seed=seed)
         return (codes, norms), tensor.size()
 
+    def fused_step(self, communicator, tensor, name):
+        """World-1 Allgather(QSGD, NoneMemory).step at bucket 128 in one pass (grace_qsgd_step_w1):
+        the codes compress() would draw (same generator step), decoded as (0 + d) / 1 and never
+        stored -- bit-identical to compress + Allgather decode."""
+        if not (ops.w1_elementwise_ok(communicator, tensor) and ops.qsgd_step_w1_ok([tensor.numel()], self.bucket_size)):
+            return None
+        u, seed = self._uniforms(tensor.numel(), name, tensor.device)
+        return ops.qsgd_step_w1(tensor.view(-1), self.quantum_num, variant=self.variant, u=u, seed=seed).view(tensor.shape)
+
     def decompress(self, tensor_compressed, ctx):
         codes, norms = tensor_compressed
         shape = ctx

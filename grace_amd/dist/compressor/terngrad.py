@@ -24,17 +24,28 @@ class TernGradCompressor(Compressor):
         self.wire = wire
         self._step = 0
 
-    def compress(self, tensor, name):
-        flat = ops.dev_f32(tensor)
+    def _uniforms(self, n, name, device):
         self._step += 1
         if self.rng == "torch_cpu":
-            u, seed = torch.empty(flat.numel()).uniform_(0, 1).to(flat.device), 0
-        else:
-            u, seed = None, ops.step_seed("terngrad", ops.rank_of_process(), name, self._step)
+            return torch.empty(n).uniform_(0, 1).to(device), 0
+        return None, ops.step_seed("terngrad", ops.rank_of_process(), name, self._step)
+
+    def compress(self, tensor, name):
+        flat = ops.dev_f32(tensor)
+        u, seed = self._uniforms(flat.numel(), name, flat.device)
         codes, scalar = ops.terngrad_compress(flat, u=u, seed=seed)
         if self.wire == "2bit":
             codes = ops.tern_pack(codes)
         return (codes, scalar), tensor.size()
+
+    def fused_step(self, communicator, tensor, name):
+        """World-1 Allgather(TernGrad, NoneMemory).step: statistics pass + one pass writing
+        0 + code * scalar (grace_terngrad_step_w1), the codes compress() would draw never stored --
+        bit-identical to compress + Allgather decode (the wire format does not matter at W=1)."""
+        if not ops.w1_elementwise_ok(communicator, tensor):
+            return None
+        u, seed = self._uniforms(tensor.numel(), name, tensor.device)
+        return ops.terngrad_step_w1(tensor.view(-1), u=u, seed=seed).view(tensor.shape)
 
     def decompress(self, tensor_compressed, ctx):
         codes, scalar = tensor_compressed

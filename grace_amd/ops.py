@@ -388,6 +388,22 @@ def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, se
     return codes, norms
 
 
+def qsgd_step_w1_ok(sizes, bucket_size):
+    return int(bucket_size) == 128 and len(sizes) <= _lib.query("grace_qsgd_seg_max")
+
+
+def qsgd_step_w1(x, quantum_num, sizes=None, variant=0, u=None, seed=0):
+    """World-1 Allgather(QSGD(q, bucket 128)).step in one pass (grace_qsgd_step_w1): the codes of
+    qsgd_compress decoded as (0 + d) / 1 without being stored; `sizes` segments as qsgd_compress."""
+    x = dev_f32(x)
+    sizes = [x.numel()] if sizes is None else sizes
+    seg_off, bkt_off, nb = seg_tables(sizes, 128, x.device)
+    out = torch.empty(x.numel(), dtype=F32, device=x.device)
+    _lib.call("grace_qsgd_step_w1", _p(x), _p(seg_off), _p(bkt_off), len(sizes), nb, int(quantum_num), int(variant),
+              _opt(u), int(seed) & (2 ** 64 - 1), _p(out), _stream())
+    return out
+
+
 def qsgd_decompress(codes, norms, quantum_num, bucket_size, n, sizes=None, variant=0, world=1,
                     aggregate=False, divisor=1.0):
     codes, norms = require_dev(codes), require_dev(norms)
@@ -430,6 +446,21 @@ def terngrad_compress(x, sizes=None, clip=None, u=None, seed=0):
     _lib.call("grace_terngrad_compress", _p(x), _p(seg_off), _p(unit_off), len(sizes), nunits, _opt(clip),
               _opt(u), int(seed) & (2 ** 64 - 1), _p(codes), _p(scalars), _p(ws), _stream())
     return codes, scalars
+
+
+def terngrad_step_w1(x, sizes=None, clip=None, u=None, seed=0):
+    """World-1 Allgather(TernGrad).step (grace_terngrad_step_w1): the statistics pass, then one pass
+    writing 0 + code * scalar for the codes terngrad_compress would draw, never storing them."""
+    x = dev_f32(x)
+    sizes = [x.numel()] if sizes is None else sizes
+    unit = _lib.query("grace_terngrad_unit")
+    seg_off, unit_off, nunits = seg_tables(sizes, unit, x.device)
+    scalars = torch.empty(len(sizes), dtype=F32, device=x.device)
+    out = torch.empty(x.numel(), dtype=F32, device=x.device)
+    ws = workspace("terngrad", _lib.query("grace_terngrad_workspace_bytes", nunits), x.device)
+    _lib.call("grace_terngrad_step_w1", _p(x), _p(seg_off), _p(unit_off), len(sizes), nunits, _opt(clip),
+              _opt(u), int(seed) & (2 ** 64 - 1), _p(scalars), _p(ws), _p(out), _stream())
+    return out
 
 
 def terngrad_decompress(codes, scalars, n, sizes=None, world=1, aggregate=False, divisor=1.0):

@@ -153,6 +153,13 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
  * qsgd_cuda.cu:320-388).  bkt_off[nseg + 1] (device) = per-segment bucket offsets, bucket =
  * ceil(n_s / bucket_size) per segment; norms_out[nbuckets] f32; codes int8 (q < 128) or fp16.
  * norms_in (optional) injects the bucket norms (parity of codewords). */
+/* World-1 Allgather(QSGD, NoneMemory).step with bucket_size 128 in one pass: out = 0 + (norm / q) *
+ * code for the codes grace_qsgd_compress would produce (same seed / u), never stored; nseg <=
+ * grace_qsgd_seg_max(). */
+grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg,
+                                  int64_t nbuckets, int32_t quantum_num, int32_t variant, const float* u,
+                                  uint64_t seed, float* out, void* stream);
+int32_t grace_qsgd_seg_max(void);
 grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const int64_t* bkt_off,
                                    int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
                                    int32_t variant, const float* u, uint64_t seed, const float* norms_in,
@@ -182,6 +189,12 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
                                        int32_t nseg, int64_t nunits, const float* clip_in, const float* u,
                                        uint64_t seed, int8_t* codes, float* scalars, void* ws,
                                        void* stream);
+/* World-1 Allgather(TernGrad, NoneMemory).step: the statistics pass, then ONE pass writing
+ * out = 0 + code * scalar for the codes grace_terngrad_compress would produce (same seed / u / clip)
+ * without storing them; scalars[nseg] are still written.  16-B aligned x and out. */
+grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, const int64_t* unit_off, int32_t nseg,
+                                     int64_t nunits, const float* clip_in, const float* u, uint64_t seed,
+                                     float* scalars, void* ws, float* out, void* stream);
 grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scalars, int64_t code_stride,
                                          int64_t scal_stride, int32_t world, const int64_t* seg_off,
                                          int32_t nseg, int64_t n, int32_t aggregate, float divisor, float* out,

@@ -382,3 +382,63 @@ def test_cast_world1_fused_step_equals_unfused(cls, rng, n):
     for step in range(2):
         a, b = _np(cf.step(xd, "w")), _np(cp.step(xd, "w"))
         assert same_bits(a, b), (cls, rng, n, step)
+
+
+@pytest.mark.parametrize("cls,q", [("qsgd", 127), ("qsgd", 255), ("qsgd_cuda", 127)])
+def test_qsgd_world1_fused_step_equals_unfused(cls, q):
+    """grace_qsgd_step_w1 == compress -> Allgather decode at world 1, bit for bit (same device
+    generator draws, and the injected torch_cpu stream), on a tensor with a ragged last bucket and
+    NaN / Inf / zero buckets; plus the segmented ResNet-50 set through ops.qsgd_step_w1."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.qsgd import QSGDCompressor, QSGDCompressor_CUDA
+    from grace_amd.dist.memory.none import NoneMemory
+    mk = QSGDCompressor if cls == "qsgd" else QSGDCompressor_CUDA
+    x = (np.random.default_rng(q).standard_normal(100003) * 0.01).astype(np.float32)
+    x[128:256] = 0.0
+    x[300] = np.inf
+    x[700] = np.nan
+    for rng in ("device", "torch_cpu"):
+        fused, plain = mk(q, 128, rng=rng), mk(q, 128, rng=rng)
+        plain.fused_step = lambda *a: None
+        cf, cp = Allgather(fused, NoneMemory(), 1), Allgather(plain, NoneMemory(), 1)
+        for step in range(2):
+            torch.manual_seed(step)
+            a = _np(cf.step(_t(x), "w"))
+            torch.manual_seed(step)
+            b = _np(cp.step(_t(x), "w"))
+            assert same_bits(a, b), (cls, q, rng, step)
+    from bench import resnet50_shapes
+    sizes = [int(np.prod(s)) for s in resnet50_shapes()]
+    flat = _t((np.random.default_rng(1).standard_normal(sum(sizes)) * 0.01).astype(np.float32))
+    variant = 0 if cls == "qsgd" else 1
+    codes, norms = ops.qsgd_compress(flat, q, 128, sizes=sizes, variant=variant, seed=7)
+    dec = ops.qsgd_decompress(codes, norms, q, 128, flat.numel(), sizes=sizes, variant=variant, aggregate=True)
+    assert same_bits(_np(ops.qsgd_step_w1(flat, q, sizes=sizes, variant=variant, seed=7)), _np(dec))
+
+
+def test_terngrad_world1_fused_step_equals_unfused():
+    """grace_terngrad_step_w1 == compress -> Allgather decode at world 1, bit for bit (device draws
+    and the injected torch_cpu stream, int8 and 2-bit wires), ragged tail and a zero tensor; plus the
+    segmented ResNet-50 set through ops.terngrad_step_w1 against terngrad_compress/decompress."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.terngrad import TernGradCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    x = (np.random.default_rng(5).standard_normal(100003) * 0.01).astype(np.float32)
+    for xin in (x, np.zeros(4099, np.float32)):
+        for rng in ("device", "torch_cpu"):
+            for wire in ("int8", "2bit"):
+                fused, plain = TernGradCompressor(rng=rng, wire=wire), TernGradCompressor(rng=rng, wire=wire)
+                plain.fused_step = lambda *a: None
+                cf, cp = Allgather(fused, NoneMemory(), 1), Allgather(plain, NoneMemory(), 1)
+                for step in range(2):
+                    torch.manual_seed(step)
+                    a = _np(cf.step(_t(xin), "w"))
+                    torch.manual_seed(step)
+                    b = _np(cp.step(_t(xin), "w"))
+                    assert same_bits(a, b), (rng, wire, step, xin.size)
+    from bench import resnet50_shapes
+    sizes = [int(np.prod(s)) for s in resnet50_shapes()]
+    flat = _t((np.random.default_rng(2).standard_normal(sum(sizes)) * 0.01).astype(np.float32))
+    codes, scal = ops.terngrad_compress(flat, sizes=sizes, seed=9)
+    dec = ops.terngrad_decompress(codes, scal, flat.numel(), sizes=sizes, aggregate=True)
+    assert same_bits(_np(ops.terngrad_step_w1(flat, sizes=sizes, seed=9)), _np(dec))
