@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
-                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "powersgd",
+                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "qsgd_step", "terngrad_step", "powersgd",
                              "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
@@ -119,7 +119,7 @@ def main():
         else:
             dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
-           "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant,
+           "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant, "qsgd_step": bench_quant, "terngrad_step": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd, "natural": bench_cast, "cnat": bench_cast,
            "fp16": bench_cast}[args.workload]
     line = run(args, world, rank, dev)
@@ -371,7 +371,17 @@ def bench_quant(args, world, rank, dev):
     total = sum(sizes)
     nbuf = 3
     flats = [torch.randn(total, device=dev) * 0.01 for _ in range(nbuf)]
-    if args.workload == "qsgd":
+    if args.workload == "qsgd_step":
+        # world-1 Allgather(QSGD(127, 128)).step fused (grace_qsgd_step_w1): x read once, out written once
+        def step(i):
+            return ops.qsgd_step_w1(flats[i % nbuf], 127, sizes=sizes, seed=i)
+        alg = 8 * total
+    elif args.workload == "terngrad_step":
+        # statistics pass (read x) + fused encode/decode pass (read x, write out)
+        def step(i):
+            return ops.terngrad_step_w1(flats[i % nbuf], sizes=sizes, seed=i)
+        alg = 12 * total + 4 * len(sizes)
+    elif args.workload == "qsgd":
         def step(i):
             x = flats[i % nbuf]
             codes, norms = ops.qsgd_compress(x, 127, 128, sizes=sizes, seed=i)
@@ -388,7 +398,9 @@ def bench_quant(args, world, rank, dev):
     t = elapsed / args.steps
     line = base_line(args, world, elapsed, 4.0 * total,
                      metric=f"grad-codec GB/s (device-resident encode+decode), ResNet-50 set {args.workload}")
-    line["config"] = {"workload": f"{args.workload} compress+decompress, 161 ResNet-50 tensors in one segmented "
+    what = ("world-1 fused Allgather step (codes never stored)" if args.workload.endswith("_step")
+            else "compress+decompress")
+    line["config"] = {"workload": f"{args.workload} {what}, 161 ResNet-50 tensors in one segmented "
                                   "launch per stage (BASELINE configs[2])", "numel": total, "tensors": len(sizes)}
     traffic, ratio = pmc_traffic(args.workload, alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
