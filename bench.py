@@ -216,11 +216,45 @@ def bench_topk(args, world, rank, dev):
                 roofline["traffic"] = pmc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
+    # the fraction against a copy bandwidth measured on this box as well
+    copy_gbs = measured_copy_gbs(dev)
+    roofline["measured_copy_gbs"] = copy_gbs
+    roofline["measured_copy_kind"] = "torch copy_, 1 GiB -> 1 GiB, read + write bytes"
+    roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
     line["roofline"] = roofline
     line["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_steps > 0:
         line["cpu_baseline"] = cpu_baseline_topk(n, args.ratio, args.cpu_baseline_steps)
     return line
+
+
+def measured_copy_gbs(dev, nbytes=1 << 30, reps=10):
+    """Device-to-device copy bandwidth (read + write bytes / time) of torch's copy kernel on 1 GiB
+    buffers (4x the Infinity Cache), median of `reps` event-timed copies."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dst.copy_(src)
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e-3)
+    del src, dst
+    return round(2 * nbytes / sorted(ts)[len(ts) // 2] / 1e9, 1)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline_topk(n, ratio, steps):
@@ -237,8 +271,11 @@ def cpu_baseline_topk(n, ratio, steps):
         _, _, _, r, _ = O.topk_residual_step(g, r, ratio)
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{steps} full 256 MiB top-k 1% + residual steps of oracle/grace_oracle.py "
-                      f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step"}
+                      f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step",
+            "note": "conservative: the oracle's numpy partition is faster than the reference's torch.topk "
+                    "path (SURVEY.md §6 timed the reference itself at 1,843 ms/step on the 8-core build container)"}
 
 
 def bench_topk_e2e(args, world, rank, dev):
