@@ -257,6 +257,10 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 #endif
 // variance inflation allowed for in the bracket's margin (design effect of clustered samples)
 constexpr double kSampleDeff = GRACE_SAMPLE_DEFF;
+#ifndef GRACE_SAMPLE_SIGMA
+#define GRACE_SAMPLE_SIGMA 6.0
+#endif
+constexpr double kSampleSigma = GRACE_SAMPLE_SIGMA;        // bracket half-width in binomial sigmas
 constexpr int kSamplePer = GRACE_SAMPLE_PER;               // samples per thread: 1 is fastest --
                                                            // the strided samples are latency-bound
                                                            // random loads that want many waves
@@ -314,8 +318,8 @@ __device__ void bracket_select(const StepArgs& a, const TopkWs& w, uint32_t* lh)
   const double p = (double)a.k / (double)a.n;
   const double mu = p * (double)S;
   const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
-  const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
-  const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
+  const int64_t rank_hi = (int64_t)floor(mu - kSampleSigma * sd - 2.0);   // < 0: nothing is "sure"
+  const int64_t rank_lo = (int64_t)ceil(mu + kSampleSigma * sd + 2.0);    // >= S: everything a candidate
   const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
                           (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1)};
   // descending scan: thread t owns the chunk of bins [PER*(NT-1-t), PER*(NT-1-t)+PER)
@@ -445,8 +449,8 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   const double p = (double)a.k / (double)a.n;
   const double mu = p * (double)S;
   const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
-  const int64_t rank_hi = (int64_t)floor(mu - 6.0 * sd - 2.0);   // < 0: nothing is "sure"
-  const int64_t rank_lo = (int64_t)ceil(mu + 6.0 * sd + 2.0);    // >= S: everything a candidate
+  const int64_t rank_hi = (int64_t)floor(mu - kSampleSigma * sd - 2.0);   // < 0: nothing is "sure"
+  const int64_t rank_lo = (int64_t)ceil(mu + kSampleSigma * sd + 2.0);    // >= S: everything a candidate
   // third target: the sample's estimate of the k-th rank itself, for the provisional selection
   const int64_t rank_mid = (int64_t)floor(mu);
   const uint32_t r1[3] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
