@@ -76,9 +76,8 @@ SIGNATURES = {
     "grace_sparse_aggregate": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),
     "grace_sparse_aggregate_into": (ST, [P, P, I64, P, I32, F32, P, P, I64, P]),
     "grace_sort_payload_workspace_bytes": (SZ, [I64, I64]),
-    "grace_sort_payload": (ST, [P, P, I64, I64, P, P, P, SZ, P]),
-    "grace_sorted_aggregate_workspace_bytes": (SZ, [I64, I32]),
-    "grace_sparse_aggregate_sorted": (ST, [P, P, I64, I64, I32, F32, P, I64, P, P]),
+    "grace_sort_payload": (ST, [P, P, I64, I64, P, P, P, P, SZ, P]),
+    "grace_sparse_aggregate_sorted": (ST, [P, P, P, I64, I32, F32, P, I64, P]),
     "grace_qsgd_step_w1": (ST, [P, P, P, I32, I64, I32, I32, P, U64, P, P]),
     "grace_qsgd_seg_max": (I32, []),
     "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),

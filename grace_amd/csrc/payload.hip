@@ -8,7 +8,8 @@
 // needed and costs ~10x more), and the decode is one pass over the OUTPUT: a workgroup per chunk
 // finds every rank's sub-range of that chunk from a boundary table, accumulates the ranks in
 // order in LDS -- ((0 + d0) + d1) + ... exactly as Python's sum -- divides, and writes the chunk
-// densely, which also replaces the zero-fill.
+// densely, which also replaces the zero-fill.  Each rank's chunk end offsets (a by-product of the
+// grouping) travel with its payload, so the receiver needs no pass to find the sub-ranges.
 
 #include "common.h"
 
@@ -131,53 +132,68 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
   }
 }
 
-// start[w][c] = first entry of rank w whose index is in chunk >= c  (c = 0 .. nchunks)
-__global__ __launch_bounds__(kPBlock) void chunk_bounds_kernel(const int32_t* __restrict__ idx, int64_t stride,
-                                                              int64_t per, int world, int64_t nchunks,
-                                                              int32_t* __restrict__ start) {
-  const int64_t total = per * world;
-  for (int64_t t = (int64_t)blockIdx.x * kPBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kPBlock) {
-    const int64_t w = t / per, j = t - w * per;
-    const int32_t* iw = idx + w * stride;
-    const int64_t c = (int64_t)iw[j] >> kPChunkLog;
-    const int64_t cp = j > 0 ? ((int64_t)iw[j - 1] >> kPChunkLog) : -1;
-    int32_t* sw = start + w * (nchunks + 1);
-    for (int64_t ch = cp + 1; ch <= c; ++ch) sw[ch] = (int32_t)j;
-    if (j == per - 1)
-      for (int64_t ch = c + 1; ch <= nchunks; ++ch) sw[ch] = (int32_t)per;
-  }
-}
-
+// One workgroup per 8192-element output chunk.  Rank w's entries of chunk c are [ends_w[c - 1],
+// ends_w[c]) of its grouped payload (the chunk end offsets travel with the payload, so no receiver
+// pass rebuilds them).  The bounds of every rank go to LDS in one round trip; then, kRankBatch ranks
+// at a time, every thread loads its entry of each rank of the batch (all loads in flight together)
+// and the entries are added into the LDS tile rank by rank -- ((0 + d0) + d1) + ... exactly as
+// Python's sum, since indices are unique within a rank and a barrier separates the ranks.  Ranks
+// with more than kPBlock entries in the chunk finish their remaining rounds in order before the
+// next rank.  The tile is divided and written densely (the zero-fill included).
+constexpr int kRankBatch = 8;
+constexpr int kMaxRanks = 1024;
 __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* __restrict__ vals,
-                                                                  const int32_t* __restrict__ idx, int64_t stride,
-                                                                  int world, int64_t nchunks,
-                                                                  const int32_t* __restrict__ start, float divisor,
+                                                                  const int32_t* __restrict__ idx,
+                                                                  const int32_t* __restrict__ ends, int64_t stride,
+                                                                  int world, float divisor,
                                                                   float* __restrict__ out, int64_t n) {
   __shared__ float tile[kPChunk];
+  __shared__ int32_t s_b[2 * kMaxRanks];
+  const int t = threadIdx.x;
   const int64_t ch = blockIdx.x;
   const int64_t c0 = ch << kPChunkLog;
-  for (int e = threadIdx.x; e < kPChunk; e += kPBlock) tile[e] = 0.f;
+  for (int w = t; w < world; w += kPBlock) {
+    const int32_t* ew = ends + (int64_t)w * stride;
+    s_b[2 * w] = ch > 0 ? ew[ch - 1] : 0;
+    s_b[2 * w + 1] = ew[ch];
+  }
+  for (int e = t; e < kPChunk; e += kPBlock) tile[e] = 0.f;
   __syncthreads();
-  for (int w = 0; w < world; ++w) {
-    const int32_t* sw = start + (int64_t)w * (nchunks + 1);
-    const int32_t s0 = sw[ch], s1 = sw[ch + 1];
-    const float* vw = vals + (int64_t)w * stride;
-    const int32_t* iw = idx + (int64_t)w * stride;
-    for (int32_t p = s0 + threadIdx.x; p < s1; p += kPBlock) {
-      const int32_t l = (int32_t)(iw[p] - c0);
-      tile[l] = tile[l] + vw[p];     // indices are unique within a rank: no conflicts
+  for (int w0 = 0; w0 < world; w0 += kRankBatch) {
+    int32_t l[kRankBatch];
+    float v[kRankBatch];
+#pragma unroll
+    for (int q = 0; q < kRankBatch; ++q) {   // unconditional (clamped) loads: all in flight at once
+      const int w = w0 + q < world ? w0 + q : w0;
+      const int32_t p = s_b[2 * w] + t;
+      const bool ok = w0 + q < world && p < s_b[2 * w + 1];
+      const int64_t pc = (int64_t)w * stride + (ok ? p : 0);
+      const int32_t li = idx[pc];
+      v[q] = vals[pc];
+      l[q] = ok ? (int32_t)(li - c0) : -1;
     }
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kRankBatch; ++q) {
+      const int w = w0 + q;
+      if (w >= world) break;
+      if (l[q] >= 0) tile[l[q]] = tile[l[q]] + v[q];
+      const int32_t s1 = s_b[2 * w + 1];
+      for (int32_t p = s_b[2 * w] + kPBlock + t; p < s1; p += kPBlock) {   // rare: > 256 entries
+        const int32_t lp = (int32_t)(idx[(int64_t)w * stride + p] - c0);
+        tile[lp] = tile[lp] + vals[(int64_t)w * stride + p];
+      }
+      __syncthreads();
+    }
   }
   typedef float f4 __attribute__((ext_vector_type(4)));
   if (c0 + kPChunk <= n && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
-    for (int e = threadIdx.x * 4; e < kPChunk; e += kPBlock * 4) {
+    for (int e = t * 4; e < kPChunk; e += kPBlock * 4) {
       f4 q = {tile[e], tile[e + 1], tile[e + 2], tile[e + 3]};
       if (divisor != 1.0f) { q.x = q.x / divisor; q.y = q.y / divisor; q.z = q.z / divisor; q.w = q.w / divisor; }
       __builtin_nontemporal_store(q, reinterpret_cast<f4*>(out + c0 + e));
     }
   } else {
-    for (int e = threadIdx.x; e < kPChunk && c0 + e < n; e += kPBlock)
+    for (int e = t; e < kPChunk && c0 + e < n; e += kPBlock)
       out[c0 + e] = divisor != 1.0f ? tile[e] / divisor : tile[e];
   }
 }
@@ -190,26 +206,24 @@ extern "C" {
 
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
   (void)k;
-  const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  // the ticket first (left zeroed by every call, at a fixed place whatever n), then the counts: a
-  // ticket placed after the n-sized counts landed on a larger earlier call's counts
-  return 256 + sizeof(uint32_t) * (size_t)nchunks + 256;
+  (void)n;
+  return 256;   // the arrival ticket, left zeroed by every call
 }
 
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is
-// unspecified -- the aggregate does not depend on it)
+// unspecified -- the aggregate does not depend on it); ends_out[c] = end of chunk c's entries
 grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t k, int64_t n, float* vals_out,
-                                  int32_t* idx_out, void* ws, size_t ws_bytes, void* stream) {
+                                  int32_t* idx_out, uint32_t* ends_out, void* ws, size_t ws_bytes, void* stream) {
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  GRACE_REQUIRE(vals && idx && vals_out && idx_out && ws && k >= 0 && k < ((int64_t)1 << 31) && n >= 1 &&
-                    nchunks <= kMaxGroupChunks && ws_bytes >= grace_sort_payload_workspace_bytes(k, n),
+  GRACE_REQUIRE(vals && idx && vals_out && idx_out && ends_out && ws && k >= 0 && k < ((int64_t)1 << 31) &&
+                    n >= 1 && nchunks <= kMaxGroupChunks && ws_bytes >= grace_sort_payload_workspace_bytes(k, n),
                 "grace_sort_payload: bad arguments (n <= 2^28)");
-  if (k == 0) return GRACE_OK;
   hipStream_t s = as_stream(stream);
   uint32_t* ticket = reinterpret_cast<uint32_t*>(ws);
-  uint32_t* counts = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + 256);
+  uint32_t* counts = ends_out;   // counts -> exclusive offsets (hist) -> chunk ends (scatter cursors)
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
   if (e != hipSuccess) { set_error("grace_sort_payload", e); return GRACE_ERR_HIP; }
+  if (k == 0) return GRACE_OK;
   const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
   const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
   group_hist_kernel<<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
@@ -219,24 +233,15 @@ grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t
   return GRACE_OK;
 }
 
-size_t grace_sorted_aggregate_workspace_bytes(int64_t n, int32_t world) {
-  const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  return sizeof(int32_t) * (size_t)(nchunks + 1) * (size_t)world + 256;
-}
-
-grace_status_t grace_sparse_aggregate_sorted(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
-                                             int32_t world, float divisor, float* out, int64_t n, void* ws,
+grace_status_t grace_sparse_aggregate_sorted(const float* vals, const int32_t* idx, const uint32_t* ends,
+                                             int64_t stride, int32_t world, float divisor, float* out, int64_t n,
                                              void* stream) {
-  GRACE_REQUIRE(vals && idx && out && ws && per >= 1 && world >= 1 && n >= 1,
-                "grace_sparse_aggregate_sorted: bad arguments");
+  GRACE_REQUIRE(vals && idx && ends && out && world >= 1 && world <= kMaxRanks && n >= 1 &&
+                    (n + kPChunk - 1) / kPChunk <= kMaxGroupChunks,
+                "grace_sparse_aggregate_sorted: bad arguments (1 <= world <= 1024, n <= 2^28)");
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  int32_t* start = reinterpret_cast<int32_t*>(ws);
-  hipStream_t s = as_stream(stream);
-  chunk_bounds_kernel<<<stream_grid(per * world, kPBlock, 4096), kPBlock, 0, s>>>(idx, stride, per, world, nchunks,
-                                                                                 start);
-  GRACE_CHECK_LAUNCH("grace_sparse_aggregate_sorted");
-  chunk_accumulate_kernel<<<(unsigned)nchunks, kPBlock, 0, s>>>(vals, idx, stride, world, nchunks, start, divisor,
-                                                                out, n);
+  chunk_accumulate_kernel<<<(unsigned)nchunks, kPBlock, 0, as_stream(stream)>>>(
+      vals, idx, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
   GRACE_CHECK_LAUNCH("grace_sparse_aggregate_sorted");
   return GRACE_OK;
 }

@@ -1148,10 +1148,22 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
     // provisionally selected ones still need their fix-ups -> route with the boundary above all bins
     if (MODE == kDenseFused && B < 0) B = kHistBins;
     // residual-only mode: sure entries still hold t in r; zero them now
+    // (kFinPer entries per thread per round, every load issued before any store: one dependent
+    // load -> store chain per entry made this 14 us of the finalize at k = 671 K)
     if constexpr (MODE == kDenseRes) {
-      for (uint32_t j = fi * BLOCK + t; j < n_sure; j += fcnt * BLOCK) {
-        const float v = ld_f32<AG>(a.vals + j);
-        a.r[(int32_t)ld_u32<AG>(reinterpret_cast<const uint32_t*>(a.idx) + j)] = v - v;
+      const uint32_t stride = (uint32_t)(fcnt * BLOCK);
+      for (uint32_t j0 = fi * BLOCK + t; j0 < n_sure; j0 += stride * kFinPer) {
+        float v[kFinPer];
+        uint32_t ix[kFinPer];
+#pragma unroll
+        for (int u = 0; u < kFinPer; ++u) {
+          const uint32_t j = j0 + u * stride < n_sure ? j0 + u * stride : j0;   // clamped, unconditional
+          v[u] = ld_f32<AG>(a.vals + j);
+          ix[u] = ld_u32<AG>(reinterpret_cast<const uint32_t*>(a.idx) + j);
+        }
+#pragma unroll
+        for (int u = 0; u < kFinPer; ++u)
+          if (j0 + u * stride < n_sure) a.r[(int32_t)ix[u]] = v[u] - v[u];
       }
     }
     if (B >= 0) {
@@ -1323,9 +1335,19 @@ __global__ __launch_bounds__(kSelBlock) void topk_shard_route(StepArgs a, TopkWs
   const TopkCtl c = *w.ctl;
   const int t = threadIdx.x;
   const int64_t base = a.idx_base;
-  for (uint32_t j = blockIdx.x * kSelBlock + t; j < c.n_sure; j += gridDim.x * kSelBlock) {
-    const float v = a.vals[j];
-    a.r[a.idx[j] - base] = v - v;
+  const uint32_t stride = gridDim.x * kSelBlock;
+  for (uint32_t j0 = blockIdx.x * kSelBlock + t; j0 < c.n_sure; j0 += stride * kFinPer) {
+    float v[kFinPer];
+    int32_t ix[kFinPer];
+#pragma unroll
+    for (int u = 0; u < kFinPer; ++u) {   // every load before any store (no dependent chains)
+      const uint32_t j = j0 + u * stride < c.n_sure ? j0 + u * stride : j0;
+      v[u] = a.vals[j];
+      ix[u] = a.idx[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kFinPer; ++u)
+      if (j0 + u * stride < c.n_sure) a.r[ix[u] - base] = v[u] - v[u];
   }
   int2* blist = reinterpret_cast<int2*>(bsend + 1);
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];

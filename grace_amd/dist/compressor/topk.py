@@ -79,7 +79,7 @@ class TopKCompressor(Compressor):
         # sort the local payload by index, exchange, then decode all W payloads in one pass over the
         # output (grace_amd/csrc/payload.hip) instead of W random scatters
         sbuf = ops.sort_payload(buf, k, n)
-        gathered = torch.empty(world * 2 * k, dtype=torch.float32, device=g.device)
+        gathered = torch.empty(world * sbuf.numel(), dtype=torch.float32, device=g.device)
         dist.all_gather_into_tensor(gathered, sbuf)
         out = ops.sparse_aggregate_sorted(gathered, k, world, n, divisor)
         return out.view(tensor.shape)

@@ -224,10 +224,13 @@ def test_sparse_aggregate_rank_ordered(world, n, k):
     buf = _t(payload)
     # chunk-grouped payloads (grace_sort_payload) for the one-pass aggregate
     sorted_buf = torch.cat([G.sort_payload(buf[w * 2 * k:(w + 1) * 2 * k], k, n) for w in range(world)])
+    L = ops.sorted_payload_len(k, n)
     for w in range(world):
-        idx_s = _np(sorted_buf[w * 2 * k + k:(w + 1) * 2 * k].view(torch.int32))
-        vals_s = _np(sorted_buf[w * 2 * k:w * 2 * k + k])
+        idx_s = _np(sorted_buf[w * L + k:w * L + 2 * k].view(torch.int32))
+        vals_s = _np(sorted_buf[w * L:w * L + k])
+        ends = _np(sorted_buf[w * L + 2 * k:(w + 1) * L].view(torch.int32))
         assert np.all(np.diff(idx_s >> 13) >= 0)                       # grouped by 8192-chunk
+        assert np.array_equal(ends, np.searchsorted(idx_s >> 13, np.arange(L - 2 * k), side="right"))
         order = np.argsort(idx_s)
         assert np.array_equal(idx_s[order], np.sort(idx_l[w]))        # same entries
         assert same_bits(vals_s[order], vals_l[w][np.argsort(idx_l[w])])
@@ -251,7 +254,7 @@ def test_sort_payload_workspace_reuse_across_sizes():
         vals = rng.standard_normal(k).astype(np.float32)
         buf = torch.cat([torch.from_numpy(vals), torch.from_numpy(idx.view(np.float32))]).to(dev)
         out = ops.sort_payload(buf, k, n).cpu().numpy()
-        ov, oi = out[:k], out[k:].view(np.int32)
+        ov, oi = out[:k], out[k:2 * k].view(np.int32)
         assert np.all(np.diff(oi // 8192) >= 0), (n, k)
         order = np.argsort(idx)
         o2 = np.argsort(oi)
