@@ -22,7 +22,7 @@
 //                               thr_lo <= key <= thr_hi -> candidate list + 2048-bin histogram
 //                               of the candidate key range.  Appends use wave64 ballot + mbcnt
 //                               into LDS staging, one global atomic per workgroup and list.
-//   4. finalize (64 WGs)        every WG finds the boundary bin B from the global histogram;
+//   4. finalize (128 WGs)       every WG finds the boundary bin B from the global histogram;
 //                               candidates above B go to the payload and those in B to a short
 //                               boundary list (block scan + one atomic per round); the last WG
 //                               to arrive selects the final `need` entries of B by (key, -idx).
@@ -59,7 +59,7 @@ constexpr int kSampleRunLen = 16;
 constexpr int kSampleRuns = 2048;
 constexpr int kSample = kSampleRuns * kSampleRunLen;       // 32768 keys, 32 per thread
 #ifndef GRACE_FIN_BLOCKS
-#define GRACE_FIN_BLOCKS 64
+#define GRACE_FIN_BLOCKS 128
 #endif
 constexpr int kFinBlocks = GRACE_FIN_BLOCKS;
 constexpr int kFinPer = 8;                                 // candidates per thread per round
@@ -834,6 +834,18 @@ struct MainTs {
     const float o = ld_f32<AG>(out + i), rr = ld_f32<AG>(r + i);   // both issued: no dependent load
     return f2u(o) != 0u ? o : rr;
   }
+  // four consecutive elements (i % 4 == 0, 16-B aligned buffers): 16-B loads unless AG
+  __device__ float4 quad(int64_t i) const {
+    if constexpr (AG) {
+      return make_float4((*this)(i), (*this)(i + 1), (*this)(i + 2), (*this)(i + 3));
+    } else {
+      if constexpr (MODE == kDenseNone) return *reinterpret_cast<const float4*>(g + i);
+      if constexpr (MODE == kDenseRes) return *reinterpret_cast<const float4*>(r + i);
+      const float4 o = *reinterpret_cast<const float4*>(out + i), rr = *reinterpret_cast<const float4*>(r + i);
+      return make_float4(f2u(o.x) != 0u ? o.x : rr.x, f2u(o.y) != 0u ? o.y : rr.y, f2u(o.z) != 0u ? o.z : rr.z,
+                         f2u(o.w) != 0u ? o.w : rr.w);
+    }
+  }
 };
 
 // the boundary list into LDS (pairwise-ranking case); issued by the last workgroup BEFORE its own
@@ -942,7 +954,7 @@ __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[k
 
 // ---- parallel exact fallback (the sampled bracket missed or a list overflowed: in practice massive
 // ties, e.g. a bucket that is mostly exact zeros, or a constant one).  All finalize workgroups
-// (co-resident: 64 of them) radix-select the k-th largest KEY over the whole bucket together, one
+// (co-resident: 128 of them) radix-select the k-th largest KEY over the whole bucket together, one
 // digit per pass with a grid barrier after each global histogram merge (3 passes); the ties at that
 // key are then taken lowest index first straight from per-slice counts: a count pass and an
 // ordered write pass, each slice in index order after exclusive scans of the (key > T, key == T)
@@ -969,18 +981,53 @@ __device__ __forceinline__ void grid_barrier(const TopkWs& w, int fcnt) {
   __syncthreads();
 }
 
-constexpr int kFbUnroll = 8;   // parallel fallback: elements in flight per thread
+constexpr int kFbUnroll = 8;   // parallel fallback: elements per thread per ordered-write round
+constexpr int kFbQ = 8;        // parallel fallback: quads in flight per thread (histogram / count passes)
+
+// one key into the LDS histogram, wave-aggregated for the bin of the wave's first active lane:
+// degenerate buckets (ties: all zeros, a constant) put every key in one bin, and a workgroup's LDS
+// atomics on one address serialise (the loop exits can leave lanes inactive, hence the lead lane)
+__device__ __forceinline__ void hist_add_agg(uint32_t* hist, int bin) {
+  const int b0 = __builtin_amdgcn_readfirstlane(bin);
+  const uint64_t same = __ballot(bin == b0);
+  const int lead = __ffsll((unsigned long long)__ballot(1)) - 1;
+  if (bin >= 0 && bin != b0) atomicAdd(&hist[bin], 1u);
+  if (b0 >= 0 && (int)(threadIdx.x & 63) == lead) atomicAdd(&hist[b0], (uint32_t)__popcll(same));
+}
 
 template <int MODE, int BLOCK, bool AG>
 __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
   const int t = threadIdx.x;
   const uint32_t k = (uint32_t)a.k;
-  const int64_t per = (a.n + fcnt - 1) / fcnt;
+  // slices of whole quads (16-B loads) when the buffers are 16-B aligned; [q1, s1) is a scalar tail
+  const bool vq = !AG && ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r) |
+                           reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
+  int64_t per = (a.n + fcnt - 1) / fcnt;
+  if (vq) per = (per + 3) & ~(int64_t)3;
   const int64_t s0 = min((int64_t)fi * per, a.n), s1 = min(s0 + per, a.n);
+  const int64_t q1 = vq ? s0 + ((s1 - s0) & ~(int64_t)3) : s0;
   uint32_t* gh = w.shist;                      // [3][2048] key-digit histograms
   uint32_t* cnt = w.shist + 3 * 2048;          // [fcnt][2] per-slice (key > T, key == T) counts
   if (fi == 0 && t == 0) w.ctl->status = 1;
   const MainTs<MODE, AG> f{a.g, a.r, a.out};
+  // fn(key) for every element of the slice, in no particular order; every load of a round issued
+  // before any key is used
+  auto for_keys = [&](auto&& fn) {
+    for (int64_t b = s0 + 4 * (int64_t)t; b < q1; b += 4 * (int64_t)BLOCK * kFbQ) {
+      float4 v[kFbQ];
+#pragma unroll
+      for (int u = 0; u < kFbQ; ++u) {
+        const int64_t i = b + 4 * (int64_t)u * BLOCK;
+        v[u] = f.quad(i < q1 ? i : s0);
+      }
+#pragma unroll
+      for (int u = 0; u < kFbQ; ++u) {
+        const bool in = b + 4 * (int64_t)u * BLOCK < q1;
+        fn(abs_key(v[u].x), in); fn(abs_key(v[u].y), in); fn(abs_key(v[u].z), in); fn(abs_key(v[u].w), in);
+      }
+    }
+    for (int64_t i = q1 + t; i < s1; i += BLOCK) fn(abs_key(f(i)), true);
+  };
   grid_barrier<BLOCK>(w, fcnt);                // every workgroup is past its histogram zeroing
   // 1. the exact k-th largest key T (31-bit keys: digits of 11, 11 and 9 bits)
   uint32_t prefix = 0, pmask = 0, rem = k;
@@ -989,17 +1036,9 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     const uint32_t dmask = p < 2 ? 2047u : 511u;
     for (int b = t; b < 2048; b += BLOCK) fs.hist[b] = 0;
     __syncthreads();
-    for (int64_t i0 = s0 + t; i0 < s1; i0 += BLOCK * kFbUnroll) {
-      uint32_t key[kFbUnroll];
-#pragma unroll
-      for (int u = 0; u < kFbUnroll; ++u) {   // every load issued before any is used
-        const int64_t i = i0 + (int64_t)u * BLOCK;
-        key[u] = abs_key(f(i < s1 ? i : s0));
-      }
-#pragma unroll
-      for (int u = 0; u < kFbUnroll; ++u)
-        if (i0 + (int64_t)u * BLOCK < s1 && (key[u] & pmask) == prefix) atomicAdd(&fs.hist[(key[u] >> shift) & dmask], 1u);
-    }
+    for_keys([&](uint32_t key, bool in) {
+      hist_add_agg(fs.hist, in && (key & pmask) == prefix ? (int)((key >> shift) & dmask) : -1);
+    });
     __syncthreads();
     for (int b = t; b < 2048; b += BLOCK)
       if (fs.hist[b]) atomicAdd(&gh[p * 2048 + b], fs.hist[b]);
@@ -1016,20 +1055,10 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
   const uint32_t T = prefix, need_eq = rem;    // take every key > T and the need_eq lowest-index == T
   // 2. per-slice counts
   uint32_t ngt = 0, neq = 0;
-  for (int64_t i0 = s0 + t; i0 < s1; i0 += BLOCK * kFbUnroll) {
-    uint32_t key[kFbUnroll];
-#pragma unroll
-    for (int u = 0; u < kFbUnroll; ++u) {
-      const int64_t i = i0 + (int64_t)u * BLOCK;
-      key[u] = abs_key(f(i < s1 ? i : s0));
-    }
-#pragma unroll
-    for (int u = 0; u < kFbUnroll; ++u) {
-      const bool in = i0 + (int64_t)u * BLOCK < s1;
-      ngt += in && key[u] > T;
-      neq += in && key[u] == T;
-    }
-  }
+  for_keys([&](uint32_t key, bool in) {
+    ngt += in && key > T;
+    neq += in && key == T;
+  });
   uint32_t tgt, teq;
   block_excl_scan<BLOCK>(ngt, fs.s_w, &tgt);
   block_excl_scan<BLOCK>(neq, fs.s_w, &teq);
@@ -1044,14 +1073,23 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     eq_run += __hip_atomic_load(&cnt[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // 3. the slice in index order: selected-before = (# key > T before) + min(# key == T before, need_eq);
-  //    each thread owns kFbUnroll consecutive elements of a round, one block scan per round
+  //    each thread owns kFbUnroll consecutive elements of a round (two quads when whole), one block
+  //    scan per round; r' and the dense output leave as 16-B stores for whole quads
+  static_assert(kFbUnroll == 8, "two quads per thread per round");
   for (int64_t j0 = s0; j0 < s1; j0 += (int64_t)BLOCK * kFbUnroll) {
     const int64_t ib = j0 + (int64_t)t * kFbUnroll;
+    const bool whole = ib + kFbUnroll <= q1;
     float v[kFbUnroll];
+    if (whole) {
+      const float4 x0 = f.quad(ib), x1 = f.quad(ib + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < kFbUnroll; ++u) v[u] = f(ib + u < s1 ? ib + u : s0);
+    }
     uint32_t cg = 0, ce = 0;
 #pragma unroll
     for (int u = 0; u < kFbUnroll; ++u) {
-      v[u] = f(ib + u < s1 ? ib + u : s0);
       const uint32_t key = abs_key(v[u]);
       cg += ib + u < s1 && key > T;
       ce += ib + u < s1 && key == T;
@@ -1059,20 +1097,42 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     uint32_t tot;
     const uint32_t ex = block_excl_scan<BLOCK>(cg | (ce << 16), fs.s_w, &tot);
     uint32_t g_before = gt_run + (ex & 0xFFFFu), e_before = eq_run + (ex >> 16);
+    float rv[kFbUnroll], ov[kFbUnroll];
 #pragma unroll
     for (int u = 0; u < kFbUnroll; ++u) {
       const int64_t i = ib + u;
+      rv[u] = v[u];
+      ov[u] = 0.f;
       if (i < s1) {
         const uint32_t key = abs_key(v[u]);
         const bool gt = key > T, eq = key == T;
         if (gt || (eq && e_before < need_eq)) {
-          emit<MODE>(a, g_before + min(e_before, need_eq), i, v[u]);
-        } else {
-          if constexpr (MODE != kDenseNone) a.r[i] = v[u];
-          if constexpr (MODE == kDenseFused) a.out[i] = 0.f;
+          const uint32_t pos = g_before + min(e_before, need_eq);
+          a.vals[pos] = v[u];
+          a.idx[pos] = (int32_t)i;
+          rv[u] = v[u] - v[u];
+          ov[u] = 0.f + v[u];   // (0 + d) of the Python sum
         }
         g_before += gt;
         e_before += eq;
+      }
+    }
+    if constexpr (MODE != kDenseNone) {
+      if (whole) {
+        *reinterpret_cast<float4*>(a.r + ib) = make_float4(rv[0], rv[1], rv[2], rv[3]);
+        *reinterpret_cast<float4*>(a.r + ib + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
+        if constexpr (MODE == kDenseFused) {
+          *reinterpret_cast<float4*>(a.out + ib) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+          *reinterpret_cast<float4*>(a.out + ib + 4) = make_float4(ov[4], ov[5], ov[6], ov[7]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < kFbUnroll; ++u) {
+          if (ib + u < s1) {
+            a.r[ib + u] = rv[u];
+            if constexpr (MODE == kDenseFused) a.out[ib + u] = ov[u];
+          }
+        }
       }
     }
     gt_run += tot & 0xFFFFu;

@@ -4,7 +4,9 @@ grace_dl/dist/__init__.py:4-51, so caller code is unchanged.
 One addition, invisible to callers: ``Communicator.step`` asks the compressor for a fused native
 plan (``fused_step``) and, when the (compressor, memory, communicator) triple supports one, runs
 compensate -> compress -> update -> send_receive as one device pipeline.  The result is identical
-to the four-call composition (tests/test_gpu_parity.py checks both paths against the oracle).
+to the four-call composition (tests/test_gpu_topk.py::test_topk_residual_golden_sequence runs
+both paths against the reference's golden 3-step sequence; the QSGD / TernGrad / natural / fp16
+fused steps have their own fused-equals-unfused tests in tests/test_gpu_quant.py).
 """
 from abc import ABC, abstractmethod
 
