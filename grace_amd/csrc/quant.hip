@@ -221,6 +221,16 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
     const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes,
     float* __restrict__ fused_out = nullptr) {
   __shared__ SegTables32 tab;
+  // int8 codes leave as 16-B stores: each row stages its kQNB buckets' codes (128 B each) here and
+  // every lane stores 16 contiguous bytes (a 4-B store per quad covered four 64-B pieces per wave
+  // instruction: 10 of the encoder's 33 us)
+#ifdef GRACE_QSGD_STORE4   // A/B build only: the per-quad 4-B code stores
+  constexpr bool kStage16 = false;
+#else
+  constexpr bool kStage16 = !FUSED && sizeof(CodeT) == 1;
+#endif
+  const bool codes16 = (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
+  __shared__ uint32_t cst[kStage16 ? kQBlock / 16 : 1][kQNB * 32];
   stage_tables32(tab, seg_off, bkt_off, nseg);
   const int l16 = threadIdx.x & 15;
   constexpr int kRows = kQBlock / 16;
@@ -276,6 +286,12 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
         norm[h] = VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
       }
     }
+    bool st16[kQNB];   // row-uniform: bucket h is whole (128 elements), 16-B aligned codes
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      const int32_t bbase = e[h][0] - 4 * l16;
+      st16[h] = kStage16 && codes16 && ok[h] && (bbase & 15) == 0 && bbase + 128 <= end[h];
+    }
 #pragma unroll
     for (int h = 0; h < kQNB; ++h) {
       if (!ok[h]) continue;
@@ -318,8 +334,30 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
             for (int j = 0; j < 4; ++j)
               if (eq + j < end[h]) fused_out[eq + j] = o[j];
           }
+        } else if (kStage16 && st16[h]) {
+          cst[threadIdx.x >> 4][h * 32 + q * 16 + l16] =
+              (uint32_t)(uint8_t)c[0] | ((uint32_t)(uint8_t)c[1] << 8) | ((uint32_t)(uint8_t)c[2] << 16) |
+              ((uint32_t)(uint8_t)c[3] << 24);
         } else {
+#ifdef GRACE_DIAG_NOSTORE   // diagnostic A/B build only: no code stores (a never-true runtime guard)
+          if (norm[h] < 0.f)
+#endif
           store_codes4(codes, eq, end[h], fast[h][q], c);
+        }
+      }
+    }
+    if constexpr (kStage16) {
+      // the row's staged buckets: lane l16 stores bytes [16 (l16 % 8), +16) of bucket l16 / 8 (same
+      // wave wrote them: LDS keeps the wave's order, no barrier)
+#pragma unroll
+      for (int h0 = 0; h0 < kQNB; h0 += 2) {
+        const int h = h0 + (l16 >> 3);
+        if (h < kQNB && ok[h] && st16[h]) {
+          const uint4 wv = *reinterpret_cast<const uint4*>(&cst[threadIdx.x >> 4][h * 32 + 4 * (l16 & 7)]);
+#ifdef GRACE_DIAG_NOSTORE
+          if (norm[h] < 0.f)
+#endif
+          *reinterpret_cast<uint4*>(codes + (e[h][0] - 4 * l16) + 16 * (l16 & 7)) = wv;
         }
       }
     }
