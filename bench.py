@@ -15,6 +15,8 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   qsgd       QSGD(127, 128) compress + decompress over the 161-tensor ResNet-50 set, one
              segmented launch per stage (configs[2])
   terngrad   TernGrad, same set (configs[2])
+  topk_nomem top-k 1 % without memory, Allgather(TopK, NoneMemory).step on the 256 MiB bucket
+             (8n + 16k algorithmic bytes); world 1 is one streaming pass
   topk_e2e   the headline step with the bucket arriving from pinned host memory (H2D) and the
              aggregated dense gradient returned to it (D2H): the PCIe-inclusive rate in DESIGN.md
   topk_sharded  ONE 256 MiB bucket sharded over the N ranks, top-k 0.1 % + residual, exact global
@@ -52,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
-                    choices=["topk", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "qsgd_step", "terngrad_step", "powersgd",
+                    choices=["topk", "topk_nomem", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "qsgd_step", "terngrad_step", "powersgd",
                              "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
@@ -118,7 +120,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    run = {"topk": bench_topk, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
+    run = {"topk": bench_topk, "topk_nomem": bench_topk_nomem, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant, "qsgd_step": bench_quant, "terngrad_step": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd, "natural": bench_cast, "cnat": bench_cast,
            "fp16": bench_cast}[args.workload]
@@ -276,6 +278,53 @@ def cpu_baseline_topk(n, ratio, steps):
                       f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step",
             "note": "conservative: the oracle's numpy partition is faster than the reference's torch.topk "
                     "path (SURVEY.md §6 timed the reference itself at 1,843 ms/step on the 8-core build container)"}
+
+
+def bench_topk_nomem(args, world, rank, dev):
+    """Allgather(TopK 1 %, NoneMemory).step on the 256 MiB bucket ('top-k 1 %
+    c+d, no memory'): at world 1 one streaming pass reads g and writes the dense result."""
+    from grace_amd import ops
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+
+    n = args.numel
+    k = ops.ratio_k(n, args.ratio)
+    comm = Allgather(TopKCompressor(args.ratio), NoneMemory(), world)
+    gen = torch.Generator(device=dev)
+    grads = []
+    for j in range(args.buffers):
+        gen.manual_seed(1000 * rank + j + 1)
+        grads.append(torch.randn(n, device=dev, generator=gen))
+
+    def step(i):
+        return comm.step(grads[i % args.buffers], "bucket")
+
+    def step_unfused(i):            # the reference's four calls (compress, then send_receive)
+        payload, ctx = comm.compressor.compress(grads[i % args.buffers], "bucket")
+        return comm.send_receive(payload, "bucket", ctx)
+
+    for i in range(args.warmup):
+        step(i)
+    ops.timer_enable(True)
+    elapsed = timed(step, args.steps, 0, world, dev)
+    main_ms, launches = ops.timer_collect()
+    ops.timer_enable(False)
+    t_unfused = timed(step_unfused, args.steps, args.warmup, world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket, top-k 1 %, no memory")
+    line["config"] = {"workload": "Allgather(TopK 1%, NoneMemory).step on a 256 MiB fp32 bucket (BASELINE.md section 4)",
+                      "numel": n, "k": k, "unfused_ms_per_step": round(t_unfused / args.steps * 1e3, 4)}
+    step_bytes = 8 * n + 16 * k                     # BASELINE.md section 4: 8n + 16k
+    main_avg_ms = main_ms / max(launches, 1)
+    main_bytes = (8 if world == 1 else 4) * n       # g read (+ dense out written at world 1)
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(step_bytes / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(step_bytes / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "step_algorithmic_bytes": step_bytes, "kernel": "topk_main",
+                        "kernel_avg_us": round(main_avg_ms * 1e3, 2),
+                        "kernel_frac": round(main_bytes / (main_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return line
 
 
 def bench_topk_e2e(args, world, rank, dev):

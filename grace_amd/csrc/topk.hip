@@ -40,7 +40,11 @@
 namespace grace {
 
 // dense outputs written by a top-k launch
-enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2 };
+// kDenseOut: no memory (Allgather(TopK, NoneMemory) at world 1): t = g, only the dense output is
+// written next to the payload, the input stays read-only
+enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2, kDenseOut = 3 };
+template <int MODE> constexpr bool kWritesR = MODE == kDenseRes || MODE == kDenseFused;
+template <int MODE> constexpr bool kWritesOut = MODE == kDenseFused || MODE == kDenseOut;
 
 #ifndef GRACE_MAIN_BLOCK
 #define GRACE_MAIN_BLOCK 256
@@ -222,7 +226,7 @@ struct StepArgs {
   int64_t n, k;
   float* vals;
   int32_t* idx;
-  float* out;          // dense output (kDenseFused)
+  float* out;          // dense output (kDenseFused, kDenseOut)
   int64_t sample_n;    // stratified sample size (<= kSampleMax)
   int64_t stratum;     // n / sample_n
   int64_t idx_base;    // sharded mode: global index of this shard's element 0 (payload indices)
@@ -613,14 +617,14 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
 #endif
       msure |= (uint32_t)sure << (u * 4 + j);
       mcand |= (uint32_t)cand << (u * 4 + j);
-      if constexpr (MODE == kDenseFused) {
+      if constexpr (kWritesOut<MODE>) {
         // sure elements, and candidates above the provisional threshold, are written as selected;
         // the finalize fixes up only the candidates whose final decision differs
         if (sure || (cand && key > mid)) { set4(rout, j, tv - tv); set4(dout, j, 0.f + tv); }
       }
     }
-    if constexpr (MODE == kDenseRes || MODE == kDenseFused) st4<FAST>(a.r, i0, n, rout);
-    if constexpr (MODE == kDenseFused) st4<FAST>(a.out, i0, n, dout);
+    if constexpr (kWritesR<MODE>) st4<FAST>(a.r, i0, n, rout);
+    if constexpr (kWritesOut<MODE>) st4<FAST>(a.out, i0, n, dout);
   }
   const uint32_t msel = msure | mcand;
   if (msel) {
@@ -754,8 +758,8 @@ template <int MODE>
 __device__ __forceinline__ void emit(const StepArgs& a, uint32_t pos, int64_t i, float v) {
   a.vals[pos] = v;
   a.idx[pos] = (int32_t)i;
-  if constexpr (MODE != kDenseNone) a.r[i] = v - v;
-  if constexpr (MODE == kDenseFused) a.out[i] = 0.f + v;   // (0 + d) of the Python sum
+  if constexpr (kWritesR<MODE>) a.r[i] = v - v;
+  if constexpr (kWritesOut<MODE>) a.out[i] = 0.f + v;   // (0 + d) of the Python sum
 }
 
 // Ordered (ascending index) single-workgroup write of every element with composite >= T over a
@@ -778,8 +782,8 @@ __device__ void block_write_selected(const StepArgs& a, const F& f, int64_t n, u
       if (sel) {
         emit<MODE>(a, run + ex, i, v);
       } else {
-        if constexpr (MODE != kDenseNone) a.r[i] = v;
-        if constexpr (MODE == kDenseFused) a.out[i] = 0.f;
+        if constexpr (kWritesR<MODE>) a.r[i] = v;
+        if constexpr (kWritesOut<MODE>) a.out[i] = 0.f;
       }
     }
     run += tot;
@@ -829,7 +833,7 @@ template <int MODE, bool AG>
 struct MainTs {
   const float* g; const float* r; const float* out;
   __device__ float operator()(int64_t i) const {
-    if constexpr (MODE == kDenseNone) return g[i];
+    if constexpr (MODE == kDenseNone || MODE == kDenseOut) return g[i];
     if constexpr (MODE == kDenseRes) return ld_f32<AG>(r + i);
     const float o = ld_f32<AG>(out + i), rr = ld_f32<AG>(r + i);   // both issued: no dependent load
     return f2u(o) != 0u ? o : rr;
@@ -839,7 +843,7 @@ struct MainTs {
     if constexpr (AG) {
       return make_float4((*this)(i), (*this)(i + 1), (*this)(i + 2), (*this)(i + 3));
     } else {
-      if constexpr (MODE == kDenseNone) return *reinterpret_cast<const float4*>(g + i);
+      if constexpr (MODE == kDenseNone || MODE == kDenseOut) return *reinterpret_cast<const float4*>(g + i);
       if constexpr (MODE == kDenseRes) return *reinterpret_cast<const float4*>(r + i);
       const float4 o = *reinterpret_cast<const float4*>(out + i), rr = *reinterpret_cast<const float4*>(r + i);
       return make_float4(f2u(o.x) != 0u ? o.x : rr.x, f2u(o.y) != 0u ? o.y : rr.y, f2u(o.z) != 0u ? o.z : rr.z,
@@ -865,9 +869,12 @@ __device__ __forceinline__ bool boundary_preload(const TopkWs& w, bool ok, uint3
 // boundary-bin entry not selected: in the fused mode undo a provisional selection (key > mid)
 template <int MODE>
 __device__ __forceinline__ void unselect(const StepArgs& a, int2 e, uint32_t mid) {
-  if constexpr (MODE == kDenseFused) {
+  if constexpr (kWritesOut<MODE>) {
     const float v = u2f((uint32_t)e.y);
-    if (abs_key(v) > mid) { a.r[e.x] = v; a.out[e.x] = 0.f; }
+    if (abs_key(v) > mid) {
+      if constexpr (kWritesR<MODE>) a.r[e.x] = v;
+      a.out[e.x] = 0.f;
+    }
   }
 }
 
@@ -941,12 +948,15 @@ __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[k
       a.vals[ps] = v;
       a.idx[ps] = e[u].x;
       if constexpr (MODE == kDenseRes) a.r[e[u].x] = v - v;
-      if constexpr (MODE == kDenseFused) {
-        if (!above_mid) { a.r[e[u].x] = v - v; a.out[e[u].x] = 0.f + v; }
+      if constexpr (kWritesOut<MODE>) {
+        if (!above_mid) {
+          if constexpr (kWritesR<MODE>) a.r[e[u].x] = v - v;
+          a.out[e[u].x] = 0.f + v;
+        }
       }
       ++ps;
-    } else if (MODE == kDenseFused && ((fbelow >> u) & 1u) && above_mid) {
-      a.r[e[u].x] = v;
+    } else if (kWritesOut<MODE> && ((fbelow >> u) & 1u) && above_mid) {
+      if constexpr (kWritesR<MODE>) a.r[e[u].x] = v;
       a.out[e[u].x] = 0.f;
     }
   }
@@ -1119,9 +1129,11 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     }
     if constexpr (MODE != kDenseNone) {
       if (whole) {
-        *reinterpret_cast<float4*>(a.r + ib) = make_float4(rv[0], rv[1], rv[2], rv[3]);
-        *reinterpret_cast<float4*>(a.r + ib + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
-        if constexpr (MODE == kDenseFused) {
+        if constexpr (kWritesR<MODE>) {
+          *reinterpret_cast<float4*>(a.r + ib) = make_float4(rv[0], rv[1], rv[2], rv[3]);
+          *reinterpret_cast<float4*>(a.r + ib + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
+        }
+        if constexpr (kWritesOut<MODE>) {
           *reinterpret_cast<float4*>(a.out + ib) = make_float4(ov[0], ov[1], ov[2], ov[3]);
           *reinterpret_cast<float4*>(a.out + ib + 4) = make_float4(ov[4], ov[5], ov[6], ov[7]);
         }
@@ -1129,8 +1141,8 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
 #pragma unroll
         for (int u = 0; u < kFbUnroll; ++u) {
           if (ib + u < s1) {
-            a.r[ib + u] = rv[u];
-            if constexpr (MODE == kDenseFused) a.out[ib + u] = ov[u];
+            if constexpr (kWritesR<MODE>) a.r[ib + u] = rv[u];
+            if constexpr (kWritesOut<MODE>) a.out[ib + u] = ov[u];
           }
         }
       }
@@ -1206,7 +1218,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
     STAMP_IF(fi == 0, w.ctl, 9);
     // fused mode, no candidate needed (k sure elements): every candidate is unselected, but the
     // provisionally selected ones still need their fix-ups -> route with the boundary above all bins
-    if (MODE == kDenseFused && B < 0) B = kHistBins;
+    if (kWritesOut<MODE> && B < 0) B = kHistBins;
     // residual-only mode: sure entries still hold t in r; zero them now
     // (kFinPer entries per thread per round, every load issued before any store: one dependent
     // load -> store chain per entry made this 14 us of the finalize at k = 671 K)
@@ -1684,6 +1696,15 @@ grace_status_t grace_topk_compress(const float* x, int64_t n, int64_t k, float* 
   GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_compress: workspace required");
   StepArgs a{x, nullptr, 1.f, 1.f, n, k, vals, idx, nullptr};
   return run_topk<false, kDenseNone>(a, ws, ws_bytes_, as_stream(stream));
+}
+
+grace_status_t grace_topk_step_dense(const float* x, int64_t n, int64_t k, float* vals, int32_t* idx, float* out,
+                                     void* ws, size_t ws_bytes_, void* stream) {
+  GRACE_REQUIRE(x && vals && idx && out && n > 0 && k >= 1 && k <= n && n < (int64_t)1 << 31,
+                "grace_topk_step_dense: bad arguments");
+  GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_step_dense: workspace required");
+  StepArgs a{x, nullptr, 1.f, 1.f, n, k, vals, idx, out};
+  return run_topk<false, kDenseOut>(a, ws, ws_bytes_, as_stream(stream));
 }
 
 grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t has_residual,

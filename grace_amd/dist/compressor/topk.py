@@ -11,6 +11,7 @@ import torch.distributed as dist
 
 from grace_amd import ops
 from grace_amd.dist.communicator.allgather import Allgather
+from grace_amd.dist.memory.none import NoneMemory
 from grace_amd.dist.memory.residual import ResidualMemory
 from grace_amd.dist import Compressor
 
@@ -45,8 +46,15 @@ class TopKCompressor(Compressor):
         return out.view(ctx)
 
     def fused_step(self, communicator, tensor, name):
-        """compensate -> compress -> update -> send_receive for (TopK, Residual|None, Allgather)."""
+        """compensate -> compress -> update -> send_receive for (TopK, Residual, Allgather) at any world
+        size, and for (TopK, NoneMemory, Allgather) at world 1."""
         mem = communicator.memory
+        if (isinstance(communicator, Allgather) and type(mem) is NoneMemory and int(communicator.world_size) == 1
+                and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
+            # no memory, world 1: payload and (0 + d) / 1 from one read of the tensor
+            g = ops.dev_f32(tensor)
+            _, _, _, out = ops.topk_step_dense(g, ops.ratio_k(g.numel(), self.compress_ratio))
+            return out.view(tensor.shape)
         if not (isinstance(communicator, Allgather) and type(mem) is ResidualMemory
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
             return None

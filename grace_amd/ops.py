@@ -230,6 +230,18 @@ def topk_compress(x, k):
     return buf, vals, idx
 
 
+def topk_step_dense(x, k, out=None):
+    """World-1 Allgather(TopK, NoneMemory).step in one streaming pass (grace_topk_step_dense): the
+    payload of topk_compress plus the dense (0 + decode) / 1 result; x is only read."""
+    x = dev_f32(x)
+    n = x.numel()
+    buf, vals, idx = new_payload(k, x.device)
+    out = torch.empty(n, dtype=F32, device=x.device) if out is None else out
+    ws = topk_workspace(n, k, x.device)
+    _lib.call("grace_topk_step_dense", _p(x), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
+    return buf, vals, idx, out
+
+
 def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payload=None):
     g = dev_f32(g)
     n = g.numel()

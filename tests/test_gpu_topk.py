@@ -127,6 +127,30 @@ def test_topk_residual_step_vs_oracle(n, kind, with_out):
         assert same_bits(_np(out), oout)
 
 
+@pytest.mark.parametrize("n", [1000, 32768, 32769, 100003, (1 << 21) + 5])
+@pytest.mark.parametrize("kind", ["normal", "ties", "sparse", "special"])
+def test_topk_nomemory_step_one_pass(n, kind):
+    """Allgather(TopK, NoneMemory).step at world 1 through the one-pass path (grace_topk_step_dense):
+    payload and (0 + decode) / 1 bit-exact against the oracle's compress + decompress + Python sum;
+    the input is left untouched.  'sparse' takes the exact fallback (k > non-zeros)."""
+    from grace_amd import ops
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    x = _inputs(n, kind, seed=n + 3)
+    xt = torch.from_numpy(x).to(DEV)
+    k = O.ratio_k(n, 0.01)
+    expect = np.float32(0.0) + O.sparse_decode(*O.topk_select(x, k), n)     # Python sum starts at 0
+    _, vals, idx, out = ops.topk_step_dense(xt, k)
+    check_topk(x, k, vals, idx)
+    assert same_bits(_np(out), expect)
+    comm = Allgather(TopKCompressor(0.01), NoneMemory(), 1)
+    out2 = comm.step(xt.view(-1, 1) if n % 2 else xt, "w")
+    assert tuple(out2.shape) == ((n, 1) if n % 2 else (n,))
+    assert same_bits(_np(out2).ravel(), expect)
+    assert same_bits(_np(xt), x)
+
+
 def test_topk_fallback_taken_and_exact():
     """k larger than the number of non-zeros: the sampled bracket cannot hold; the exact
     single-workgroup path must produce the oracle's result (lowest-index zeros fill the tail)."""
