@@ -55,6 +55,15 @@ template <int MODE> constexpr bool kWritesOut = MODE == kDenseFused || MODE == k
 constexpr int kMainBlock = GRACE_MAIN_BLOCK;
 constexpr int kMainVec = GRACE_MAIN_VEC;                   // float4 per thread
 constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 16384 elements per workgroup
+#ifndef GRACE_MAIN_VEC_NORES
+#define GRACE_MAIN_VEC_NORES 32
+#endif
+// with no residual stream (a first step, compress only, no memory) a chunk is twice as long: half
+// the bytes per element, and each workgroup's fixed costs (histogram clear and flush, list flushes)
+// then weighed twice as much (A/B at 256 MiB, no memory: main 132 -> 107.5 us; with the residual
+// stream 32768-element chunks are slower, 196.9 -> 208.8 us)
+template <bool HAS_RES> constexpr int kVecOf = HAS_RES ? kMainVec : GRACE_MAIN_VEC_NORES;
+template <bool HAS_RES> constexpr int kChunkOf = kMainBlock * 4 * kVecOf<HAS_RES>;
 constexpr int kHistBins = 2048;                            // candidate histogram
 constexpr int kStage = 512;                                // LDS staging entries per list
 constexpr int kSelBlock = 1024;                            // single-workgroup selectors
@@ -672,9 +681,27 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
 template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
                                               uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
-  constexpr int NG = kMainVec / kGroup;
-  const int64_t cbase = chunk * kMainChunk + (int64_t)threadIdx.x * 4;
+  constexpr int NG = kVecOf<HAS_RES> / kGroup;
+  const int64_t cbase = chunk * kChunkOf<HAS_RES> + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
+#ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
+  if constexpr (!HAS_RES && NG >= 3) {
+    // one input stream (g only): the loads run TWO groups ahead, so a lane keeps as many bytes in
+    // flight as with the residual stream (8 x 16 B)
+    float4 g1[kGroup], g2[kGroup];
+    load_group<false, FAST>(a, cbase, rc, gc);
+    load_group<false, FAST>(a, cbase + kGroup * (kMainBlock * 4), rc, g1);
+#pragma unroll 1
+    for (int q = 0; q < NG; ++q) {
+      const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
+      if (q + 2 < NG) load_group<false, FAST>(a, gbase + 2 * kGroup * (kMainBlock * 4), rc, g2);
+      classify_group<false, MODE, FAST>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc);
+#pragma unroll
+      for (int u = 0; u < kGroup; ++u) { gc[u] = g1[u]; g1[u] = g2[u]; }
+    }
+    return;
+  }
+#endif
   load_group<HAS_RES, FAST>(a, cbase, rc, gc);
 #pragma unroll 1
   for (int q = 0; q < NG; ++q) {
@@ -730,7 +757,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
-  const int64_t nchunks = (a.n + kMainChunk - 1) / kMainChunk;
+  const int64_t nchunks = (a.n + kChunkOf<HAS_RES> - 1) / kChunkOf<HAS_RES>;
   // sharded mode: this rank's shard length rides in the exchanged counters, so every rank can
   // check the shard sizes it planned with (grace_amd/dist/sharded.py)
   if (w.xcnt && blockIdx.x == 0 && tid == 0) w.xcnt[2] = (uint32_t)a.n;
@@ -738,7 +765,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    if (VEC && (chunk + 1) * kMainChunk <= a.n)
+    if (VEC && (chunk + 1) * kChunkOf<HAS_RES> <= a.n)
       main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
     else
       main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
@@ -1377,7 +1404,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   static_assert(kSmallN >= 2 * kSampleBlock, "bracket grid covers the histogram zeroing");
   topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
-  const unsigned nblk = (unsigned)((a.n + kMainChunk - 1) / kMainChunk);
+  const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES> - 1) / kChunkOf<HAS_RES>);
   if (vec)
     launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
   else
@@ -1842,7 +1869,8 @@ grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t ha
   StepArgs a{g, residual, beta, gamma, m, k, vals, idx, nullptr};
   a.idx_base = idx_base;
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual)) & 15u) == 0;
-  unsigned nblk = (unsigned)((m + kMainChunk - 1) / kMainChunk);
+  unsigned nblk = (unsigned)((m + kChunkOf<true> - 1) / kChunkOf<true>);
+  if (!has_residual) nblk = (unsigned)((m + kChunkOf<false> - 1) / kChunkOf<false>);
 #ifdef GRACE_MAIN_PERSIST
   if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
 #endif
