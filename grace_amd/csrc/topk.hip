@@ -17,7 +17,7 @@
 //   2. select   (1 WG)          ranks of the k-th key in the sample +-6 sigma (binomial) ->
 //                               thr_hi >= thr_lo bracketing the k-th largest key; zeroes this
 //                               step's counters, cursors and histograms.
-//   3. main     (n/16384 WGs)   one streaming pass: t = beta r + gamma g, write r' (and the dense
+//   3. main     (n/12288 WGs)   one streaming pass: t = beta r + gamma g, write r' (and the dense
 //                               world-1 output), key > thr_hi  -> "sure": appended to the payload;
 //                               thr_lo <= key <= thr_hi -> candidate list + 2048-bin histogram
 //                               of the candidate key range.  Appends use wave64 ballot + mbcnt
@@ -50,11 +50,13 @@ template <int MODE> constexpr bool kWritesOut = MODE == kDenseFused || MODE == k
 #define GRACE_MAIN_BLOCK 256
 #endif
 #ifndef GRACE_MAIN_VEC
-#define GRACE_MAIN_VEC 16
+#define GRACE_MAIN_VEC 12
 #endif
 constexpr int kMainBlock = GRACE_MAIN_BLOCK;
 constexpr int kMainVec = GRACE_MAIN_VEC;                   // float4 per thread
-constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 16384 elements per workgroup
+constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 12288 elements per workgroup (A/B, 256 MiB
+                                                           // top-k 1 % + residual: 8192 / 12288 / 16384 /
+                                                           // 20480 / 24576 -> 240 / 195 / 196.5 / 204 / 205 us)
 #ifndef GRACE_MAIN_VEC_NORES
 #define GRACE_MAIN_VEC_NORES 32
 #endif
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
 // ------------------------------------------------------------------------------------------------
 // 2. main streaming pass
 //
-// Each workgroup streams one 16384-element chunk: 4 groups of 4 float4 per lane per array, with
+// Each workgroup streams one 12288-element chunk: 3 groups of 4 float4 per lane per array, with
 // the next group's loads issued before the current group is classified (16-B loads, 8 in flight
 // per lane).  Per group every lane counts its sure / candidate elements, one wave-wide prefix
 // scan (packed 16|16 bits) places them, and ONE LDS atomic per wave per group reserves staging
