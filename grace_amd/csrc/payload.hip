@@ -20,10 +20,17 @@ constexpr int kPChunk = 1 << kPChunkLog;
 constexpr int kPBlock = 256;
 
 #ifndef GRACE_GROUP_BLOCK
-#define GRACE_GROUP_BLOCK 256
+#define GRACE_GROUP_BLOCK 1024
 #endif
-constexpr int kGroupBlock = GRACE_GROUP_BLOCK;         // more, smaller workgroups: the payload is
-constexpr int kGroupPer = 16;                          // only ~0.7M entries; entries per thread
+#ifndef GRACE_GROUP_PER
+#define GRACE_GROUP_PER 4
+#endif
+// 4096 entries per workgroup over 1024 threads: the per-workgroup clear and scan of the 8192-bin
+// LDS histogram (one bin per output chunk) dominate a pass, so they are spread over as many threads
+// as possible (A/B, 671,088 entries: 256 x 16 -> 37.4 us, 512 x 8 -> 29.7, 1024 x 4 -> 27.6,
+// 1024 x 8 -> 35.3, 256 x 64 -> 64.1)
+constexpr int kGroupBlock = GRACE_GROUP_BLOCK;
+constexpr int kGroupPer = GRACE_GROUP_PER;             // entries per thread
 constexpr int kMaxGroupChunks = 32768;                 // LDS histogram bins (128 KB): n <= 2^28
 
 // pass 1: per-workgroup LDS histogram of chunk ids, flushed with one atomic per non-zero bin; the
