@@ -57,15 +57,26 @@ constexpr int kMainVec = GRACE_MAIN_VEC;                   // float4 per thread
 constexpr int kMainChunk = kMainBlock * 4 * kMainVec;      // 12288 elements per workgroup (A/B, 256 MiB
                                                            // top-k 1 % + residual: 8192 / 12288 / 16384 /
                                                            // 20480 / 24576 -> 240 / 195 / 196.5 / 204 / 205 us)
+#ifndef GRACE_MAIN_VEC_12B
+#define GRACE_MAIN_VEC_12B 20
+#endif
 #ifndef GRACE_MAIN_VEC_NORES
 #define GRACE_MAIN_VEC_NORES 32
 #endif
-// with no residual stream (a first step, compress only, no memory) a chunk is twice as long: half
-// the bytes per element, and each workgroup's fixed costs (histogram clear and flush, list flushes)
-// then weighed twice as much (A/B at 256 MiB, no memory: main 132 -> 107.5 us; with the residual
-// stream 32768-element chunks are slower, 196.9 -> 208.8 us)
-template <bool HAS_RES> constexpr int kVecOf = HAS_RES ? kMainVec : GRACE_MAIN_VEC_NORES;
-template <bool HAS_RES> constexpr int kChunkOf = kMainBlock * 4 * kVecOf<HAS_RES>;
+// Chunk length by the bytes the pass moves per element: each workgroup has fixed costs (histogram
+// clear and flush, list flushes), so the fewer bytes per element, the longer its chunk.  A/B at
+// 256 MiB (main pass):
+//   16 B (g, r read; r', out written; the world-1 headline): 8192 / 12288 / 16384 / 20480 / 24576 /
+//        32768 elements -> 240 / 194-198 / 196-206 / 204 / 205 / 209 us;
+//   12 B (g, r read; r' written; world > 1): 12288 / 16384 / 20480 -> 217-221 / 208-212 / 206 us;
+//    8 B (no residual stream; no memory or a first step): 16384 -> 132, 32768 -> 107 us;
+//        24576 / 28672 / 40960 -> 116 / 114 / 112 us.
+template <bool HAS_RES, int MODE>
+constexpr int kBytesOf = 4 + (HAS_RES ? 4 : 0) + (kWritesR<MODE> ? 4 : 0) + (kWritesOut<MODE> ? 4 : 0);
+template <bool HAS_RES, int MODE>
+constexpr int kVecOf = kBytesOf<HAS_RES, MODE> >= 16 ? kMainVec
+                       : (kBytesOf<HAS_RES, MODE> >= 12 ? GRACE_MAIN_VEC_12B : GRACE_MAIN_VEC_NORES);
+template <bool HAS_RES, int MODE> constexpr int kChunkOf = kMainBlock * 4 * kVecOf<HAS_RES, MODE>;
 constexpr int kHistBins = 2048;                            // candidate histogram
 constexpr int kStage = 512;                                // LDS staging entries per list
 constexpr int kSelBlock = 1024;                            // single-workgroup selectors
@@ -683,8 +694,8 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
 template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
                                               uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
-  constexpr int NG = kVecOf<HAS_RES> / kGroup;
-  const int64_t cbase = chunk * kChunkOf<HAS_RES> + (int64_t)threadIdx.x * 4;
+  constexpr int NG = kVecOf<HAS_RES, MODE> / kGroup;
+  const int64_t cbase = chunk * kChunkOf<HAS_RES, MODE> + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
 #ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
   if constexpr (!HAS_RES && NG >= 3) {
@@ -759,7 +770,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
-  const int64_t nchunks = (a.n + kChunkOf<HAS_RES> - 1) / kChunkOf<HAS_RES>;
+  const int64_t nchunks = (a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>;
   // sharded mode: this rank's shard length rides in the exchanged counters, so every rank can
   // check the shard sizes it planned with (grace_amd/dist/sharded.py)
   if (w.xcnt && blockIdx.x == 0 && tid == 0) w.xcnt[2] = (uint32_t)a.n;
@@ -767,7 +778,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    if (VEC && (chunk + 1) * kChunkOf<HAS_RES> <= a.n)
+    if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n)
       main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
     else
       main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
@@ -1406,7 +1417,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   static_assert(kSmallN >= 2 * kSampleBlock, "bracket grid covers the histogram zeroing");
   topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
-  const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES> - 1) / kChunkOf<HAS_RES>);
+  const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>);
   if (vec)
     launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
   else
@@ -1871,8 +1882,8 @@ grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t ha
   StepArgs a{g, residual, beta, gamma, m, k, vals, idx, nullptr};
   a.idx_base = idx_base;
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual)) & 15u) == 0;
-  unsigned nblk = (unsigned)((m + kChunkOf<true> - 1) / kChunkOf<true>);
-  if (!has_residual) nblk = (unsigned)((m + kChunkOf<false> - 1) / kChunkOf<false>);
+  unsigned nblk = (unsigned)((m + kChunkOf<true, kDenseRes> - 1) / kChunkOf<true, kDenseRes>);
+  if (!has_residual) nblk = (unsigned)((m + kChunkOf<false, kDenseRes> - 1) / kChunkOf<false, kDenseRes>);
 #ifdef GRACE_MAIN_PERSIST
   if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
 #endif
