@@ -686,7 +686,10 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
 // Stage 1 writes f64 partials per work unit (16384 elements); stage 2 (encode) reduces its
 // segment's partials with the whole workgroup in a fixed order (every unit of a segment derives
 // the identical scale), then encodes its unit.  Both stages move 16 B per lane.
-constexpr int kTernUnit = 16384;
+#ifndef GRACE_TERN_UNIT
+#define GRACE_TERN_UNIT 16384   // A/B, ResNet-50 set compress: 4096 / 8192 / 16384 / 32768 -> 64.7 /
+#endif                          // 56.5 / 54.0 / 60.6 us (tools/ab_quant.py, one process)
+constexpr int kTernUnit = GRACE_TERN_UNIT;
 
 struct TernPartial { double sum, sq; float amax; uint32_t nan; };
 

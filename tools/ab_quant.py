@@ -26,11 +26,13 @@ n = sum(sizes)
 dev = torch.device("cuda", 0)
 xs = [torch.randn(n, device=dev) * 0.01 for _ in range(3)]
 seg_off, bkt_off, nb = ops.seg_tables(sizes, 128, dev)
-tseg, tunit, nunits = ops.seg_tables(sizes, libs[0].grace_terngrad_unit(), dev)
+# unit tables per build (the TernGrad work-unit size is a build constant)
+ttab = [ops.seg_tables(sizes, L.grace_terngrad_unit(), dev) for L in libs]
 codes = torch.empty(n, dtype=torch.int8, device=dev)
 norms = torch.empty(nb, device=dev)
 scal = torch.empty(len(sizes), device=dev)
-wss = [torch.zeros(L.grace_terngrad_workspace_bytes(nunits), dtype=torch.uint8, device=dev) for L in libs]
+wss = [torch.zeros(L.grace_terngrad_workspace_bytes(ttab[i][2]), dtype=torch.uint8, device=dev)
+       for i, L in enumerate(libs)]
 stream = torch.cuda.current_stream().cuda_stream
 
 
@@ -40,8 +42,10 @@ def qsgd(L, i, j):
 
 
 def tern(L, i, j):
+    li = libs.index(L)
+    tseg, tunit, nunits = ttab[li]
     L.grace_terngrad_compress(xs[j].data_ptr(), tseg.data_ptr(), tunit.data_ptr(), len(sizes), nunits, None, None,
-                              i, codes.data_ptr(), scal.data_ptr(), wss[libs.index(L)].data_ptr(), stream)
+                              i, codes.data_ptr(), scal.data_ptr(), wss[li].data_ptr(), stream)
 
 
 res = {(w, i): [] for w in ("qsgd", "tern") for i in range(len(libs))}
