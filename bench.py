@@ -27,6 +27,8 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
              (examples/dist/CIFAR10-dawndist/core.py:204-208), the same per-tensor semantics in one
              launch sequence (SegmentedTopK), and one flat bucket with a single global top-k
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
+  dgc        DGC 1 % with momentum-correction memory on the 256 MiB bucket
+  sign_bits  signSGD with the 1-bit wire layout, compress + Allgather decode, 256 MiB (8f.4)
 
 Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
@@ -55,7 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="topk",
                     choices=["topk", "topk_nomem", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "qsgd_step", "terngrad_step", "powersgd",
-                             "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented"])
+                             "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented", "dgc",
+                             "sign_bits"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -122,7 +125,7 @@ def main():
             dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_nomem": bench_topk_nomem, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant, "qsgd_step": bench_quant, "terngrad_step": bench_quant,
-           "terngrad": bench_quant, "powersgd": bench_powersgd, "natural": bench_cast, "cnat": bench_cast,
+           "terngrad": bench_quant, "powersgd": bench_powersgd, "dgc": bench_dgc, "sign_bits": bench_sign_bits, "natural": bench_cast, "cnat": bench_cast,
            "fp16": bench_cast}[args.workload]
     line = run(args, world, rank, dev)
     if args.workload == "topk" and world > 1 and not args.no_sharded:
@@ -528,6 +531,65 @@ def bench_cast(args, world, rank, dev):
 
 
 # ------------------------------------------------------------------------------------------ PowerSGD
+def bench_dgc(args, world, rank, dev):
+    """Allgather(DgcCompressor(1 %), DgcMemory(0.9)).step on the 256 MiB
+    bucket (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39).  The payload size is data
+    dependent (variable-size Allgather, one host read of the count per step, as the reference)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.dgc import DgcCompressor
+    from grace_amd.dist.memory.dgc import DgcMemory
+    n = args.numel
+    comm = Allgather(DgcCompressor(args.ratio), DgcMemory(0.9, False, world), world)
+    grads = [torch.randn(n, device=dev) for _ in range(args.buffers)]
+    for j in range(args.buffers):
+        comm.step(grads[j], f"b{j}")
+    elapsed = timed(lambda i: comm.step(grads[i % args.buffers], f"b{i % args.buffers}"), args.steps, args.warmup,
+                    world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket, DGC 1 %")
+    line["config"] = {"workload": "Allgather(DgcCompressor(1%), DgcMemory(0.9)).step, 256 MiB fp32 (SURVEY.md 8f.3)",
+                      "numel": n}
+    # compensate 20 B (g, r, a read; r, a written), threshold histogram over a 4 B, compaction 4 B,
+    # mask update 16 B (r, a), dense decode 4 B
+    alg = 48.0 * n
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": alg,
+                        "note": "48n: compensate 20n, threshold histogram 4n, compaction 4n, mask update 16n, "
+                                "dense decode 4n (the reference's passes, each fused to one kernel)"}
+    return line
+
+
+def bench_sign_bits(args, world, rank, dev):
+    """signSGD with the 1-bit wire layout (SignSGDCompressor(wire="bits")),
+    compress + Allgather decode on the 256 MiB bucket at world size 1 (the packed payload is what a
+    world > 1 exchange would move: n / 8 bytes per rank)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.signsgd import SignSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    n = args.numel
+    comm = Allgather(SignSGDCompressor(wire="bits"), NoneMemory(), world)
+    grads = [torch.randn(n, device=dev) for _ in range(args.buffers)]
+
+    def step(i):   # the four calls, so the packed payload is produced and decoded
+        g = grads[i % args.buffers]
+        payload, ctx = comm.compressor.compress(g, "w")
+        return comm.send_receive(payload, "w", ctx)
+
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 signSGD, 1-bit wire")
+    line["config"] = {"workload": "SignSGD wire='bits': compress (1 bit / element) + Allgather decode, 256 MiB fp32",
+                      "numel": n}
+    alg = 4.0 * n + n / 8 + n / 8 * world + 4.0 * n     # read x, write bits; read W bit payloads, write out
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": alg}
+    return line
+
+
 def bench_powersgd(args, world, rank, dev):
     from grace_amd.dist.communicator.allreduce import Allreduce
     from grace_amd.dist.compressor.powersgd import PowerSGDCompressor

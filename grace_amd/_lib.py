@@ -65,6 +65,7 @@ SIGNATURES = {
     "grace_sumsq": (ST, [P, I64, P, P, P]),
     "grace_clip_by_sumsq": (ST, [P, P, F32, P, I64, P]),
     "grace_pack_bits": (ST, [P, I64, P, P]),
+    "grace_sign_encode_bits": (ST, [P, I64, P, P]),
     "grace_unpack_bits": (ST, [P, I64, P, P]),
     "grace_sign_majority_bits": (ST, [P, I64, I32, I64, P, P]),
     "grace_pack2_bytes": (I64, [I64]),

@@ -57,30 +57,95 @@ __global__ __launch_bounds__(kWBlock) void unpack_bits_kernel(const uint32_t* __
   }
 }
 
-// majority over W packed payloads (rank w's words at + w * stride): +1 where 2 * ones >= W
+// majority over W packed payloads (rank w's words at + w * stride): +1 where 2 * ones >= W.
+// Lane l of a wave owns elements base + 4 l .. + 3 (the 4-bit nibble l % 8 of word base / 32 + l / 8;
+// the 8 lanes of a word read it together), counts its 4 bits over the ranks and stores one float4:
+// every store instruction writes 1 KB contiguous.  (A thread per word storing its 32 floats one by
+// one touched 64 lines per instruction: 0.24 ms for a 256 MiB decode + encode.)
+constexpr int kMajU = 4;   // 256-element wave slices per lane per round
 __global__ __launch_bounds__(kWBlock) void majority_bits_kernel(const uint32_t* __restrict__ words, int64_t stride,
                                                                int world, int64_t n, float* __restrict__ out) {
-  const int64_t nw = (n + 31) / 32;
-  for (int64_t w = (int64_t)blockIdx.x * kWBlock + threadIdx.x; w < nw; w += (int64_t)gridDim.x * kWBlock) {
-    // bit-sliced counters: 6 planes count up to 63 ranks per bit position
-    uint32_t c[6] = {0, 0, 0, 0, 0, 0};
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kWBlock / 64);
+  const int64_t wave = (int64_t)blockIdx.x * (kWBlock / 64) + (threadIdx.x >> 6);
+  const bool vec = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+  for (int64_t base = wave * 256 * kMajU; base < n; base += nwaves * 256 * kMajU) {
+    uint32_t ones[kMajU][4] = {};
     for (int r = 0; r < world; ++r) {
-      uint32_t carry = words[r * stride + w];
+      uint32_t wv[kMajU];
 #pragma unroll
-      for (int p = 0; p < 6; ++p) {
-        const uint32_t t = c[p] & carry;
-        c[p] ^= carry;
-        carry = t;
+      for (int u = 0; u < kMajU; ++u) {   // every word of the round in flight before any is used
+        const int64_t e = base + 256 * u + 4 * lane;
+        wv[u] = e < n ? words[r * stride + (e >> 5)] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kMajU; ++u) {
+        const uint32_t nib = wv[u] >> (4 * (lane & 7));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ones[u][j] += (nib >> j) & 1u;
       }
     }
-    const int64_t e = w * 32;
-#pragma unroll 4
-    for (int j = 0; j < 32; ++j) {
-      if (e + j >= n) break;
-      uint32_t ones = 0;
 #pragma unroll
-      for (int p = 0; p < 6; ++p) ones |= ((c[p] >> j) & 1u) << p;
-      out[e + j] = 2 * (int)ones - world >= 0 ? 1.f : -1.f;
+    for (int u = 0; u < kMajU; ++u) {
+      const int64_t e = base + 256 * u + 4 * lane;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = 2 * (int)ones[u][j] - world >= 0 ? 1.f : -1.f;
+      if (vec && e + 3 < n) {
+        *reinterpret_cast<float4*>(out + e) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (e + j < n) out[e + j] = v[j];
+      }
+    }
+  }
+}
+
+// sign encode straight into the 1-bit layout (signsgd.py:13-16, code = x >= 0: -0 -> 1, NaN -> 0):
+// lane l reads elements base + 4 l .. + 3 as one float4, four wave ballots collect the codes, and
+// lanes 0..7 assemble and store the wave's 8 words (bit e % 32 of word e / 32, LSB first, as
+// pack_bits_kernel).  The u8 codes are never stored.
+__device__ __forceinline__ uint32_t spread4(uint32_t b) {   // bit i of b (i < 8) -> bit 4 i
+  b = (b | (b << 12)) & 0x000F000Fu;
+  b = (b | (b << 6)) & 0x03030303u;
+  b = (b | (b << 3)) & 0x11111111u;
+  return b;
+}
+constexpr int kEncU = 4;
+__global__ __launch_bounds__(kWBlock) void sign_encode_bits_kernel(const float* __restrict__ x, int64_t n,
+                                                                  uint32_t* __restrict__ words) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (kWBlock / 64);
+  const int64_t wave = (int64_t)blockIdx.x * (kWBlock / 64) + (threadIdx.x >> 6);
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;
+  const int64_t nw = (n + 31) >> 5;
+  for (int64_t base = wave * 256 * kEncU; base < n; base += nwaves * 256 * kEncU) {
+    float v[kEncU][4];
+#pragma unroll
+    for (int u = 0; u < kEncU; ++u) {
+      const int64_t e = base + 256 * u + 4 * lane;
+      if (vec && e + 3 < n) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v q = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + e));
+        v[u][0] = q.x; v[u][1] = q.y; v[u][2] = q.z; v[u][3] = q.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = e + j < n ? x[e + j] : -1.f;   // past n: code 0
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kEncU; ++u) {
+      uint64_t bal[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bal[j] = __ballot(v[u][j] >= 0.f);
+      if (lane < 8) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wd |= spread4((uint32_t)(bal[j] >> (8 * lane)) & 0xFFu) << j;
+        const int64_t wi = ((base + 256 * u) >> 5) + lane;
+        if (wi < nw) words[wi] = wd;
+      }
     }
   }
 }
@@ -156,6 +221,14 @@ grace_status_t grace_pack_bits(const uint8_t* codes, int64_t n, uint32_t* words,
   return GRACE_OK;
 }
 
+grace_status_t grace_sign_encode_bits(const float* x, int64_t n, uint32_t* words, void* stream) {
+  GRACE_REQUIRE(x && words && n >= 0, "grace_sign_encode_bits: bad arguments");
+  if (n == 0) return GRACE_OK;
+  sign_encode_bits_kernel<<<stream_grid((n + 1023) / 1024, kEncU, 4096), kWBlock, 0, as_stream(stream)>>>(x, n, words);
+  GRACE_CHECK_LAUNCH("grace_sign_encode_bits");
+  return GRACE_OK;
+}
+
 grace_status_t grace_unpack_bits(const uint32_t* words, int64_t n, uint8_t* codes, void* stream) {
   GRACE_REQUIRE(codes && words && n >= 0, "grace_unpack_bits: bad arguments");
   const int64_t nw = (n + 31) / 32;
@@ -170,8 +243,8 @@ grace_status_t grace_sign_majority_bits(const uint32_t* words, int64_t stride_wo
   GRACE_REQUIRE(words && out && world >= 1 && world <= 63 && n >= 0, "grace_sign_majority_bits: bad arguments");
   const int64_t nw = (n + 31) / 32;
   if (nw == 0) return GRACE_OK;
-  majority_bits_kernel<<<stream_grid(nw, kWBlock, 2048), kWBlock, 0, as_stream(stream)>>>(words, stride_words, world,
-                                                                                         n, out);
+  majority_bits_kernel<<<stream_grid((n + 1023) / 1024, kMajU, 4096), kWBlock, 0, as_stream(stream)>>>(
+      words, stride_words, world, n, out);
   GRACE_CHECK_LAUNCH("grace_sign_majority_bits");
   return GRACE_OK;
 }

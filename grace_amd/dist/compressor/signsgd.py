@@ -21,10 +21,9 @@ class SignSGDCompressor(Compressor):
         self.wire = wire
 
     def compress(self, tensor, name):
-        codes = ops.sign_encode(tensor)
         if self.wire == "bits":
-            return [ops.pack_bits(codes)], tensor.size()
-        return [codes], tensor.size()
+            return [ops.sign_encode_bits(tensor)], tensor.size()   # one pass, no u8 codes
+        return [ops.sign_encode(tensor)], tensor.size()
 
     def decompress(self, tensors, shape):
         sign_encode, = tensors

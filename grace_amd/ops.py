@@ -832,6 +832,15 @@ def pack_bits(codes):
     return words
 
 
+def sign_encode_bits(x):
+    """sign codes (x >= 0) of a f32 device tensor straight into int32 words (the pack_bits layout)."""
+    x = dev_f32(x)
+    n = x.numel()
+    words = torch.empty((n + 31) // 32, dtype=torch.int32, device=x.device)
+    _lib.call("grace_sign_encode_bits", _p(x), n, _p(words), _stream())
+    return words
+
+
 def unpack_bits(words, n):
     words = require_dev(words, "words")
     codes = torch.empty(n, dtype=torch.uint8, device=words.device)

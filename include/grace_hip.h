@@ -398,6 +398,9 @@ grace_status_t grace_clip_by_sumsq(const float* x, const float* sumsq_dev, float
  * 2-bit: grace_dl/tensorflow/compressor/packing.py:4-29 byte layout (planar quarters, pad values
  * range(0, 4 - n % 4)); grace_pack2_bytes(n) output bytes.  TernGrad codes travel as code + 1. */
 grace_status_t grace_pack_bits(const uint8_t* codes, int64_t n, uint32_t* words, void* stream);
+/* SignSGDCompressor.compress (signsgd.py:13-16) straight into the 1-bit layout: word i bit j =
+ * (x[32 i + j] >= 0); the words grace_pack_bits would make from grace_sign_encode's codes. */
+grace_status_t grace_sign_encode_bits(const float* x, int64_t n, uint32_t* words, void* stream);
 grace_status_t grace_unpack_bits(const uint32_t* words, int64_t n, uint8_t* codes, void* stream);
 grace_status_t grace_sign_majority_bits(const uint32_t* words, int64_t stride_words, int32_t world, int64_t n,
                                         float* out, void* stream);

@@ -30,7 +30,24 @@ def test_pack_bits_roundtrip(n):
     assert np.array_equal(_np(ops.unpack_bits(words, n)), codes)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 4, 7])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 255, 256, 1023, 4097, (1 << 20) + 5])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_sign_encode_bits_equals_pack_of_codes(n, offset):
+    """grace_sign_encode_bits (one pass) == pack_bits(sign_encode(x)), incl. -0, NaN, +-inf, ragged
+    tails and a misaligned input view (offset 1: the scalar path)."""
+    rng = np.random.default_rng(n + offset)
+    x = rng.standard_normal(n + offset).astype(np.float32)
+    for v in (-0.0, 0.0, np.nan, np.inf, -np.inf):
+        x[rng.integers(0, n + offset, 3)] = v
+    xt = _t(x)[offset:]
+    got = _np(ops.sign_encode_bits(xt))
+    exp = _np(ops.pack_bits(ops.sign_encode(xt)))
+    assert np.array_equal(got, exp)
+    assert np.array_equal(got.view(np.uint8)[:(n + 7) // 8],
+                          np.packbits(O.sign_encode(x[offset:]).astype(np.uint8), bitorder="little"))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8, 16])
 def test_majority_bits_equals_u8(world):
     n = 100003
     rng = np.random.default_rng(world)
