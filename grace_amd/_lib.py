@@ -61,6 +61,8 @@ SIGNATURES = {
     "grace_dgc_write": (ST, [P, I64, P, P, P, P]),
     "grace_dgc_compensate": (ST, [P, P, P, I32, F32, I64, P]),
     "grace_dgc_mask_update": (ST, [P, P, P, I64, P, P]),
+    "grace_dgc_select": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),
+    "grace_dgc_step_w1": (ST, [P, P, P, I64, P, P, P]),
     "grace_sumsq_workspace_bytes": (SZ, []),
     "grace_sumsq": (ST, [P, I64, P, P, P]),
     "grace_clip_by_sumsq": (ST, [P, P, F32, P, I64, P]),

@@ -28,6 +28,8 @@ constexpr int kDChunk = 4096;          // elements per compaction chunk
 constexpr int kDepth = 10;              // dgc.py:26 range(10)
 constexpr int kNodes = (1 << (kDepth + 1)) - 1;   // 2047 thresholds the loop can visit
 constexpr int kTab = 2048;              // sorted table (padded with +inf)
+constexpr int kDQ = 4;                  // quads per thread per round in the streaming passes
+typedef float f4d __attribute__((ext_vector_type(4)));
 
 struct DgcMeta {
   uint32_t thr0;      // bits of the sampled threshold
@@ -37,10 +39,14 @@ struct DgcMeta {
   uint32_t pad[12];
 };
 
+constexpr int kLutShift = 18;                         // coarse key bins: 1/32 octave
+constexpr int kLut = (0x7F800000 >> kLutShift) + 2;   // every finite / inf key's bin, plus its end
+
 struct DgcWs {
   DgcMeta* meta;
   float* tab;         // [kTab] ascending
   uint32_t* hist;     // [kTab + 1]
+  uint16_t* lut;      // [kLut]: table entries with key < (b << kLutShift)
   uint32_t* part;     // [nchunks] counts
   uint32_t* offs;     // [nchunks] exclusive offsets
 };
@@ -57,6 +63,8 @@ static DgcWs dgc_carve(void* ws, int64_t n) {
   p += al256(sizeof(float) * kTab);
   w.hist = reinterpret_cast<uint32_t*>(p);
   p += al256(sizeof(uint32_t) * (kTab + 1));
+  w.lut = reinterpret_cast<uint16_t*>(p);
+  p += al256(sizeof(uint16_t) * kLut);
   w.part = reinterpret_cast<uint32_t*>(p);
   p += al256(sizeof(uint32_t) * nch);
   w.offs = reinterpret_cast<uint32_t*>(p);
@@ -66,7 +74,7 @@ static DgcWs dgc_carve(void* ws, int64_t n) {
 static size_t dgc_ws_bytes(int64_t n) {
   const int64_t nch = (n + kDChunk - 1) / kDChunk;
   return 256 + al256(sizeof(float) * kTab) + al256(sizeof(uint32_t) * (kTab + 1)) +
-         2 * al256(sizeof(uint32_t) * nch);
+         al256(sizeof(uint16_t) * kLut) + 2 * al256(sizeof(uint32_t) * nch);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -148,6 +156,18 @@ __global__ __launch_bounds__(1024) void dgc_table_kernel(const float* __restrict
   }
   for (int e = t; e < kTab; e += 1024) w.tab[e] = s[e];
   for (int e = t; e <= kTab; e += 1024) w.hist[e] = 0u;
+  // coarse-bin index: lut[b] = number of entries whose key is below b << kLutShift, so an element
+  // of coarse bin b has its upper bound in [lut[b], lut[b + 1]] (entries are >= 0 or +inf, or all
+  // NaN, which nothing passes)
+  for (int b = t; b < kLut; b += 1024) {
+    const uint32_t kb = (uint32_t)b << kLutShift;
+    int lo = 0, hi = kTab;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (__float_as_uint(s[mid]) < kb) lo = mid + 1; else hi = mid;
+    }
+    w.lut[b] = (uint16_t)lo;
+  }
 }
 
 // number of table entries <= key (upper bound); NaN compares false -> 0
@@ -161,29 +181,53 @@ __device__ __forceinline__ int tab_bin(const float* tab, float key) {
   return lo;
 }
 
+// tab_bin through the coarse-bin index: a binary search over the few entries of the key's 1/32
+// octave instead of all 2048 (11 dependent LDS reads per element made the pass 0.94 TB/s)
+__device__ __forceinline__ int tab_bin_lut(const float* tab, const uint16_t* lut, float key) {
+  const uint32_t b = __float_as_uint(key) >> kLutShift;   // key >= tab[0] >= 0 here
+  int lo = lut[b], hi = lut[b + 1];
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (key >= tab[mid]) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
 // one pass: histogram of |t| over the table (elements below the smallest entry skip the search)
 __global__ __launch_bounds__(kDBlock) void dgc_count_kernel(const float* __restrict__ t, int64_t n, DgcWs w) {
   __shared__ float tab[kTab];
   __shared__ uint32_t h[kTab + 1];
+  __shared__ uint16_t lut[kLut];
   for (int e = threadIdx.x; e < kTab; e += kDBlock) tab[e] = w.tab[e];
   for (int e = threadIdx.x; e <= kTab; e += kDBlock) h[e] = 0u;
+  for (int e = threadIdx.x; e < kLut; e += kDBlock) lut[e] = w.lut[e];
   __syncthreads();
   const float t0 = tab[0];
   const int64_t n4 = n >> 2;
   const bool vec = (reinterpret_cast<uintptr_t>(t) & 15u) == 0;
   const int64_t stride = (int64_t)gridDim.x * kDBlock;
   if (vec) {
-    for (int64_t q = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q < n4; q += stride) {
-      const float4 v = reinterpret_cast<const float4*>(t)[q];
-      const float a[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+    for (int64_t q0 = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q0 < n4; q0 += stride * kDQ) {
+      f4d v[kDQ];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (a[j] >= t0) atomicAdd(&h[tab_bin(tab, a[j])], 1u);
+      for (int u = 0; u < kDQ; ++u) {   // every quad of the round in flight before any is searched
+        const int64_t q = q0 + u * stride < n4 ? q0 + u * stride : q0;
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(t) + q);
+      }
+#pragma unroll
+      for (int u = 0; u < kDQ; ++u) {
+        if (q0 + u * stride >= n4) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = fabsf(v[u][j]);
+          if (a >= t0) atomicAdd(&h[tab_bin_lut(tab, lut, a)], 1u);
+        }
+      }
     }
   }
   for (int64_t i = (vec ? n4 * 4 : 0) + (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += stride) {
     const float a = fabsf(t[i]);
-    if (a >= t0) atomicAdd(&h[tab_bin(tab, a)], 1u);
+    if (a >= t0) atomicAdd(&h[tab_bin_lut(tab, lut, a)], 1u);
   }
   __syncthreads();
   for (int e = threadIdx.x; e <= kTab; e += kDBlock)
@@ -194,10 +238,37 @@ __global__ __launch_bounds__(kDBlock) void dgc_count_kernel(const float* __restr
 // lower-bound position p is the number of elements whose bin is > p
 __global__ void dgc_replay_kernel(int64_t n, double ratio, DgcWs w) {
   __shared__ uint32_t suf[kTab + 2];
+  __shared__ float tab[kTab];
+  // the histogram and the table into LDS by every lane (the single-thread replay below then reads
+  // no global memory in its dependent chains: 62 -> a few us)
+  for (int e = threadIdx.x; e < kTab; e += blockDim.x) tab[e] = w.tab[e];
+  {  // suffix sums of the kTab + 1 bins: lane l owns a contiguous run, one wave scan of the run totals
+    constexpr int kRun = (kTab + 1 + 63) / 64;
+    const int l = threadIdx.x;            // launched with exactly one wave
+    uint32_t v[kRun], tot = 0;
+#pragma unroll
+    for (int i = 0; i < kRun; ++i) {
+      const int b = l * kRun + i;
+      v[i] = b <= kTab ? w.hist[b] : 0u;
+      tot += v[i];
+    }
+    uint32_t above = tot;                 // inclusive scan from the top lane down
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_down(above, o, 64);
+      if (l + o < 64) above += x;
+    }
+    uint32_t acc = above - tot;           // bins of the lanes above this one
+#pragma unroll
+    for (int i = kRun - 1; i >= 0; --i) {
+      const int b = l * kRun + i;
+      acc += v[i];
+      if (b <= kTab) suf[b] = acc;
+    }
+    if (l == 0) suf[kTab + 1] = 0;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
-  uint32_t acc = 0;
-  suf[kTab + 1] = 0;
-  for (int b = kTab; b >= 0; --b) { acc += w.hist[b]; suf[b] = acc; }
   // torch compares the int64 count tensor with the Python float (1.3 * numel * ratio, a double)
   // in the default dtype, f32
   const float hi = (float)(1.3 * (double)n * ratio);
@@ -207,7 +278,7 @@ __global__ void dgc_replay_kernel(int64_t n, double ratio, DgcWs w) {
     int a = 0, b = kTab;            // first index with tab >= x
     while (a < b) {
       const int mid = (a + b) >> 1;
-      if (w.tab[mid] < x) a = mid + 1; else b = mid;
+      if (tab[mid] < x) a = mid + 1; else b = mid;
     }
     return suf[a + 1];
   };
@@ -301,33 +372,99 @@ __global__ __launch_bounds__(kDBlock) void dgc_write_kernel(const float* __restr
 
 // ------------------------------------------------------------------------------------------------
 // memory
+// Elementwise memory kernels: a thread owns kDQ quads per round (16-B loads, all issued before use)
+// when every buffer is 16-B aligned; the scalar loop covers the rest.  (One 4-B access per thread
+// per element made the 256 MiB DGC step 1.36 ms.)
+__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
 // compensate: r = m r + g (r = g first), a = a + r (a = g first); returns a in `acc`
+__device__ __forceinline__ void dgc_comp1(float gv, float& rv, float& av, int has_state, float m) {
+  if (has_state) { rv = m * rv + gv; av = av + rv; } else { rv = gv; av = gv; }
+}
 __global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __restrict__ g, float* __restrict__ r,
                                                                 float* __restrict__ a, int has_state,
                                                                 float momentum, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock) {
-    const float gv = g[i];
-    if (has_state) {
-      const float rv = momentum * r[i] + gv;
-      r[i] = rv;
-      a[i] = a[i] + rv;
-    } else {
-      r[i] = gv;
-      a[i] = gv;
+  const int64_t stride = (int64_t)gridDim.x * kDBlock;
+  const int64_t nq = (al16(g) && al16(r) && al16(a)) ? n >> 2 : 0;
+  for (int64_t q0 = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q0 < nq; q0 += stride * kDQ) {
+    f4d gv[kDQ], rv[kDQ], av[kDQ];
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      const int64_t q = q0 + u * stride < nq ? q0 + u * stride : q0;
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(g) + q);
+      if (has_state) {
+        rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(r) + q);
+        av[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(a) + q);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      if (q0 + u * stride >= nq) break;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float rj = has_state ? rv[u][j] : 0.f, aj = has_state ? av[u][j] : 0.f;
+        dgc_comp1(gv[u][j], rj, aj, has_state, momentum);
+        rv[u][j] = rj;
+        av[u][j] = aj;
+      }
+      __builtin_nontemporal_store(rv[u], reinterpret_cast<f4d*>(r) + q0 + u * stride);
+      __builtin_nontemporal_store(av[u], reinterpret_cast<f4d*>(a) + q0 + u * stride);
+    }
+  }
+  for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += stride) {
+    float rv = has_state ? r[i] : 0.f, av = has_state ? a[i] : 0.f;
+    dgc_comp1(g[i], rv, av, has_state, momentum);
+    r[i] = rv;
+    a[i] = av;
   }
 }
 
 // update: keep = !(|t| >= thr) as in mask = tensor.abs() >= thr; r = r * keep, a = a * keep
-// (t is the compensated tensor the mask came from; it may alias a)
+// (t is the compensated tensor the mask came from; it may alias a).  OUT: the world-1 Allgather
+// result in the same pass, out = 0 + t where selected and 0 elsewhere -- (0 + decompress) / 1
+// of the payload grace_dgc_write would have produced (dgc.py:45-50, allgather.py:40-45).
+template <bool OUT>
 __global__ __launch_bounds__(kDBlock) void dgc_mask_kernel(const float* t, float* r, float* a, int64_t n,
-                                                          const DgcMeta* __restrict__ meta) {
+                                                          const DgcMeta* __restrict__ meta, float* out) {
   const float thr = __uint_as_float(meta->thr);
-  for (int64_t i = (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kDBlock) {
-    const float keep = fabsf(t[i]) >= thr ? 0.f : 1.f;
-    const float av = t == a ? t[i] : a[i];
+  const bool alias = t == a;
+  const int64_t stride = (int64_t)gridDim.x * kDBlock;
+  const int64_t nq = (al16(t) && al16(r) && al16(a) && (!OUT || al16(out))) ? n >> 2 : 0;
+  for (int64_t q0 = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q0 < nq; q0 += stride * kDQ) {
+    f4d tv[kDQ], rv[kDQ], av[kDQ];
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      const int64_t q = q0 + u * stride < nq ? q0 + u * stride : q0;
+      tv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(t) + q);
+      rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(r) + q);
+      if (!alias) av[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(a) + q);
+    }
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      if (q0 + u * stride >= nq) break;
+      f4d o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool sel = fabsf(tv[u][j]) >= thr;
+        const float keep = sel ? 0.f : 1.f;
+        const float avj = alias ? tv[u][j] : av[u][j];
+        o[j] = sel ? 0.f + tv[u][j] : 0.f;
+        rv[u][j] = rv[u][j] * keep;
+        av[u][j] = avj * keep;
+      }
+      __builtin_nontemporal_store(rv[u], reinterpret_cast<f4d*>(r) + q0 + u * stride);
+      __builtin_nontemporal_store(av[u], reinterpret_cast<f4d*>(a) + q0 + u * stride);
+      if constexpr (OUT) __builtin_nontemporal_store(o, reinterpret_cast<f4d*>(out) + q0 + u * stride);
+    }
+  }
+  for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += stride) {
+    const float tv = t[i];
+    const bool sel = fabsf(tv) >= thr;
+    const float keep = sel ? 0.f : 1.f;
+    const float av = alias ? tv : a[i];
     r[i] = r[i] * keep;
     a[i] = av * keep;
+    if constexpr (OUT) out[i] = sel ? 0.f + tv : 0.f;
   }
 }
 
@@ -415,7 +552,7 @@ grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accu
                                     float momentum, int64_t n, void* stream) {
   GRACE_REQUIRE(g && residual && accum && n >= 0, "grace_dgc_compensate: bad arguments");
   if (n == 0) return GRACE_OK;
-  dgc_compensate_kernel<<<stream_grid(n, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(g, residual, accum,
+  dgc_compensate_kernel<<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(g, residual, accum,
                                                                                          has_state, momentum, n);
   GRACE_CHECK_LAUNCH("grace_dgc_compensate");
   return GRACE_OK;
@@ -425,9 +562,33 @@ grace_status_t grace_dgc_mask_update(const float* t, float* residual, float* acc
                                      void* stream) {
   GRACE_REQUIRE(t && residual && accum && ws && n >= 0, "grace_dgc_mask_update: bad arguments");
   if (n == 0) return GRACE_OK;
-  dgc_mask_kernel<<<stream_grid(n, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(
-      t, residual, accum, n, reinterpret_cast<const DgcMeta*>(ws));
+  dgc_mask_kernel<false><<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(
+      t, residual, accum, n, reinterpret_cast<const DgcMeta*>(ws), nullptr);
   GRACE_CHECK_LAUNCH("grace_dgc_mask_update");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_select(const float* t, int64_t n, const float* top_vals, int64_t ks, double ratio, void* ws,
+                                void* stream) {
+  GRACE_REQUIRE(t && top_vals && ws && n >= 1 && ks >= 1, "grace_dgc_select: bad arguments");
+  hipStream_t s = as_stream(stream);
+  DgcWs w = dgc_carve(ws, n);
+  dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_select");
+  dgc_count_kernel<<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_select");
+  dgc_replay_kernel<<<1, 64, 0, s>>>(n, ratio, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_select");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_step_w1(const float* t, float* residual, float* accum, int64_t n, const void* ws, float* out,
+                                 void* stream) {
+  GRACE_REQUIRE(t && residual && accum && ws && out && n >= 0, "grace_dgc_step_w1: bad arguments");
+  if (n == 0) return GRACE_OK;
+  dgc_mask_kernel<true><<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(
+      t, residual, accum, n, reinterpret_cast<const DgcMeta*>(ws), out);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1");
   return GRACE_OK;
 }
 

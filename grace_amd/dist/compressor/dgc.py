@@ -24,23 +24,41 @@ class DgcCompressor(Compressor):
         self.rng = rng
         self._step = 0
 
-    def compress(self, tensor, name):
-        shape = tensor.size()
-        t = ops.dev_f32(tensor)
+    def _sampling(self, t, name):
+        """(sample indices, seed) of this call: the reference's CPU uniform_ stream in parity mode,
+        else the device generator keyed by (name, step)."""
         numel = t.numel()
-        sidx = None
-        seed = 0
         if self.rng == "torch_cpu":
             ns = max(1, int(numel * 0.01))
             cpu = torch.empty([ns]).uniform_(0, numel).type(torch.long)
             if ns and int(cpu.max()) >= numel:       # the reference would raise IndexError here
                 raise IndexError(f"DGC sample index {int(cpu.max())} out of range for {numel} elements")
-            sidx = cpu.to(t.device)
-        else:
-            self._step += 1
-            seed = ops.step_seed("dgc", name, self._step)
+            return cpu.to(t.device), 0
+        self._step += 1
+        return None, ops.step_seed("dgc", name, self._step)
+
+    def compress(self, tensor, name):
+        shape = tensor.size()
+        t = ops.dev_f32(tensor)
+        sidx, seed = self._sampling(t, name)
         vals, idx, meta = ops.dgc_compress(t, self.compress_ratio, sample_idx=sidx, seed=seed)
-        return (vals, idx), (shape, meta, numel)
+        return (vals, idx), (shape, meta, t.numel())
+
+    def fused_step(self, communicator, tensor, name):
+        """World-1 Allgather(DgcCompressor, DgcMemory).step: compensate, the threshold, then ONE
+        pass for DgcMemory.update and (0 + decompress) / 1 -- the same values as the four calls,
+        without materialising the payload or reading its size on the host."""
+        from grace_amd.dist.communicator.allgather import Allgather
+        from grace_amd.dist.memory.dgc import DgcMemory
+        mem = communicator.memory
+        if not (type(communicator) is Allgather and type(mem) is DgcMemory and int(communicator.world_size) == 1
+                and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
+            return None
+        t = ops.dev_f32(mem.compensate(tensor, name))
+        sidx, seed = self._sampling(t, name)
+        ws = ops.dgc_select(t, self.compress_ratio, sample_idx=sidx, seed=seed)
+        out = ops.dgc_step_w1(t, mem.residuals[name], mem.gradients[name], ws)
+        return out.view(tensor.shape)
 
     def decompress(self, tensor_compressed, ctx):
         values, indices = tensor_compressed

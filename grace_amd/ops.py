@@ -798,6 +798,28 @@ def dgc_compress(t, ratio, sample_idx=None, seed=0):
     return vals, idx, meta
 
 
+def dgc_select(t, ratio, sample_idx=None, seed=0):
+    """The sampled threshold and its adjustment loop only (grace_dgc_select); returns the DGC
+    workspace whose first 16 bytes are the meta grace_dgc_step_w1 / dgc_mask_update read."""
+    t = dev_f32(t)
+    n = t.numel()
+    ns = max(1, int(n * 0.01))
+    ks = max(1, int(n * ratio * 0.01))
+    sample = torch.empty(ns, dtype=F32, device=t.device)
+    _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
+    _, top, _ = topk_compress(sample, min(ks, ns))
+    ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
+    _lib.call("grace_dgc_select", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    return ws
+
+
+def dgc_step_w1(t, residual, accum, ws, out=None):
+    t = dev_f32(t)
+    out = torch.empty_like(t) if out is None else out
+    _lib.call("grace_dgc_step_w1", _p(t), _p(residual), _p(accum), t.numel(), _p(ws), _p(out), _stream())
+    return out
+
+
 def dgc_compensate(g, residual, accum, has_state, momentum):
     _lib.call("grace_dgc_compensate", _p(dev_f32(g)), _p(residual), _p(accum), 1 if has_state else 0,
               float(momentum), g.numel(), _stream())

@@ -385,6 +385,15 @@ grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accu
                                     float momentum, int64_t n, void* stream);
 grace_status_t grace_dgc_mask_update(const float* t, float* residual, float* accum, int64_t n, const void* meta,
                                      void* stream);
+/* grace_dgc_threshold without the payload bookkeeping: the sampled threshold and the 10-step
+ * adjustment only (meta at ws). */
+grace_status_t grace_dgc_select(const float* t, int64_t n, const float* top_vals, int64_t ks, double ratio, void* ws,
+                                void* stream);
+/* World-1 Allgather(DgcCompressor, DgcMemory).step after grace_dgc_select: DgcMemory.update
+ * (r *= keep, a *= keep) and out = (0 + decompress(payload)) / 1 = (|t| >= thr ? 0 + t : 0) in one
+ * pass; the payload and its host-read size are never materialised.  t may alias accum. */
+grace_status_t grace_dgc_step_w1(const float* t, float* residual, float* accum, int64_t n, const void* ws, float* out,
+                                 void* stream);
 /* gradient clipping (memory/dgc.py:16-19): s = sum(x*x) (f64 accumulate) into out_dev; after the
  * caller's all_reduce of s: out = clamp(x, -c, c), c = sqrt(s / world) */
 size_t grace_sumsq_workspace_bytes(void);

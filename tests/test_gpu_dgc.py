@@ -96,3 +96,36 @@ def test_dgc_nan_sample_selects_nothing():
     vals, idx, _ = ops.dgc_compress(_t(x), 0.1, sample_idx=_t(sidx))
     ev, ei, _, _ = O.dgc_compress(x, sidx, 0.1)
     assert vals.numel() == ev.size == 0
+
+
+@pytest.mark.parametrize("n", [1000, 4097, (1 << 20) + 3])
+@pytest.mark.parametrize("rng", ["device", "torch_cpu"])
+def test_dgc_world1_fused_step_equals_unfused(n, rng):
+    """Allgather(DgcCompressor, DgcMemory).step at world 1 through the one-pass path
+    (grace_dgc_select + grace_dgc_step_w1) against the reference's four calls on the same engine:
+    outputs and both memory states bit-exact over 3 steps (momentum state carried)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.dgc import DgcCompressor
+    from grace_amd.dist.memory.dgc import DgcMemory
+    gs = [np.random.default_rng(n + s).standard_normal(n).astype(np.float32) for s in range(3)]
+    runs = []
+    for fused in (True, False):
+        torch.manual_seed(5)
+        comm = Allgather(DgcCompressor(0.01, rng=rng), DgcMemory(0.9, False, 1), 1)
+        outs = []
+        for s in range(3):
+            g = _t(gs[s])
+            if fused:
+                out = comm.step(g, "w")
+            else:
+                t = comm.memory.compensate(g, "w")
+                payload, ctx = comm.compressor.compress(t, "w")
+                comm.memory.update(t, "w", comm.compressor, payload, ctx)
+                out = comm.send_receive(payload, "w", ctx)
+            outs.append(_np(out))
+        runs.append((outs, _np(comm.memory.residuals["w"]), _np(comm.memory.gradients["w"])))
+    (fo, fr, fa), (uo, ur, ua) = runs
+    for s in range(3):
+        assert same_bits(fo[s], uo[s]), s
+    assert same_bits(fr, ur) and same_bits(fa, ua)
+    assert np.count_nonzero(fo[-1]) > 0
