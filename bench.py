@@ -29,6 +29,7 @@ Secondary workloads (``--workload``; same JSON schema, reported in DESIGN.md, no
   powersgd   PowerSGD rank 4 compress + decompress on a 4096 x 4096 gradient (configs[3])
   dgc        DGC 1 % with momentum-correction memory on the 256 MiB bucket
   sign_bits  signSGD with the 1-bit wire layout, compress + Allgather decode, 256 MiB (8f.4)
+  randomk / threshold  RandomK 1 % / Threshold with residual memory on the 256 MiB bucket (8a)
 
 Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
@@ -58,7 +59,7 @@ def parse():
     ap.add_argument("--workload", default="topk",
                     choices=["topk", "topk_nomem", "topk_e2e", "topk_sharded", "sign", "sign256", "qsgd", "terngrad", "qsgd_step", "terngrad_step", "powersgd",
                              "natural", "cnat", "fp16", "ddp_params", "ddp_bucket", "ddp_segmented", "dgc",
-                             "sign_bits"])
+                             "sign_bits", "randomk", "threshold"])
     ap.add_argument("--ratio", type=float, default=0.01)
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024)
     ap.add_argument("--buffers", type=int, default=3, help="distinct buckets rotated (defeats MALL reuse)")
@@ -125,7 +126,8 @@ def main():
             dist.init_process_group(backend)
     run = {"topk": bench_topk, "topk_nomem": bench_topk_nomem, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant, "qsgd_step": bench_quant, "terngrad_step": bench_quant,
-           "terngrad": bench_quant, "powersgd": bench_powersgd, "dgc": bench_dgc, "sign_bits": bench_sign_bits, "natural": bench_cast, "cnat": bench_cast,
+           "terngrad": bench_quant, "powersgd": bench_powersgd, "dgc": bench_dgc, "sign_bits": bench_sign_bits,
+           "randomk": bench_sparse, "threshold": bench_sparse, "natural": bench_cast, "cnat": bench_cast,
            "fp16": bench_cast}[args.workload]
     line = run(args, world, rank, dev)
     if args.workload == "topk" and world > 1 and not args.no_sharded:
@@ -531,6 +533,38 @@ def bench_cast(args, world, rank, dev):
 
 
 # ------------------------------------------------------------------------------------------ PowerSGD
+def bench_sparse(args, world, rank, dev):
+    """SURVEY.md 8a rows a6 / a7 on the 256 MiB bucket with ResidualMemory: Allgather(RandomK 1 %)
+    and Allgather(Threshold), the threshold at 2.5758 (|x| above it: 1 % of N(0, 1) on the first
+    step; the residual grows it afterwards, as in training)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = args.numel
+    if args.workload == "randomk":
+        from grace_amd.dist.compressor.randomk import RandomKCompressor
+        comp = RandomKCompressor(args.ratio)
+        desc = "Allgather(RandomK 1%, ResidualMemory).step"
+    else:
+        from grace_amd.dist.compressor.threshold import ThresholdCompressor
+        comp = ThresholdCompressor(2.5758)
+        desc = "Allgather(Threshold 2.5758, ResidualMemory).step"
+    comm = Allgather(comp, ResidualMemory(), world)
+    grads = [torch.randn(n, device=dev) for _ in range(args.buffers)]
+    for j in range(args.buffers):
+        comm.step(grads[j], f"b{j}")
+    elapsed = timed(lambda i: comm.step(grads[i % args.buffers], f"b{i % args.buffers}"), args.steps, args.warmup,
+                    world, dev)
+    line = base_line(args, world, elapsed, 4.0 * n,
+                     metric=f"grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket, {args.workload}")
+    line["config"] = {"workload": f"{desc} on a 256 MiB fp32 bucket (SURVEY.md 8a)", "numel": n}
+    alg = 16.0 * n                       # g, r read; r', dense out written (payload bytes excluded)
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": alg}
+    return line
+
+
 def bench_dgc(args, world, rank, dev):
     """Allgather(DgcCompressor(1 %), DgcMemory(0.9)).step on the 256 MiB
     bucket (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39).  The payload size is data

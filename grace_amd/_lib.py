@@ -112,6 +112,7 @@ SIGNATURES = {
     "grace_cast_step_w1": (ST, [P, I64, I32, U64, P, P]),
     "grace_randomk_indices": (ST, [U64, I64, I64, P, P]),
     "grace_gather": (ST, [P, P, I64, P, P]),
+    "grace_randomk_step_w1": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, P]),
     "grace_threshold_workspace_bytes": (SZ, [I64]),
     "grace_threshold_count": (ST, [P, I64, F32, P, P]),
     "grace_threshold_recount": (ST, [P, I64, F32, P, P]),

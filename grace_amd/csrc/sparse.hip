@@ -33,6 +33,58 @@ __global__ __launch_bounds__(kSBlock) void gather_kernel(const float* __restrict
     vals[j] = x[idx[j]];
 }
 
+// World-1 Allgather(RandomK, ResidualMemory).step (randomk.py:24-41, residual.py:10-20,
+// allgather.py:40-45) in three launches instead of compensate + gather + two decodes + subtract +
+// sum: (1) one streaming pass t = beta r + gamma g -> r' = t, out = 0 (16 B per element); (2) the
+// payload gather vals = t[idx]; (3) the scatter out[idx] = 0 + vals, r'[idx] = vals - vals.  The
+// gather completes before the scatter (kernel boundary), so duplicate indices (drawn with
+// replacement) read t, never a zeroed entry -- as zeros.scatter_ / t - decompress do.
+constexpr int kRQ = 4;   // quads per lane per round, all loads in flight first
+template <bool HAS_RES>
+__global__ __launch_bounds__(kSBlock) void randomk_pass_kernel(const float* __restrict__ g, float* __restrict__ r,
+                                                              float beta, float gamma, int64_t n,
+                                                              float* __restrict__ out) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int64_t stride = (int64_t)gridDim.x * kSBlock;
+  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r) |
+                     reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
+  const int64_t nq = vec ? n >> 2 : 0;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t q0 = (int64_t)blockIdx.x * kSBlock + threadIdx.x; q0 < nq; q0 += stride * kRQ) {
+    f4 gv[kRQ], rv[kRQ];
+#pragma unroll
+    for (int u = 0; u < kRQ; ++u) {
+      const int64_t q = q0 + u * stride < nq ? q0 + u * stride : q0;
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q);
+      if (HAS_RES) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(r) + q);
+    }
+#pragma unroll
+    for (int u = 0; u < kRQ; ++u) {
+      if (q0 + u * stride >= nq) break;
+      f4 t = gv[u];
+      if (HAS_RES) t = f4{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
+                          beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
+      __builtin_nontemporal_store(t, reinterpret_cast<f4*>(r) + q0 + u * stride);
+      __builtin_nontemporal_store(z, reinterpret_cast<f4*>(out) + q0 + u * stride);
+    }
+  }
+  for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kSBlock + threadIdx.x; i < n; i += stride) {
+    r[i] = HAS_RES ? beta * r[i] + gamma * g[i] : g[i];
+    out[i] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(kSBlock) void randomk_scatter_kernel(const int64_t* __restrict__ idx,
+                                                                 const float* __restrict__ vals, int64_t k,
+                                                                 float* __restrict__ r, float* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock) {
+    const int64_t i = idx[j];
+    const float v = vals[j];
+    out[i] = 0.f + v;
+    r[i] = v - v;
+  }
+}
+
 // Random-k without replacement (grace_dl/torch/compressor/randomk.py:10, randperm(numel)[:k]):
 // j -> pi(j) for j < k, pi a keyed pseudorandom permutation of [0, numel): a balanced 4-round
 // Feistel network on 2h bits (2^(2h) >= numel, so at most 4x numel) restricted to [0, numel) by
@@ -322,6 +374,23 @@ grace_status_t grace_randomk_indices(uint64_t seed, int64_t numel, int64_t k, in
   if (k == 0) return GRACE_OK;
   randomk_idx_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(seed, numel, k, idx);
   GRACE_CHECK_LAUNCH("grace_randomk_indices");
+  return GRACE_OK;
+}
+
+grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
+                                     int64_t n, const int64_t* idx, int64_t k, float* vals, float* out,
+                                     void* stream) {
+  GRACE_REQUIRE(g && residual && idx && vals && out && n >= 1 && k >= 0, "grace_randomk_step_w1: bad arguments");
+  hipStream_t s = as_stream(stream);
+  const unsigned grid = stream_grid((n + 3) / 4, kSBlock * kRQ, 4096);
+  if (has_residual) randomk_pass_kernel<true><<<grid, kSBlock, 0, s>>>(g, residual, beta, gamma, n, out);
+  else randomk_pass_kernel<false><<<grid, kSBlock, 0, s>>>(g, residual, beta, gamma, n, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
+  if (k == 0) return GRACE_OK;
+  gather_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(residual, idx, k, vals);
+  GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
+  randomk_scatter_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(idx, vals, k, residual, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
   return GRACE_OK;
 }
 

@@ -21,17 +21,41 @@ class RandomKCompressor(Compressor):
         self.compress_ratio = compress_ratio
         self.rng = rng
 
-    def compress(self, tensor, name):
-        flat = ops.dev_f32(tensor)
+    def _indices(self, flat, name):
+        """randomk.py:26-30: the seed h, the global generator reseeded with it, k indices drawn with
+        replacement (torch's CPU stream in parity mode, else the device generator keyed by h)."""
         numel = flat.numel()
         h = sum(bytes(name, encoding='utf8'), self.global_step)
         self.global_step += 1
         torch.manual_seed(h)
         k = ops.ratio_k(numel, self.compress_ratio)
         if self.rng == "torch_cpu":
-            indices = torch.randint(numel, [k]).to(flat.device)
-        else:
-            indices = ops.randomk_indices(h, numel, k, flat.device)
+            return torch.randint(numel, [k]).to(flat.device)
+        return ops.randomk_indices(h, numel, k, flat.device)
+
+    def fused_step(self, communicator, tensor, name):
+        """World-1 Allgather(RandomK, ResidualMemory).step in three launches (grace_randomk_step_w1):
+        the same values as compensate + compress + update + send_receive."""
+        from grace_amd.dist.communicator.allgather import Allgather
+        from grace_amd.dist.memory.residual import ResidualMemory
+        mem = communicator.memory
+        if not (type(communicator) is Allgather and type(mem) is ResidualMemory and int(communicator.world_size) == 1
+                and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
+            return None
+        g = ops.dev_f32(tensor)
+        res = mem.residuals.get(name)
+        has = res is not None and res.numel() == g.numel() and res.device == g.device
+        if not has:
+            res = torch.empty_like(g)
+        indices = self._indices(g, name)
+        _, out = ops.randomk_step_w1(g, res, has, mem.beta, mem.gamma, indices)
+        mem.residuals[name] = res
+        return out.view(tensor.shape)
+
+    def compress(self, tensor, name):
+        flat = ops.dev_f32(tensor)
+        indices = self._indices(flat, name)
+        numel = flat.numel()
         values = ops.gather(flat, indices)
         ctx = indices, numel, tensor.size()
         return [values], ctx

@@ -593,6 +593,17 @@ def widen_i32(idx32):
     return out
 
 
+def randomk_step_w1(g, residual, has_residual, beta, gamma, idx):
+    """World-1 Allgather(RandomK, ResidualMemory).step (grace_randomk_step_w1): returns (vals, out)."""
+    g = dev_f32(g)
+    idx = require_dev(idx, "indices")
+    vals = torch.empty(idx.numel(), dtype=F32, device=g.device)
+    out = torch.empty_like(g)
+    _lib.call("grace_randomk_step_w1", _p(g), _p(residual), 1 if has_residual else 0, float(beta), float(gamma),
+              g.numel(), _p(idx), idx.numel(), _p(vals), _p(out), _stream())
+    return vals, out
+
+
 def gather(x, idx):
     x = dev_f32(x)
     idx = require_dev(idx)

@@ -259,6 +259,12 @@ grace_status_t grace_randomk_perm_indices(uint64_t seed, int64_t numel, int64_t 
 grace_status_t grace_widen_i32(const int32_t* src, int64_t n, int64_t* dst, void* stream);
 /* vals[j] = x[idx[j]]  (randomk.py:12 tensor[indices]) */
 grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float* vals, void* stream);
+/* World-1 Allgather(RandomK, ResidualMemory).step (randomk.py:24-41, residual.py:10-20): with the
+ * caller's idx[k] (grace_randomk_indices or torch's stream), t = beta r + gamma g (t = g when
+ * has_residual == 0), vals = t[idx], residual <- t - decode(vals), out = (0 + decode(vals)) / 1. */
+grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
+                                     int64_t n, const int64_t* idx, int64_t k, float* vals, float* out,
+                                     void* stream);
 /* Threshold (threshold.py:16-19): idx = where(|x| >= min(thr, max(x))) in ascending order.
  * count -> (host reads meta = ws[0..2]: bound bits, count, recount flag) -> [recount] -> write.
  * The caller synchronises once to size the variable-length payload. */

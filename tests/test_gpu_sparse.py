@@ -259,3 +259,35 @@ def test_sort_payload_workspace_reuse_across_sizes():
         order = np.argsort(idx)
         o2 = np.argsort(oi)
         assert np.array_equal(idx[order], oi[o2]) and np.array_equal(vals[order], ov[o2]), (n, k)
+
+
+@pytest.mark.parametrize("n", [1000, 4097, (1 << 20) + 3])
+@pytest.mark.parametrize("rng", ["device", "torch_cpu"])
+def test_randomk_world1_fused_step_equals_unfused(n, rng):
+    """Allgather(RandomK, ResidualMemory).step at world 1 through grace_randomk_step_w1 against the
+    reference's four calls on the same engine: outputs and residuals bit-exact over 3 steps
+    (duplicate indices included: they are drawn with replacement)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.randomk import RandomKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    gs = [np.random.default_rng(n + s).standard_normal(n).astype(np.float32) for s in range(3)]
+    runs = []
+    for fused in (True, False):
+        comm = Allgather(RandomKCompressor(0.05, rng=rng), ResidualMemory(), 1)
+        outs = []
+        for s in range(3):
+            g = torch.from_numpy(gs[s]).to("cuda")
+            if fused:
+                out = comm.step(g, "w")
+            else:
+                t = comm.memory.compensate(g, "w")
+                payload, ctx = comm.compressor.compress(t, "w")
+                comm.memory.update(t, "w", comm.compressor, payload, ctx)
+                out = comm.send_receive(payload, "w", ctx)
+            outs.append(out.cpu().numpy())
+        runs.append((outs, comm.memory.residuals["w"].cpu().numpy()))
+    (fo, fr), (uo, ur) = runs
+    for s in range(3):
+        assert same_bits(fo[s], uo[s]), s
+    assert same_bits(fr, ur)
+    assert np.count_nonzero(fo[-1]) > 0
