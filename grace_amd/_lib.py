@@ -92,6 +92,7 @@ SIGNATURES = {
     "grace_widen_i32": (ST, [P, I64, P, P]),
     "grace_threshold_count_fixed": (ST, [P, I64, F32, P, P]),
     "grace_threshold_count_dev": (ST, [P, I64, F32, P, P]),
+    "grace_threshold_step_w1": (ST, [P, P, I32, F32, F32, I64, F32, P, P, P]),
     "grace_sparse_sub": (ST, [P, P, I64, P, P]),
     "grace_exchange_record_words": (SZ, [I64]),
     "grace_threshold_write_capped": (ST, [P, I64, P, P, I64, P]),

@@ -174,6 +174,104 @@ __global__ __launch_bounds__(kSBlock) void thr_stats_kernel(const float* __restr
   }
 }
 
+// World-1 Allgather(Threshold, Residual|None).step without a payload (threshold.py:12-27,
+// residual.py:10-20, allgather.py:40-45): pass A computes t (beta r + gamma g, or g) into the buffer
+// that becomes the residual and the per-chunk stats of thr_stats_kernel in the same read; the bound
+// kernel picks min(thr, max t); pass B writes out = (|t| >= bound ? 0 + t : 0) and, with memory,
+// r' = t - decode = (selected ? t - t : t) in place.  MODE 0: no memory (t = g, read-only);
+// 1: residual memory, first step (t = g); 2: residual memory.
+typedef float f4s __attribute__((ext_vector_type(4)));
+constexpr int kThrU = 4;   // quads per lane per round (all loads first)
+template <int MODE>
+__global__ __launch_bounds__(kSBlock) void thr_comp_stats_kernel(const float* __restrict__ g, float* r, float beta,
+                                                                float gamma, int64_t n, float thr,
+                                                                ThrPart* __restrict__ part) {
+  const int64_t base = (int64_t)blockIdx.x * kThrChunk;
+  const int64_t end = min(base + (int64_t)kThrChunk, n);
+  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r)) & 15u) == 0;
+  const int64_t qe = vec ? base + ((end - base) & ~(int64_t)3) : base;   // [base, qe) in quads
+  float mx = -INFINITY;
+  uint32_t nan = 0, cnt = 0;
+  auto acc = [&](float v) {
+    if (v != v) nan = 1; else mx = fmaxf(mx, v);
+    cnt += fabsf(v) >= thr;
+  };
+  for (int64_t e0 = base + 4 * (int64_t)threadIdx.x; e0 < qe; e0 += 4 * (int64_t)kSBlock * kThrU) {
+    f4s gv[kThrU], rv[kThrU];
+#pragma unroll
+    for (int u = 0; u < kThrU; ++u) {
+      const int64_t e = e0 + 4 * (int64_t)u * kSBlock < qe ? e0 + 4 * (int64_t)u * kSBlock : e0;
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + e));
+      if (MODE == 2) rv[u] = *reinterpret_cast<const f4s*>(r + e);
+    }
+#pragma unroll
+    for (int u = 0; u < kThrU; ++u) {
+      const int64_t e = e0 + 4 * (int64_t)u * kSBlock;
+      if (e >= qe) break;
+      f4s t = gv[u];
+      if (MODE == 2) t = f4s{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
+                             beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
+      if (MODE != 0) *reinterpret_cast<f4s*>(r + e) = t;   // plain stores: pass B re-reads t
+      acc(t.x); acc(t.y); acc(t.z); acc(t.w);
+    }
+  }
+  for (int64_t i = qe + threadIdx.x; i < end; i += kSBlock) {
+    const float t = MODE == 2 ? beta * r[i] + gamma * g[i] : g[i];
+    if (MODE != 0) r[i] = t;
+    acc(t);
+  }
+  __shared__ float sm[kSBlock / kWave];
+  __shared__ uint32_t sn[kSBlock / kWave], sc[kSBlock / kWave];
+  mx = wave_max(mx);
+  cnt = wave_sum(cnt);
+  nan = __ballot(nan != 0) != 0;
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = mx; sn[w] = nan; sc[w] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ThrPart p{-INFINITY, 0u, 0u, 0u};
+    for (int j = 0; j < kSBlock / kWave; ++j) { p.mx = fmaxf(p.mx, sm[j]); p.nan |= sn[j]; p.cnt += sc[j]; }
+    part[blockIdx.x] = p;
+  }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(kSBlock) void thr_step_w1_kernel(float* t, int64_t n, const uint32_t* __restrict__ meta,
+                                                             float* __restrict__ out) {
+  const float bound = __uint_as_float(meta[0]);
+  const int64_t stride = (int64_t)gridDim.x * kSBlock;
+  const bool vec = ((reinterpret_cast<uintptr_t>(t) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
+  const int64_t nq = vec ? n >> 2 : 0;
+  for (int64_t q0 = (int64_t)blockIdx.x * kSBlock + threadIdx.x; q0 < nq; q0 += stride * kThrU) {
+    f4s tv[kThrU];
+#pragma unroll
+    for (int u = 0; u < kThrU; ++u) {
+      const int64_t q = q0 + u * stride < nq ? q0 + u * stride : q0;
+      tv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(t) + q);
+    }
+#pragma unroll
+    for (int u = 0; u < kThrU; ++u) {
+      if (q0 + u * stride >= nq) break;
+      f4s o, rr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = tv[u][j];
+        const bool sel = fabsf(v) >= bound;
+        o[j] = sel ? 0.f + v : 0.f;
+        rr[j] = sel ? v - v : v;
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<f4s*>(out) + q0 + u * stride);
+      if (RES) __builtin_nontemporal_store(rr, reinterpret_cast<f4s*>(t) + q0 + u * stride);
+    }
+  }
+  for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kSBlock + threadIdx.x; i < n; i += stride) {
+    const float v = t[i];
+    const bool sel = fabsf(v) >= bound;
+    out[i] = sel ? 0.f + v : 0.f;
+    if (RES) t[i] = sel ? v - v : v;
+  }
+}
+
 // pass 2 (one workgroup): global max -> bound = min(thr, max) with Python's min (NaN max -> thr);
 // exclusive offsets of the chunk counts; meta = {bound bits, total, recount flag}
 __global__ __launch_bounds__(1024) void thr_bound_kernel(ThrPart* __restrict__ part, int64_t nchunks, float thr,
@@ -421,6 +519,29 @@ grace_status_t grace_threshold_count(const float* x, int64_t n, float thr, void*
   GRACE_CHECK_LAUNCH("grace_threshold_count");
   thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 0, 0);
   GRACE_CHECK_LAUNCH("grace_threshold_count");
+  return GRACE_OK;
+}
+
+grace_status_t grace_threshold_step_w1(const float* g, float* residual, int32_t mode, float beta, float gamma,
+                                       int64_t n, float thr, void* ws, float* out, void* stream) {
+  GRACE_REQUIRE(g && out && ws && n >= 1 && mode >= 0 && mode <= 2 && (mode == 0 || residual),
+                "grace_threshold_step_w1: bad arguments");
+  const int64_t nch = (n + kThrChunk - 1) / kThrChunk;
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* meta = reinterpret_cast<uint32_t*>(p);
+  ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
+  uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  hipStream_t s = as_stream(stream);
+  if (mode == 0) thr_comp_stats_kernel<0><<<(unsigned)nch, kSBlock, 0, s>>>(g, nullptr, beta, gamma, n, thr, part);
+  else if (mode == 1) thr_comp_stats_kernel<1><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, part);
+  else thr_comp_stats_kernel<2><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, part);
+  GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
+  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 1, 0);
+  GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
+  const unsigned grid = stream_grid((n + 3) / 4, kSBlock * kThrU, 4096);
+  if (mode == 0) thr_step_w1_kernel<false><<<grid, kSBlock, 0, s>>>(const_cast<float*>(g), n, meta, out);
+  else thr_step_w1_kernel<true><<<grid, kSBlock, 0, s>>>(residual, n, meta, out);
+  GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
   return GRACE_OK;
 }
 

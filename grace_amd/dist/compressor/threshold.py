@@ -114,6 +114,23 @@ class ThresholdCompressor(Compressor):
         n = g.numel()
         dev = g.device
         residual = type(mem) is ResidualMemory
+        if W == 1 and self.exchange == "counts":
+            # world 1: no payload at all -- t and the bound's statistics from one read, then one pass
+            # for out = (0 + decompress) / 1 and r = t - decompress (grace_threshold_step_w1)
+            ws = ops.workspace("threshold", _lib.query("grace_threshold_workspace_bytes", n), dev)
+            out = torch.empty_like(g)
+            if residual:
+                r = mem.residuals.get(name)
+                has = r is not None and r.numel() == n and r.device == dev and r.is_contiguous()
+                buf = r.reshape(-1) if has else torch.empty_like(g)
+                _lib.call("grace_threshold_step_w1", g.data_ptr(), buf.data_ptr(), 2 if has else 1, float(mem.beta),
+                          float(mem.gamma), n, float(np.float32(self.threshold)), ws.data_ptr(), out.data_ptr(),
+                          ops._stream())
+                mem.residuals[name] = buf.view(tensor.shape)
+            else:
+                _lib.call("grace_threshold_step_w1", g.data_ptr(), None, 0, 1.0, 1.0, n,
+                          float(np.float32(self.threshold)), ws.data_ptr(), out.data_ptr(), ops._stream())
+            return out.view(tensor.shape)
         # compensate (residual.py:10-14): t = beta r + gamma g, computed straight into the buffer that
         # becomes the new residual; the first step's t is the tensor itself (copied for the residual)
         if residual:

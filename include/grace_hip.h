@@ -277,6 +277,12 @@ grace_status_t grace_threshold_write(const float* x, int64_t n, const void* ws, 
  * exchanged between ranks before the host reads anything (one host read per variable-size step) */
 grace_status_t grace_threshold_count_dev(const float* x, int64_t n, float thr, void* ws, void* stream);
 /* r[idx[j]] -= vals[j] (ResidualMemory.update, residual.py:16-20, when r already holds t) */
+/* World-1 Allgather(Threshold, ResidualMemory | NoneMemory).step without a payload
+ * (threshold.py:12-27, residual.py:10-20, allgather.py:40-45): mode 0 no memory (t = g), 1 residual
+ * memory's first step (t = g copied into residual), 2 t = beta r + gamma g (in place in residual);
+ * out = (|t| >= min(thr, max t) ? 0 + t : 0), residual <- t - decode.  ws as grace_threshold_count. */
+grace_status_t grace_threshold_step_w1(const float* g, float* residual, int32_t mode, float beta, float gamma,
+                                       int64_t n, float thr, void* ws, float* out, void* stream);
 grace_status_t grace_sparse_sub(const float* vals, const int32_t* idx, int64_t count, float* r, void* stream);
 /* Capacity-bounded variable-size exchange (allgather.py:15-38 without the size round trip): each rank
  * writes one record of grace_exchange_record_words(cap) u32 words {count, cap, 0, 0 | vals f32[cap] |
