@@ -695,6 +695,7 @@ template <bool HAS_RES, int MODE, bool FAST>
 __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
                                               uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
   constexpr int NG = kVecOf<HAS_RES, MODE> / kGroup;
+  static_assert(NG * kGroup == kVecOf<HAS_RES, MODE>, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
   const int64_t cbase = chunk * kChunkOf<HAS_RES, MODE> + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
 #ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
