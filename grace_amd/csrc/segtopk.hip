@@ -240,7 +240,10 @@ __global__ __launch_bounds__(kSegSelBlock) void seg_select_kernel(SegArgs a) {
     const int2 e = list[j];
     return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
   };
-  const uint64_t T = block_select_comp<kSegSelBlock>(src, nc, ct.need, hist, s_w, s_res);
+  // every candidate's key is in bin B (key >> 20 == B), so the top digit of the composite (its
+  // bits 53..63 = key bits 21..31) is B >> 1 for all of them: start at the second pass
+  const uint64_t T = block_select_comp<kSegSelBlock>(src, nc, ct.need, hist, s_w, s_res, 1,
+                                                     (uint64_t)((uint32_t)ct.B >> 1) << 53, (uint64_t)2047u << 53);
   if (threadIdx.x == 0) s_pos = 0;
   __syncthreads();
   const int64_t kb = a.k_off[s] + ct.above;

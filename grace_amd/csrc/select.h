@@ -104,20 +104,36 @@ __device__ __forceinline__ int2 ld_agent_i2(const int2* p) {
 }
 
 // Exact single-workgroup radix select: returns T such that exactly `need` items of src have
-// composite >= T (composites are unique).  6 passes of 11/11/11/11/11/9 bits.
+// composite >= T (composites are unique).  Passes of 11/11/11/11/11/9 bits from the top; a caller
+// that knows the top digit every item shares starts at pass 1 with that prefix.  Stops as soon as
+// the chosen bin holds exactly the items still needed (every one of them is taken: T = the prefix
+// with zero low bits) -- for untied keys that is after the key bits, so the index passes are skipped.
 template <int BLOCK = 1024, typename Src>
 __device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, uint32_t* hist,
-                                      uint32_t* s_w, uint32_t* s_res) {
-  uint64_t prefix = 0, pmask = 0;
+                                      uint32_t* s_w, uint32_t* s_res, int first_pass = 0,
+                                      uint64_t prefix0 = 0, uint64_t pmask0 = 0) {
+#ifdef GRACE_SELECT_U1   // A/B build only
+  constexpr int kU = 1;
+#else
+  constexpr int kU = 4;   // items per thread per round, all loaded before any is counted
+#endif
+  uint64_t prefix = prefix0, pmask = pmask0;
   uint32_t rem = need;
-  for (int p = 0; p < 6; ++p) {
+  for (int p = first_pass; p < 6; ++p) {
     const int shift = p < 5 ? 53 - 11 * p : 0;
     const uint32_t dmask = p < 5 ? 2047u : 511u;
     for (int b = threadIdx.x; b < 2048; b += BLOCK) hist[b] = 0;
     __syncthreads();
-    for (int64_t j = threadIdx.x; j < N; j += BLOCK) {
-      const uint64_t c = src(j);
-      if ((c & pmask) == prefix) atomicAdd(&hist[(c >> shift) & dmask], 1u);
+    for (int64_t j0 = threadIdx.x; j0 < N; j0 += (int64_t)BLOCK * kU) {
+      uint64_t c[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t j = j0 + (int64_t)u * BLOCK;
+        c[u] = src(j < N ? j : j0);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (j0 + (int64_t)u * BLOCK < N && (c[u] & pmask) == prefix) atomicAdd(&hist[(c[u] >> shift) & dmask], 1u);
     }
     __syncthreads();
     uint32_t above;
@@ -125,6 +141,13 @@ __device__ uint64_t block_select_comp(const Src& src, int64_t N, uint32_t need, 
     rem -= above;
     prefix |= (uint64_t)d << shift;
     pmask |= (uint64_t)dmask << shift;
+#ifdef GRACE_SELECT_NOEARLY   // A/B build only
+    const bool whole = false;
+#else
+    const bool whole = hist[d] == rem;   // LDS, identical for every thread
+#endif
+    __syncthreads();
+    if (whole) break;
   }
   return prefix;
 }
