@@ -324,8 +324,10 @@ def bench_topk_nomem(args, world, rank, dev):
     main_avg_ms = main_ms / max(launches, 1)
     main_bytes = (8 if world == 1 else 4) * n       # g read (+ dense out written at world 1)
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic("topk_nomem", step_bytes)
     line["roofline"] = {"bound": "hbm", "achieved": round(step_bytes / t / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(step_bytes / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(step_bytes / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio,
                         "step_algorithmic_bytes": step_bytes, "kernel": "topk_main",
                         "kernel_avg_us": round(main_avg_ms * 1e3, 2),
                         "kernel_frac": round(main_bytes / (main_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -559,9 +561,10 @@ def bench_sparse(args, world, rank, dev):
     line["config"] = {"workload": f"{desc} on a 256 MiB fp32 bucket (SURVEY.md 8a)", "numel": n}
     alg = 16.0 * n                       # g, r read; r', dense out written (payload bytes excluded)
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic(args.workload, alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes_per_step": alg}
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
     return line
 
 
@@ -587,9 +590,10 @@ def bench_dgc(args, world, rank, dev):
     # mask update 16 B (r, a), dense decode 4 B
     alg = 48.0 * n
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic("dgc", alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes_per_step": alg,
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg,
                         "note": "48n: compensate 20n, threshold histogram 4n, compaction 4n, mask update 16n, "
                                 "dense decode 4n (the reference's passes, each fused to one kernel)"}
     return line
@@ -618,9 +622,10 @@ def bench_sign_bits(args, world, rank, dev):
                       "numel": n}
     alg = 4.0 * n + n / 8 + n / 8 * world + 4.0 * n     # read x, write bits; read W bit payloads, write out
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic("sign_bits", alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes_per_step": alg}
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
     return line
 
 

@@ -3,7 +3,7 @@
 wide (16-B per lane) streaming read is tallied at half its bytes (x2); WRITE_SIZE is in KB and
 exact for 16-B-per-lane stores.  Other access widths (the codecs' 4-B code stores, 8-B loads) are
 uncalibrated, so the per-kernel figures are reported raw-corrected and flagged.
-usage: python tools/pmc_all.py OUT_JSON WORKLOAD=FETCH_DIR,WRITE_DIR [...]"""
+usage: python tools/pmc_all.py OUT_JSON [--last N] [--exclude WL:REGEX] WORKLOAD=FETCH_DIR,WRITE_DIR [...]"""
 import collections
 import csv
 import json
@@ -30,18 +30,38 @@ def per_kernel(d):
             disp[r["Dispatch_Id"]] += float(r["Counter_Value"])
             name[r["Dispatch_Id"]] = k.split("(")[0].replace("void ", "")
     out = collections.defaultdict(list)
-    for did, v in disp.items():
-        out[name[did]].append(v)
+    for did in sorted(disp, key=int):     # dispatch order, so `--last` keeps the timed steps
+        out[name[did]].append(disp[did])
     return out
 
 
 def main():
+    """Options before the workloads: --last N averages only each kernel's last N dispatches (the
+    timed steps; warm-up and first-step variants drop out), --exclude WL:REGEX leaves kernels whose
+    name matches out of WL's per-step sum (e.g. a comparison path the bench also runs)."""
+    import re
     res = {"correction": "FETCH_SIZE KB x1024 x2 (gfx950 16-B streaming reads), WRITE_SIZE KB x1024",
            "workloads": {}}
-    for arg in sys.argv[2:]:
+    args, last, excl = sys.argv[2:], 0, {}
+    while args and args[0].startswith("--"):
+        if args[0] == "--last":
+            last = int(args[1])
+        elif args[0] == "--exclude":
+            w, rx = args[1].split(":", 1)
+            excl[w] = re.compile(rx)
+        args = args[2:]
+    if last:
+        res["steady_state"] = f"mean of each kernel's last {last} dispatches"
+    for arg in args:
         wl, dirs = arg.split("=", 1)
         fdir, wdir = dirs.split(",")
         fk, wk = per_kernel(fdir), per_kernel(wdir)
+        if last:
+            fk = {k: v[-last:] for k, v in fk.items()}
+            wk = {k: v[-last:] for k, v in wk.items()}
+        if wl in excl:
+            fk = {k: v for k, v in fk.items() if not excl[wl].search(k)}
+            wk = {k: v for k, v in wk.items() if not excl[wl].search(k)}
         kern = {}
         step = 0.0
         for k in sorted(set(fk) | set(wk)):
