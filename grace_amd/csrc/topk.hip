@@ -131,6 +131,12 @@ constexpr int kXcnt = 8;                                   // sharded exchange c
 #endif
 constexpr int kSampleMax = GRACE_SAMPLE_MAX;               // stratified sample size
 constexpr int kSampleBlock = 1024;
+#ifndef GRACE_BRACKET_BLOCK
+#define GRACE_BRACKET_BLOCK 1024
+#endif
+// single-GPU bracket: one sample per thread.  A/B (step, one process): 1024 -> 232 us, 512 -> 236-240
+// (twice the workgroups, each still one per CU for the 136 KB of LDS histograms), 256 -> 256
+constexpr int kBracketBlock = GRACE_BRACKET_BLOCK;
 constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
 constexpr int kCoarseBins = 2048;                          // key >> 20: 1/8-octave bins
 constexpr int kHistStride = 1;
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
 // accumulates into (the previous step's finalize has completed, stream order), and the finalize
 // kernel zeroes both sample histograms once the main pass no longer needs them.
 template <bool HAS_RES>
-__global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs w) {
+__global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs w) {
   __shared__ uint32_t lh[kBracketBins];
   __shared__ uint32_t lc[kCoarseBins];
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];
@@ -434,7 +440,7 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   const int tid = threadIdx.x;
   STAMP(w.ctl, 0);
   const uint32_t st = (uint32_t)a.stratum;
-  const int64_t sidx = (int64_t)blockIdx.x * kSampleBlock + tid;
+  const int64_t sidx = (int64_t)blockIdx.x * kBracketBlock + tid;
   const bool valid = sidx < a.sample_n;
   float t = 0.f;
   if (valid) {
@@ -447,10 +453,10 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   }
   // counters of this step's main / finalize passes (their previous users have completed)
   if (blockIdx.x == 0 && tid >= 3 && tid < 12) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
-  if (blockIdx.x < (unsigned)(kHistBins / kSampleBlock))
-    w.hist[(blockIdx.x * kSampleBlock + tid) * kHistStride] = 0u;
-  for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
-  for (int b = tid; b < kCoarseBins; b += kSampleBlock) lc[b] = 0;
+  if (blockIdx.x < (unsigned)(kHistBins / kBracketBlock))
+    w.hist[(blockIdx.x * kBracketBlock + tid) * kHistStride] = 0u;
+  for (int b = tid; b < kBracketBins; b += kBracketBlock) lh[b] = 0;
+  for (int b = tid; b < kCoarseBins; b += kBracketBlock) lc[b] = 0;
   __syncthreads();
   STAMP(w.ctl, 1);
   if (valid) {
@@ -459,9 +465,9 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
     atomicAdd(&lc[key >> 20], 1u);
   }
   __syncthreads();
-  for (int b = tid; b < kBracketBins; b += kSampleBlock)
+  for (int b = tid; b < kBracketBins; b += kBracketBlock)
     if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
-  for (int b = tid; b < kCoarseBins; b += kSampleBlock)
+  for (int b = tid; b < kCoarseBins; b += kBracketBlock)
     if (lc[b]) atomicAdd(&w.chist[b], lc[b]);
   STAMP(w.ctl, 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -482,19 +488,32 @@ __global__ __launch_bounds__(kSampleBlock) void topk_bracket(StepArgs a, TopkWs 
   const uint32_t r1[3] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
                           (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1),
                           (uint32_t)((rank_mid < 0 ? 0 : (rank_mid >= S ? S - 1 : rank_mid)) + 1)};
-  // coarse: thread t owns bins top, top-1 (descending); one block scan finds the three coarse bins
-  static_assert(kCoarseBins == 2 * kSampleBlock, "two coarse bins per thread");
-  const int top = kCoarseBins - 1 - 2 * tid;
-  const uint32_t h0 = __hip_atomic_load(w.chist + top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t h1 = __hip_atomic_load(w.chist + top - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // coarse: thread t owns kCPT consecutive bins from top down (descending); one block scan finds
+  // the three coarse bins
+  constexpr int kCPT = kCoarseBins / kBracketBlock;
+  static_assert(kCPT * kBracketBlock == kCoarseBins && kCPT >= 1, "coarse bins tile the block");
+  const int top = kCoarseBins - 1 - kCPT * tid;
+  uint32_t hc[kCPT], hs = 0;
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    hc[c] = __hip_atomic_load(w.chist + top - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hs += hc[c];
+  }
   if (tid < 6) s_fc[tid] = 0;
-  const uint32_t ex = block_excl_scan<kSelBlock>(h0 + h1, s_w, nullptr);
+  const uint32_t ex = block_excl_scan<kBracketBlock>(hs, s_w, nullptr);
 #pragma unroll
   for (int q = 0; q < 3; ++q)
-    if (ex < r1[q] && r1[q] <= ex + h0 + h1) {
-      const bool first = r1[q] <= ex + h0;
-      s_fc[2 * q] = (uint32_t)(first ? top : top - 1);
-      s_fc[2 * q + 1] = first ? ex : ex + h0;
+    if (ex < r1[q] && r1[q] <= ex + hs) {
+      uint32_t acc = ex;
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        if (r1[q] <= acc + hc[c]) {
+          s_fc[2 * q] = (uint32_t)(top - c);
+          s_fc[2 * q + 1] = acc;
+          break;
+        }
+        acc += hc[c];
+      }
     }
   __syncthreads();
   // fine: one 16-lane group per target rank, inclusive scan of the coarse bin's 16 fine bins
@@ -1415,8 +1434,8 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
   a.stratum = a.n / a.sample_n;
   // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
-  static_assert(kSmallN >= 2 * kSampleBlock, "bracket grid covers the histogram zeroing");
-  topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kSampleBlock - 1) / kSampleBlock), kSampleBlock, 0, s>>>(a, w);
+  static_assert(kSmallN >= kHistBins, "bracket grid covers the histogram zeroing");
+  topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kBracketBlock - 1) / kBracketBlock), kBracketBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
   const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>);
   if (vec)
