@@ -25,6 +25,10 @@ SIGNATURES = {
     "grace_read_status": (ST, [P, P, P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
     "grace_timer_collect": (ST, [P, P]),
+    "grace_event_create": (ST, [P]),
+    "grace_event_destroy": (ST, [P]),
+    "grace_topk_arm_main_event": (ST, [P]),
+    "grace_stream_wait_event": (ST, [P, P]),
     "grace_axpby": (ST, [P, P, F32, F32, P, I64, P]),
     "grace_sub": (ST, [P, P, P, I64, P]),
     "grace_div_scalar": (ST, [P, F32, P, I64, P]),

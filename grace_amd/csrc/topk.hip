@@ -200,9 +200,19 @@ static int g_ev_used = 0;
 // events ride on the kernel's own dispatch packet: no separate marker packets, so no extra
 // system-scope release (an L2 writeback of every XCD, ~6 us per hipEventRecord on gfx950) is
 // inserted between the step's kernels and the timed step is the untimed one.
+// armed by grace_topk_arm_main_event: completes with the next main pass launched from this thread
+static thread_local hipEvent_t t_main_ev = nullptr;
+
 template <typename... KArgs, typename... Args>
 static void launch_timed(void (*kern)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
-  if (g_timer_on && g_ev_used < kMaxEv) {
+  if (t_main_ev) {
+    hipEvent_t ev = t_main_ev;
+    t_main_ev = nullptr;
+    const bool timed = g_timer_on && g_ev_used < kMaxEv;
+    const int slot = timed ? g_ev_used++ : 0;
+    hipExtLaunchKernelGGL(kern, grid, block, 0, s, timed ? g_ev[2 * slot] : nullptr, ev, 0, args...);
+    if (timed) hipEventRecord(g_ev[2 * slot + 1], s);
+  } else if (g_timer_on && g_ev_used < kMaxEv) {
     const int slot = g_ev_used++;
     hipExtLaunchKernelGGL(kern, grid, block, 0, s, g_ev[2 * slot], g_ev[2 * slot + 1], 0, args...);
   } else {
@@ -1725,6 +1735,43 @@ grace_status_t grace_timer_enable(int enable) {
   }
   g_timer_on = enable ? 1 : 0;
   g_ev_used = 0;
+  return GRACE_OK;
+}
+
+grace_status_t grace_event_create(void** event) {
+  GRACE_REQUIRE(event, "grace_event_create: bad arguments");
+  hipEvent_t ev = nullptr;
+  const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableSystemFence | hipEventDisableTiming);
+  if (e != hipSuccess) {
+    set_error("grace_event_create", e);
+    return GRACE_ERR_HIP;
+  }
+  *event = ev;
+  return GRACE_OK;
+}
+
+grace_status_t grace_event_destroy(void* event) {
+  GRACE_REQUIRE(event, "grace_event_destroy: bad arguments");
+  const hipError_t e = hipEventDestroy(static_cast<hipEvent_t>(event));
+  if (e != hipSuccess) {
+    set_error("grace_event_destroy", e);
+    return GRACE_ERR_HIP;
+  }
+  return GRACE_OK;
+}
+
+grace_status_t grace_topk_arm_main_event(void* event) {
+  t_main_ev = static_cast<hipEvent_t>(event);
+  return GRACE_OK;
+}
+
+grace_status_t grace_stream_wait_event(void* stream, void* event) {
+  GRACE_REQUIRE(event, "grace_stream_wait_event: bad arguments");
+  const hipError_t e = hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0);
+  if (e != hipSuccess) {
+    set_error("grace_stream_wait_event", e);
+    return GRACE_ERR_HIP;
+  }
   return GRACE_OK;
 }
 

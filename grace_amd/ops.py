@@ -252,6 +252,33 @@ def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payl
     return buf, vals, idx
 
 
+class MainEvent:
+    """A native event that completes with the main pass of the next top-k step it is armed for
+    (grace_topk_arm_main_event): the next bucket's step on another stream waits on it, so its
+    bracket runs beside this bucket's finalize (tools/exp_two_streams.py)."""
+
+    def __init__(self):
+        import ctypes
+        h = ctypes.c_void_p()
+        _lib.call("grace_event_create", ctypes.addressof(h))
+        self.handle = h.value
+
+    def arm(self):
+        _lib.call("grace_topk_arm_main_event", self.handle)
+
+    def wait(self, stream=None):
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        _lib.call("grace_stream_wait_event", s, self.handle)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                _lib.call("grace_event_destroy", h)
+            except Exception:
+                pass
+
+
 def topk_status(n, k, device):
     """Whether the last top-k launch on this stream took the exact fallback (syncs; tests only)."""
     import ctypes

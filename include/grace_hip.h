@@ -50,6 +50,16 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
 grace_status_t grace_timer_enable(int enable);
 grace_status_t grace_timer_collect(float* total_ms, int32_t* launches);
 
+/* Cross-bucket overlap: an event that completes with the MAIN pass of a top-k step, so
+ * that the next bucket's step on another stream can start its bracket while this bucket's
+ * finalize runs.  grace_topk_arm_main_event arms `event` for the next top-k step launched from
+ * the calling thread (one-shot; the event rides on the main pass's dispatch packet, no marker).
+ * Events come from grace_event_create (no system fence, no timing). */
+grace_status_t grace_event_create(void** event);
+grace_status_t grace_event_destroy(void* event);
+grace_status_t grace_topk_arm_main_event(void* event);
+grace_status_t grace_stream_wait_event(void* stream, void* event);
+
 /* ------------------------------------------------------------------------ elementwise memory */
 /* t = beta * r + gamma * g  (ResidualMemory.compensate, grace_dl/dist/memory/residual.py:10-14;
  * EFSignSGDMemory.compensate with beta = 1, gamma = lr, memory/efsignsgd.py:11-13) */
