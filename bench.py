@@ -233,7 +233,8 @@ def bench_topk(args, world, rank, dev):
     # the fraction against a copy bandwidth measured on this box as well
     copy_gbs = measured_copy_gbs(dev)
     roofline["measured_copy_gbs"] = copy_gbs
-    roofline["measured_copy_kind"] = "torch copy_, 1 GiB -> 1 GiB, read + write bytes"
+    roofline["measured_copy_kind"] = ("grace_hbm_probe: 2-read / 2-write non-temporal 16-B stream (the step's "
+                                      "dense traffic mix, no arithmetic), 3 x 1 GiB buffers, HIP events")
     roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
     line["roofline"] = roofline
     if world == 1 and not args.no_overlap:
@@ -278,21 +279,57 @@ def bench_topk_two_streams(args, grads, names):
 
 
 def measured_copy_gbs(dev, nbytes=1 << 30, reps=10):
-    """Device-to-device copy bandwidth (read + write bytes / time) of torch's copy kernel on 1 GiB
-    buffers (4x the Infinity Cache), median of `reps` event-timed copies."""
-    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
-    dst = torch.empty_like(src)
-    dst.copy_(src)
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        dst.copy_(src)
-        b.record()
-        b.synchronize()
-        ts.append(a.elapsed_time(b) * 1e-3)
-    del src, dst
-    return round(2 * nbytes / sorted(ts)[len(ts) // 2] / 1e9, 1)
+    """The box's HBM ceiling for the headline step's traffic mix (the fraction
+    against a measured bandwidth too): ``grace_hbm_probe``, read r, g and write r' = r + g, o = 0
+    with non-temporal 16-B loads / stores and no arithmetic, on three 1 GiB buffers (12x the
+    Infinity Cache), HIP events on the probe's own stream; the faster of the chunked and
+    grid-stride variants, median of `reps` launches each.  (bytes = 16 per element.)"""
+    from grace_amd import _lib, ops
+    n = nbytes // 4
+    r = torch.zeros(n, dtype=torch.float32, device=dev)
+    g = torch.zeros_like(r)
+    o = torch.empty_like(r)
+    best = 0.0
+    for variant in (0, 1):
+        ts = []
+        for i in range(reps + 2):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            _lib.call("grace_hbm_probe", r.data_ptr(), g.data_ptr(), o.data_ptr(), n, variant, ops._stream())
+            b.record()
+            b.synchronize()
+            if i >= 2:
+                ts.append(a.elapsed_time(b) * 1e-3)
+        best = max(best, 16.0 * n / sorted(ts)[len(ts) // 2] / 1e9)
+    del r, g, o
+    return round(best, 1)
+
+
+def host_cores():
+    """(threads to use, how they were chosen): the physical cores of the CPUs this process may run
+    on (its affinity mask, SMT siblings counted once), capped by OMP_NUM_THREADS when the box sets
+    it (the GPU box grants 16 CPUs of a larger host and exports that share there)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", c))
+    phys = max(1, len(cores))
+    why = f"{phys} physical cores in this process's affinity mask ({len(cpus)} logical CPUs)"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < phys:
+        why += f", capped at OMP_NUM_THREADS={omp} (the box's CPU share)"
+        phys = int(omp)
+    return phys, why
 
 
 def cpu_model():
@@ -310,7 +347,9 @@ def cpu_baseline_topk(n, ratio, steps):
     """The oracle's top-k + residual step on the host cores over the same bucket size."""
     import numpy as np
     from oracle import grace_oracle as O
-    threads = torch.get_num_threads()
+    threads, why = host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
     g = rng.standard_normal(n, dtype=np.float32)
     r = (0.1 * rng.standard_normal(n, dtype=np.float32)).astype(np.float32)
@@ -319,8 +358,9 @@ def cpu_baseline_topk(n, ratio, steps):
     for _ in range(steps):
         _, _, _, r, _ = O.topk_residual_step(g, r, ratio)
     dt = (time.perf_counter() - t0) / steps
+    torch.set_num_threads(prev)
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cores_chosen": why, "cpu_model": cpu_model(),
             "sample": f"{steps} full 256 MiB top-k 1% + residual steps of oracle/grace_oracle.py "
                       f"(numpy partition + torch CPU ops, {threads} torch threads), {dt * 1e3:.0f} ms/step",
             "note": "conservative: the oracle's numpy partition is faster than the reference's torch.topk "

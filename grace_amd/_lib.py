@@ -33,6 +33,7 @@ SIGNATURES = {
     "grace_sub": (ST, [P, P, P, I64, P]),
     "grace_div_scalar": (ST, [P, F32, P, I64, P]),
     "grace_fill": (ST, [P, F32, I64, P]),
+    "grace_hbm_probe": (ST, [P, P, P, I64, I32, P]),
     "grace_accumulate": (ST, [P, P, I64, I32, P]),
     "grace_sign_encode": (ST, [P, P, I64, P]),
     "grace_sign_decode": (ST, [P, P, P, I64, P]),

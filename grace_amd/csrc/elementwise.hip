@@ -326,6 +326,52 @@ static grace_status_t run_reduce(const char* name, const float* x, int64_t n, Ac
   return GRACE_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// HBM ceiling probe (bench.py's measured roofline): the headline step's dense traffic
+// mix without any of its arithmetic -- read r, g; write r' = r + g and o = 0 -- with non-temporal
+// 16-B loads and stores.  Variant 0: one 16384-element chunk per 256-thread workgroup, 4 float4 per
+// array in flight per lane, the next group's loads issued before the current group is stored (the
+// top-k main pass's layout).  Variant 1: a grid-stride loop over 2048 workgroups.
+constexpr int kProbeChunk = 16384;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void probe_2r2w_chunk(f32x4v* __restrict__ r, const f32x4v* __restrict__ g,
+                                                       f32x4v* __restrict__ o) {
+  constexpr int G = 4, NG = kProbeChunk / 4 / 256 / G;
+  const int64_t base = (int64_t)blockIdx.x * (kProbeChunk / 4) + threadIdx.x;
+  f32x4v a[G], b[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    a[u] = __builtin_nontemporal_load(r + base + u * 256);
+    b[u] = __builtin_nontemporal_load(g + base + u * 256);
+  }
+#pragma unroll 1
+  for (int q = 0; q < NG; ++q) {
+    f32x4v an[G], bn[G];
+    if (q + 1 < NG) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        an[u] = __builtin_nontemporal_load(r + base + ((q + 1) * G + u) * 256);
+        bn[u] = __builtin_nontemporal_load(g + base + ((q + 1) * G + u) * 256);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      __builtin_nontemporal_store(a[u] + b[u], r + base + (q * G + u) * 256);
+      __builtin_nontemporal_store(f32x4v{0.f, 0.f, 0.f, 0.f}, o + base + (q * G + u) * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) { a[u] = an[u]; b[u] = bn[u]; }
+  }
+}
+__global__ __launch_bounds__(256) void probe_2r2w_stride(f32x4v* __restrict__ r, const f32x4v* __restrict__ g,
+                                                        f32x4v* __restrict__ o, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4v a = __builtin_nontemporal_load(r + i), b = __builtin_nontemporal_load(g + i);
+    __builtin_nontemporal_store(a + b, r + i);
+    __builtin_nontemporal_store(f32x4v{0.f, 0.f, 0.f, 0.f}, o + i);
+  }
+}
+
 }  // namespace grace
 
 using namespace grace;
@@ -353,6 +399,19 @@ grace_status_t grace_div_scalar(const float* x, float divisor, float* out, int64
   GRACE_REQUIRE(n >= 0 && x && out, "grace_div_scalar: bad arguments");
   return launch_stream("grace_div_scalar", DivOp{x, divisor, out}, n, aligned16(x) && aligned16(out),
                        stream);
+}
+
+grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream) {
+  GRACE_REQUIRE(r && g && o && n > 0 && (variant == 0 || variant == 1) && aligned16(r) && aligned16(g) &&
+                    aligned16(o) && n % kProbeChunk == 0,
+                "grace_hbm_probe: bad arguments (n a multiple of 16384, 16-B aligned buffers)");
+  f32x4v* r4 = reinterpret_cast<f32x4v*>(r);
+  const f32x4v* g4 = reinterpret_cast<const f32x4v*>(g);
+  f32x4v* o4 = reinterpret_cast<f32x4v*>(o);
+  if (variant == 0) probe_2r2w_chunk<<<(unsigned)(n / kProbeChunk), 256, 0, as_stream(stream)>>>(r4, g4, o4);
+  else probe_2r2w_stride<<<2048, 256, 0, as_stream(stream)>>>(r4, g4, o4, n / 4);
+  GRACE_CHECK_LAUNCH("grace_hbm_probe");
+  return GRACE_OK;
 }
 
 grace_status_t grace_fill(float* x, float value, int64_t n, void* stream) {

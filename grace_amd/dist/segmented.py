@@ -30,7 +30,9 @@ class SegmentedTopK:
         self.last_payload = None
 
     def tables(self, sizes, device):
-        key = (tuple(int(s) for s in sizes), str(device))
+        # per stream as well: the workspace's histograms and counters are re-zeroed by the next
+        # launch on the same stream, so two streams must never share one
+        key = (tuple(int(s) for s in sizes), str(device), ops._stream())
         hit = self._tables.get(key)
         if hit is None:
             chunk = _lib.query("grace_topk_segmented_chunk")

@@ -103,6 +103,7 @@ class ShardedTopK:
         self._sizes = {}
         self.last_payload = None      # (vals, idx) of this rank's entries of the last step
         self.last_fallback = False
+        self.resizes = 0              # steps that found a rank's shard resized (and were redone)
 
     def _world(self):
         if dist.is_available() and dist.is_initialized():
@@ -127,9 +128,12 @@ class ShardedTopK:
         return sizes
 
     def step(self, shard, name):
+        return self._step(shard.reshape(-1), name, compensated=False)
+
+    def _step(self, g, name, compensated):
+        """compensated=True: g already is t = beta r + gamma g (the redo after a resize)."""
         K = self.k_ops
         world, rank = self._world()
-        g = shard.reshape(-1)
         dev = g.device
         m = g.numel()
         sizes = self._shard_sizes(name, m, dev, world)
@@ -137,8 +141,8 @@ class ShardedTopK:
         n = sum(sizes)
         k = ops.ratio_k(n, self.compress_ratio)
         res = self.residuals.get(name)
-        has_res = res is not None and res.numel() == m
-        if not has_res:
+        has_res = res is not None and res.numel() == m and not compensated
+        if res is None or res.numel() != m:
             res = K.empty(m, torch.float32, dev)
         self.residuals[name] = res
         stratum = max(1, n // ops.SAMPLE_MAX)
@@ -166,11 +170,14 @@ class ShardedTopK:
         seen = [int(v) for v in rows[:, HIST_BINS + 2]]
         if seen != list(sizes):
             # some rank's shard changed size: this pass ran on stale offsets.  Every rank sees the
-            # same gathered lengths, so all of them redo the step with the new sizes; the residuals
-            # belong to the old partition and are dropped (the main pass left t in them).
+            # same gathered lengths, so all of them redo the step with the new sizes.  The main
+            # pass left t = beta r + gamma g in the residual buffer, so the redo starts from a copy
+            # of t as an already-compensated gradient: a rank whose shard kept its size keeps its
+            # error feedback exactly (residual.py:10-14 applied once), a resized rank starts from
+            # t = g as on a first step.  Counted in ``resizes``.
             self._sizes[name] = seen
-            self.residuals.pop(name, None)
-            return self.step(shard, name)
+            self.resizes += 1
+            return self._step(res.clone(), name, compensated=True)
         ok, B, need, cap_b, cap_p = plan_boundary(rows, k, world, K.cand_cap(m, k))
         self.last_fallback = not ok
         if not ok:

@@ -69,6 +69,7 @@ def workspace(slot, nbytes, device):
 
 _reuse = {}
 _getrefcount = __import__("sys").getrefcount
+_storage_uses = torch._C._storage_Use_Count
 
 
 _sign_w1 = None
@@ -87,17 +88,23 @@ def launch_sign_step_w1(x, out):
 
 def reusable_output(slot, shape, dtype, device):
     """An output tensor for a per-step codec result, reused across calls when nobody outside this
-    cache still holds the previous one (CPython refcount: dict + local + argument = 3) and the call
-    runs on the stream it was made on, so reuse is stream-ordered behind every earlier use.  A
-    caller that keeps its results gets a fresh tensor each call, exactly as the reference's new
-    allocations; one that consumes and drops them (``grad.copy_(grc.step(grad, name))``,
-    examples/dist/CIFAR10-dawndist/core.py:204-206) skips the allocator on launch-bound steps."""
+    cache still holds the previous one and the call runs on the stream it was made on, so reuse is
+    stream-ordered behind every earlier use.  "Nobody holds it" needs two checks: the Python object
+    (CPython refcount: tuple + local + argument = 3) and its storage, because a view or reshape
+    (``out.view(-1)``, ``out[1:]``) is another tensor on the same storage that the object's refcount
+    cannot see -- the StorageImpl use count is 2 exactly when only the cached tensor and the cached
+    storage handle refer to it.  A caller that keeps its results, or any view of them, gets a fresh
+    tensor each call, exactly as the reference's new allocations; one that consumes and drops them
+    (``grad.copy_(grc.step(grad, name))``, examples/dist/CIFAR10-dawndist/core.py:204-206) skips
+    the allocator on launch-bound steps."""
     key = (slot, shape, dtype, device, _stream())
-    buf = _reuse.get(key)
-    if buf is not None and _getrefcount(buf) == 3:
-        return buf
+    hit = _reuse.get(key)
+    if hit is not None:
+        buf = hit[0]
+        if _getrefcount(buf) == 3 and _storage_uses(hit[1]) == 2:
+            return buf
     buf = torch.empty(shape, dtype=dtype, device=device)
-    _reuse[key] = buf
+    _reuse[key] = (buf, buf.untyped_storage()._cdata, buf.untyped_storage())
     return buf
 
 

@@ -70,6 +70,10 @@ grace_status_t grace_sub(const float* t, const float* d, float* r, int64_t n, vo
 /* out = x / divisor  (Communicator average: allgather.py:45, allreduce.py:12) */
 grace_status_t grace_div_scalar(const float* x, float divisor, float* out, int64_t n, void* stream);
 grace_status_t grace_fill(float* x, float value, int64_t n, void* stream);
+/* HBM ceiling probe for bench.py (no reference counterpart): r = r + g, o = 0 with non-temporal 16-B
+   loads / stores (the top-k step's 2-read / 2-write dense traffic, none of its arithmetic).
+   variant 0: 16384-element chunks per workgroup; 1: grid-stride.  n % 16384 == 0. */
+grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream);
 /* Compressor.aggregate = Python sum() in rank order (grace_dl/dist/__init__.py:32-34):
  * first != 0: acc = 0.0f + x (so -0 -> +0), else acc = acc + x. */
 grace_status_t grace_accumulate(float* acc, const float* x, int64_t n, int32_t first, void* stream);

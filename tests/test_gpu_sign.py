@@ -127,3 +127,31 @@ def test_w1_step_output_reuse_never_clobbers_a_held_result():
     assert p1 == p2
     out = comm.step(_t(xs[2]).view(ROWS_COLS), "w")             # 2-D input keeps its shape
     assert out.shape == ROWS_COLS
+
+
+def test_w1_step_output_reuse_respects_views():
+    """A caller that keeps only a view / reshape / slice of the result (``grads.append(step(g).view(-1))``)
+    or gets a view back (non-contiguous input) must never see that result overwritten by a later
+    step: the reuse guard checks the storage's use count, not just the object's."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.signsgd import SignSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    comm = Allgather(SignSGDCompressor(), NoneMemory(), 1)
+    rng = np.random.default_rng(10)
+    xs = [rng.standard_normal(4099).astype(np.float32) for _ in range(6)]
+    exp = [np.where(x >= 0, 1.0, -1.0).astype(np.float32) for x in xs]
+    held = [comm.step(_t(x), "w").view(-1) for x in xs[:2]]        # views only
+    held.append(comm.step(_t(xs[2]), "w")[1:])                     # a slice only
+    held.append(comm.step(_t(xs[3]), "w").reshape(1, -1))          # a reshape (view) only
+    for h, e, cut in zip(held, exp, (0, 0, 1, 0)):
+        assert np.array_equal(_np(h).ravel(), e[cut:])
+    # non-contiguous input: the result the caller gets is a view of the cached output
+    m = rng.standard_normal((64, 96)).astype(np.float32)
+    nc = _t(m).t()
+    assert not nc.is_contiguous()
+    a = comm.step(nc, "w")
+    b = comm.step(_t(-m).t(), "w")
+    assert np.array_equal(_np(a), np.where(m.T >= 0, 1.0, -1.0).astype(np.float32))
+    assert np.array_equal(_np(b), np.where(-m.T >= 0, 1.0, -1.0).astype(np.float32))
+    for h, e, cut in zip(held, exp, (0, 0, 1, 0)):                # still intact after more steps
+        assert np.array_equal(_np(h).ravel(), e[cut:])

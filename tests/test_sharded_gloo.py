@@ -183,6 +183,7 @@ def _worker(rank, world, path, outdir, sizes, case, ratio, dense, sizes2=None):
         res[f"idx{s}"] = i.numpy()[keep].copy()
         res[f"res{s}"] = eng.residuals["bucket"].numpy().copy()
         res[f"fb{s}"] = np.array([eng.last_fallback])
+        res[f"rs{s}"] = np.array([eng.resizes])
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
@@ -233,9 +234,10 @@ def test_sharded_topk_matches_single_bucket(world, sizes, case, ratio):
 
 
 def test_sharded_resize_one_rank_between_steps():
-    """ADVICE r1: only rank 1's shard changes size at step 2.  Every rank must see it in the same
-    step (no rank-local collective, no hang), re-plan with the new partition and drop the residual
-    that belongs to the old one."""
+    """ADVICE r1/r2: only rank 1's shard changes size at step 2.  Every rank must see it in the same
+    step (no rank-local collective, no hang) and re-plan with the new partition.  Rank 0's shard
+    kept its size, so it keeps its error feedback (t = r + g, residual.py:10-14); rank 1 starts
+    from t = g.  The event is counted in ``resizes`` on every rank."""
     sizes, sizes2 = [40000, 40000], [40000, 25000]
     outs = _run(2, sizes, "normal", 0.01, sizes2=sizes2)
     g0 = _bucket("normal", sum(sizes), 100)
@@ -243,7 +245,8 @@ def test_sharded_resize_one_rank_between_steps():
     idx = np.sort(np.concatenate([o["idx0"] for o in outs]).astype(np.int64))
     assert np.array_equal(idx, i0.astype(np.int64))
     g1 = _bucket("normal", sum(sizes2), 101)
-    _, v1, i1, r1, out1 = O.topk_residual_step(g1, None, 0.01)      # residual dropped
+    carried = np.concatenate([r0[:40000], np.zeros(25000, np.float32)])   # rank 0's residual kept
+    _, v1, i1, r1, out1 = O.topk_residual_step(g1, carried, 0.01)
     idx = np.concatenate([o["idx1"] for o in outs]).astype(np.int64)
     vals = np.concatenate([o["vals1"] for o in outs])
     order = np.argsort(idx)
@@ -252,6 +255,7 @@ def test_sharded_resize_one_rank_between_steps():
     assert _bits(np.concatenate([o["res1"] for o in outs]), r1)
     for o in outs:
         assert _bits(o["out1"], out1)
+        assert int(o["rs0"][0]) == 0 and int(o["rs1"][0]) == 1
 
 
 def test_sharded_dense_shard_mode():
