@@ -231,10 +231,11 @@ def bench_topk(args, world, rank, dev):
         except (OSError, ValueError, KeyError):
             pass
     # the fraction against a copy bandwidth measured on this box as well
-    copy_gbs = measured_copy_gbs(dev)
+    copy_gbs, variant = measured_copy_gbs(dev)
     roofline["measured_copy_gbs"] = copy_gbs
     roofline["measured_copy_kind"] = ("grace_hbm_probe: 2-read / 2-write non-temporal 16-B stream (the step's "
-                                      "dense traffic mix, no arithmetic), 3 x 1 GiB buffers, HIP events")
+                                      "dense traffic mix, no arithmetic) over 256 MiB arrays, 3 rotated sets, "
+                                      f"fastest of 6 layouts (variant {variant}), HIP events")
     roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
     line["roofline"] = roofline
     if world == 1 and not args.no_overlap:
@@ -278,31 +279,34 @@ def bench_topk_two_streams(args, grads, names):
             "note": "bucket j on stream j % 2; not the headline value (that is one stream, in order)"}
 
 
-def measured_copy_gbs(dev, nbytes=1 << 30, reps=10):
+def measured_copy_gbs(dev, n=1 << 26, sets=3, reps=7):
     """The box's HBM ceiling for the headline step's traffic mix (the fraction
     against a measured bandwidth too): ``grace_hbm_probe``, read r, g and write r' = r + g, o = 0
-    with non-temporal 16-B loads / stores and no arithmetic, on three 1 GiB buffers (12x the
-    Infinity Cache), HIP events on the probe's own stream; the faster of the chunked and
-    grid-stride variants, median of `reps` launches each.  (bytes = 16 per element.)"""
+    with non-temporal 16-B loads / stores and no arithmetic, over 256 MiB arrays (the bucket size)
+    in `sets` rotated buffer sets (768 MiB each, so no launch finds its bytes in the 256 MB
+    Infinity Cache), HIP events on the probe's own stream.  Six streaming layouts (chunked like the
+    main pass, grid-stride); the fastest one's median over `reps` launches is the ceiling.
+    Returns (GB/s, variant)."""
     from grace_amd import _lib, ops
-    n = nbytes // 4
-    r = torch.zeros(n, dtype=torch.float32, device=dev)
-    g = torch.zeros_like(r)
-    o = torch.empty_like(r)
-    best = 0.0
-    for variant in (0, 1):
+    bufs = [tuple(torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(3)) for _ in range(sets)]
+    best, best_v = 0.0, None
+    for variant in range(6):
+        elems = int(_lib.query("grace_hbm_probe_elems", n, variant))
         ts = []
-        for i in range(reps + 2):
+        for i in range(reps + sets):
+            r, g, o = bufs[i % sets]
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             _lib.call("grace_hbm_probe", r.data_ptr(), g.data_ptr(), o.data_ptr(), n, variant, ops._stream())
             b.record()
             b.synchronize()
-            if i >= 2:
+            if i >= sets:
                 ts.append(a.elapsed_time(b) * 1e-3)
-        best = max(best, 16.0 * n / sorted(ts)[len(ts) // 2] / 1e9)
-    del r, g, o
-    return round(best, 1)
+        gbs = 16.0 * elems / sorted(ts)[len(ts) // 2] / 1e9
+        if gbs > best:
+            best, best_v = gbs, variant
+    del bufs
+    return round(best, 1), best_v
 
 
 def host_cores():

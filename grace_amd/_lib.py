@@ -33,6 +33,7 @@ SIGNATURES = {
     "grace_sub": (ST, [P, P, P, I64, P]),
     "grace_div_scalar": (ST, [P, F32, P, I64, P]),
     "grace_fill": (ST, [P, F32, I64, P]),
+    "grace_hbm_probe_elems": (I64, [I64, I32]),
     "grace_hbm_probe": (ST, [P, P, P, I64, I32, P]),
     "grace_accumulate": (ST, [P, P, I64, I32, P]),
     "grace_sign_encode": (ST, [P, P, I64, P]),
@@ -64,6 +65,8 @@ SIGNATURES = {
     "grace_dgc_sample": (ST, [P, I64, P, U64, I64, P, P]),
     "grace_dgc_threshold": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),
     "grace_dgc_write": (ST, [P, I64, P, P, P, P]),
+    "grace_dgc_write_capped": (ST, [P, I64, P, P, I64, P]),
+    "grace_dgc_mask_update_capped": (ST, [P, I64, P, P, P]),
     "grace_dgc_compensate": (ST, [P, P, P, I32, F32, I64, P]),
     "grace_dgc_mask_update": (ST, [P, P, P, I64, P, P]),
     "grace_dgc_select": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),

@@ -350,11 +350,22 @@ __global__ __launch_bounds__(1024) void dgc_offsets_kernel(int64_t nch, DgcWs w)
   if (threadIdx.x == 0) w.meta->total = run;
 }
 
-// ordered compaction of |t| >= thr: values f32, indices int64 (torch.where order)
+// ordered compaction of |t| >= thr: values f32, indices int64 (torch.where order).  With a header
+// pointer it writes the capacity-bounded exchange record of sparse.hip instead -- {count, cap, 0,
+// 0 | vals f32[cap] | idx i32[cap]}, entries past cap (ascending index order) dropped.
+constexpr int kDgcRecHdr = 4;          // = sparse.hip kRecHdr (grace_exchange_record_words)
+template <typename IdxT>
 __global__ __launch_bounds__(kDBlock) void dgc_write_kernel(const float* __restrict__ t, int64_t n, DgcWs w,
-                                                           float* __restrict__ vals, int64_t* __restrict__ idx) {
+                                                           float* __restrict__ vals, IdxT* __restrict__ idx,
+                                                           int64_t cap, uint32_t* __restrict__ hdr) {
   __shared__ uint32_t s_w[kDBlock / kWave + 1];
   const float thr = __uint_as_float(w.meta->thr);
+  if (hdr && blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr[0] = w.meta->total;
+    hdr[1] = (uint32_t)cap;
+    hdr[2] = 0u;
+    hdr[3] = 0u;
+  }
   const int64_t base = (int64_t)blockIdx.x * kDChunk;
   const int64_t end = min(base + (int64_t)kDChunk, n);
   uint32_t run = w.offs[blockIdx.x];
@@ -365,8 +376,23 @@ __global__ __launch_bounds__(kDBlock) void dgc_write_kernel(const float* __restr
     if (i < end) { v = t[i]; sel = fabsf(v) >= thr; }
     uint32_t tot;
     const uint32_t ex = dgc_excl_scan<kDBlock>(sel ? 1u : 0u, s_w, &tot);
-    if (sel) { vals[run + ex] = v; idx[run + ex] = i; }
+    if (sel && (int64_t)(run + ex) < cap) { vals[run + ex] = v; idx[run + ex] = (IdxT)i; }
     run += tot;
+  }
+}
+
+// DgcMemory.update (memory/dgc.py:21-28) over the entries that travelled in this rank's record:
+// r = r * 0, a = a * 0 at those indices (the mask multiply, so a negative entry becomes -0 exactly
+// as r * ~mask does).  Without overflow the record holds every selected index, so this equals
+// grace_dgc_mask_update; on overflow the unsent entries keep r and a (error feedback).
+__global__ __launch_bounds__(kDBlock) void dgc_rec_mask_kernel(const uint32_t* __restrict__ rec, int64_t cap,
+                                                              float* __restrict__ r, float* __restrict__ a) {
+  const int64_t c = min((int64_t)rec[0], cap);
+  const int32_t* idx = reinterpret_cast<const int32_t*>(rec + kDgcRecHdr + cap);
+  for (int64_t j = (int64_t)blockIdx.x * kDBlock + threadIdx.x; j < c; j += (int64_t)gridDim.x * kDBlock) {
+    const int32_t i = idx[j];
+    r[i] = r[i] * 0.f;
+    a[i] = a[i] * 0.f;
   }
 }
 
@@ -543,8 +569,29 @@ grace_status_t grace_dgc_write(const float* t, int64_t n, const void* ws, float*
   GRACE_REQUIRE(t && ws && n >= 1, "grace_dgc_write: bad arguments");
   DgcWs w = dgc_carve(const_cast<void*>(ws), n);
   const int64_t nch = (n + kDChunk - 1) / kDChunk;
-  dgc_write_kernel<<<(unsigned)nch, kDBlock, 0, as_stream(stream)>>>(t, n, w, vals, idx);
+  dgc_write_kernel<int64_t><<<(unsigned)nch, kDBlock, 0, as_stream(stream)>>>(t, n, w, vals, idx, n, nullptr);
   GRACE_CHECK_LAUNCH("grace_dgc_write");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_write_capped(const float* t, int64_t n, const void* ws, uint32_t* rec, int64_t cap,
+                                      void* stream) {
+  GRACE_REQUIRE(t && ws && rec && n >= 1 && cap >= 1 && cap <= n && n < ((int64_t)1 << 31),
+                "grace_dgc_write_capped: bad arguments (1 <= cap <= n < 2^31)");
+  DgcWs w = dgc_carve(const_cast<void*>(ws), n);
+  const int64_t nch = (n + kDChunk - 1) / kDChunk;
+  float* vals = reinterpret_cast<float*>(rec + kDgcRecHdr);
+  int32_t* idx = reinterpret_cast<int32_t*>(rec + kDgcRecHdr + cap);
+  dgc_write_kernel<int32_t><<<(unsigned)nch, kDBlock, 0, as_stream(stream)>>>(t, n, w, vals, idx, cap, rec);
+  GRACE_CHECK_LAUNCH("grace_dgc_write_capped");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_mask_update_capped(const uint32_t* rec, int64_t cap, float* residual, float* accum,
+                                            void* stream) {
+  GRACE_REQUIRE(rec && residual && accum && cap >= 1, "grace_dgc_mask_update_capped: bad arguments");
+  dgc_rec_mask_kernel<<<stream_grid(cap, kDBlock, 2048), kDBlock, 0, as_stream(stream)>>>(rec, cap, residual, accum);
+  GRACE_CHECK_LAUNCH("grace_dgc_mask_update_capped");
   return GRACE_OK;
 }
 

@@ -329,22 +329,25 @@ static grace_status_t run_reduce(const char* name, const float* x, int64_t n, Ac
 // ------------------------------------------------------------------------------------------------
 // HBM ceiling probe (bench.py's measured roofline): the headline step's dense traffic
 // mix without any of its arithmetic -- read r, g; write r' = r + g and o = 0 -- with non-temporal
-// 16-B loads and stores.  Variant 0: one 16384-element chunk per 256-thread workgroup, 4 float4 per
-// array in flight per lane, the next group's loads issued before the current group is stored (the
-// top-k main pass's layout).  Variant 1: a grid-stride loop over 2048 workgroups.
-constexpr int kProbeChunk = 16384;
+// 16-B loads and stores.  A family of pure streaming layouts; bench.py reports the fastest as the
+// box's ceiling.  Variants 0-2: one chunk of 256 x 4 x VEC elements per 256-thread workgroup
+// (VEC = 8 / 12 / 16 float4 per lane per array; 12 is the top-k main pass's residual layout), the
+// lane's float4s loaded in groups of 4 with the next group in flight while the current one is
+// stored; at most 4 workgroups per CU as the main pass.  Variants 3-5: a grid-stride loop over
+// 1024 / 2048 / 4096 workgroups.  Chunk variants cover floor(n / chunk) chunks.
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void probe_2r2w_chunk(f32x4v* __restrict__ r, const f32x4v* __restrict__ g,
-                                                       f32x4v* __restrict__ o) {
-  constexpr int G = 4, NG = kProbeChunk / 4 / 256 / G;
-  const int64_t base = (int64_t)blockIdx.x * (kProbeChunk / 4) + threadIdx.x;
+template <int VEC>
+__global__ __launch_bounds__(256, 4) void probe_2r2w_chunk(f32x4v* __restrict__ r, const f32x4v* __restrict__ g,
+                                                          f32x4v* __restrict__ o) {
+  constexpr int G = 4, NG = VEC / G;
+  const int64_t base = (int64_t)blockIdx.x * (256 * VEC) + threadIdx.x;
   f32x4v a[G], b[G];
 #pragma unroll
   for (int u = 0; u < G; ++u) {
     a[u] = __builtin_nontemporal_load(r + base + u * 256);
     b[u] = __builtin_nontemporal_load(g + base + u * 256);
   }
-#pragma unroll 1
+#pragma unroll
   for (int q = 0; q < NG; ++q) {
     f32x4v an[G], bn[G];
     if (q + 1 < NG) {
@@ -359,8 +362,10 @@ __global__ __launch_bounds__(256) void probe_2r2w_chunk(f32x4v* __restrict__ r, 
       __builtin_nontemporal_store(a[u] + b[u], r + base + (q * G + u) * 256);
       __builtin_nontemporal_store(f32x4v{0.f, 0.f, 0.f, 0.f}, o + base + (q * G + u) * 256);
     }
+    if (q + 1 < NG) {
 #pragma unroll
-    for (int u = 0; u < G; ++u) { a[u] = an[u]; b[u] = bn[u]; }
+      for (int u = 0; u < G; ++u) { a[u] = an[u]; b[u] = bn[u]; }
+    }
   }
 }
 __global__ __launch_bounds__(256) void probe_2r2w_stride(f32x4v* __restrict__ r, const f32x4v* __restrict__ g,
@@ -371,6 +376,8 @@ __global__ __launch_bounds__(256) void probe_2r2w_stride(f32x4v* __restrict__ r,
     __builtin_nontemporal_store(f32x4v{0.f, 0.f, 0.f, 0.f}, o + i);
   }
 }
+constexpr int kProbeVariants = 6;
+static int64_t probe_chunk(int variant) { return variant == 0 ? 8192 : variant == 1 ? 12288 : variant == 2 ? 16384 : 0; }
 
 }  // namespace grace
 
@@ -401,15 +408,27 @@ grace_status_t grace_div_scalar(const float* x, float divisor, float* out, int64
                        stream);
 }
 
+int64_t grace_hbm_probe_elems(int64_t n, int32_t variant) {
+  if (variant < 0 || variant >= kProbeVariants || n < 0) return -1;
+  const int64_t c = probe_chunk(variant);
+  return c ? n / c * c : n / 4 * 4;
+}
+
 grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream) {
-  GRACE_REQUIRE(r && g && o && n > 0 && (variant == 0 || variant == 1) && aligned16(r) && aligned16(g) &&
-                    aligned16(o) && n % kProbeChunk == 0,
-                "grace_hbm_probe: bad arguments (n a multiple of 16384, 16-B aligned buffers)");
+  GRACE_REQUIRE(r && g && o && n >= 16384 && variant >= 0 && variant < kProbeVariants && aligned16(r) &&
+                    aligned16(g) && aligned16(o),
+                "grace_hbm_probe: bad arguments (n >= 16384, 16-B aligned buffers, variant 0..5)");
   f32x4v* r4 = reinterpret_cast<f32x4v*>(r);
   const f32x4v* g4 = reinterpret_cast<const f32x4v*>(g);
   f32x4v* o4 = reinterpret_cast<f32x4v*>(o);
-  if (variant == 0) probe_2r2w_chunk<<<(unsigned)(n / kProbeChunk), 256, 0, as_stream(stream)>>>(r4, g4, o4);
-  else probe_2r2w_stride<<<2048, 256, 0, as_stream(stream)>>>(r4, g4, o4, n / 4);
+  const hipStream_t s = as_stream(stream);
+  const unsigned chunks = (unsigned)(grace_hbm_probe_elems(n, variant) / (probe_chunk(variant) ? probe_chunk(variant) : 1));
+  switch (variant) {
+    case 0: probe_2r2w_chunk<8><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
+    case 1: probe_2r2w_chunk<12><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
+    case 2: probe_2r2w_chunk<16><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
+    default: probe_2r2w_stride<<<1024u << (variant - 3), 256, 0, s>>>(r4, g4, o4, n / 4); break;
+  }
   GRACE_CHECK_LAUNCH("grace_hbm_probe");
   return GRACE_OK;
 }

@@ -2,7 +2,23 @@
 
 Differences: ``communicator='broadcast'`` works (the reference omits ``rank``, helper.py:95-97);
 ``kernel`` for top-k and the ``*_cuda`` codec names select the same native HIP codecs.
+
+Extra keys (ignored by the reference's helper, so a params dict stays valid for both): for the
+variable-size codecs ``threshold`` and ``dgc``, ``exchange`` ('counts' | 'capacity'),
+``capacity_margin`` and ``overflow`` ('retry' | 'defer') pick the W > 1 payload exchange
+(grace_amd/dist/compressor/threshold.py, dgc.py): 'capacity' moves one fixed-size record per rank
+with no host read in the common step.
 """
+
+
+def _exchange_kwargs(params, default_overflow):
+    kw = {}
+    if 'exchange' in params:
+        kw['exchange'] = params['exchange']
+    if 'capacity_margin' in params:
+        kw['capacity_margin'] = params['capacity_margin']
+    kw['overflow'] = params.get('overflow', default_overflow)
+    return kw
 
 
 def grace_from_params(params):
@@ -11,7 +27,7 @@ def grace_from_params(params):
     comm = params.get('communicator', 'allreduce')
     if comp == 'dgc':
         from grace_amd.dist.compressor.dgc import DgcCompressor
-        compressor = DgcCompressor(params.get('compress_ratio', 0.3))
+        compressor = DgcCompressor(params.get('compress_ratio', 0.3), **_exchange_kwargs(params, 'defer'))
     elif comp == 'efsignsgd':
         from grace_amd.dist.compressor.efsignsgd import EFSignSGDCompressor
         compressor = EFSignSGDCompressor(params.get('lr', 0.1))
@@ -53,7 +69,7 @@ def grace_from_params(params):
         compressor = TernGradCompressor()
     elif comp == 'threshold':
         from grace_amd.dist.compressor.threshold import ThresholdCompressor
-        compressor = ThresholdCompressor(params.get('threshold', 0.01))
+        compressor = ThresholdCompressor(params.get('threshold', 0.01), **_exchange_kwargs(params, 'retry'))
     elif comp == 'topk':
         from grace_amd.dist.compressor.topk import TopKCompressor
         compressor = TopKCompressor(params.get('compress_ratio', 0.3), params.get('kernel', 'torch'))

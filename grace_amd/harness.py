@@ -22,7 +22,10 @@ def step_parameters(model, grc):
 
 
 class GradBucket:
-    """One flat f32 buffer holding every parameter's gradient (parameters' .grad become views)."""
+    """One flat f32 buffer holding every parameter's gradient (parameters' .grad become views).
+    Autograd accumulates into the existing .grad views in place, so a backward pass writes straight
+    into ``flat``; clear it with ``zero_()`` (not ``optimizer.zero_grad()``, whose default
+    set_to_none=True would detach the views)."""
 
     def __init__(self, model):
         params = [p for p in model.parameters() if p.requires_grad]
@@ -36,6 +39,10 @@ class GradBucket:
             off += n
         self.params = params
         self.sizes = [p.numel() for p in params]
+
+    def zero_(self):
+        self.flat.zero_()
+        return self
 
 
 def step_segmented(bucket, engine, name="bucket"):
@@ -56,3 +63,41 @@ class ShapeModel(torch.nn.Module):
     def __init__(self, shapes, device):
         super().__init__()
         self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(s, device=device) * 0.01) for s in shapes])
+
+
+class _ConvBN(torch.nn.Sequential):
+    def __init__(self, c_in, c_out):
+        super().__init__(torch.nn.Conv2d(c_in, c_out, 3, padding=1, bias=False), torch.nn.BatchNorm2d(c_out),
+                         torch.nn.ReLU(inplace=True))
+
+
+class _Residual(torch.nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.res1, self.res2 = _ConvBN(c, c), _ConvBN(c, c)
+
+    def forward(self, x):
+        return x + self.res2(self.res1(x))
+
+
+class ResNet9(torch.nn.Module):
+    """The DAWNBench ResNet-9 of the reference's DDP example (examples/dist/CIFAR10-dawndist/
+    dawn.py:26-63: prep 64, layer1 128 + residual, layer2 256, layer3 512 + residual, 4x4 max pool,
+    linear 512 -> 10 without bias, output x 0.125), from torch.nn layers: a real model whose
+    backward writes the gradients the harness compresses (random init; the example's CIFAR-10
+    download is not available offline, so inputs are synthetic)."""
+
+    def __init__(self, channels=(64, 128, 256, 512), weight=0.125):
+        super().__init__()
+        c0, c1, c2, c3 = channels
+        self.prep = _ConvBN(3, c0)
+        self.layer1 = torch.nn.Sequential(_ConvBN(c0, c1), torch.nn.MaxPool2d(2), _Residual(c1))
+        self.layer2 = torch.nn.Sequential(_ConvBN(c1, c2), torch.nn.MaxPool2d(2))
+        self.layer3 = torch.nn.Sequential(_ConvBN(c2, c3), torch.nn.MaxPool2d(2), _Residual(c3))
+        self.linear = torch.nn.Linear(c3, 10, bias=False)
+        self.weight = weight
+
+    def forward(self, x):
+        x = self.layer3(self.layer2(self.layer1(self.prep(x))))
+        x = torch.nn.functional.max_pool2d(x, 4).flatten(1)
+        return self.linear(x) * self.weight

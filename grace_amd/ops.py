@@ -843,6 +843,34 @@ def dgc_compress(t, ratio, sample_idx=None, seed=0):
     return vals, idx, meta
 
 
+def dgc_threshold_dev(t, ratio, sample_idx=None, seed=0):
+    """DgcCompressor.compress's threshold, chunk counts and offsets (grace_dgc_threshold) with NO
+    host read: the count stays on the device (meta words: thr0, thr, count at ws[8:12]) for the
+    capacity-bounded or counts exchange (grace_amd/dist/compressor/dgc.py)."""
+    t = dev_f32(t)
+    n = t.numel()
+    ns = max(1, int(n * 0.01))
+    ks = max(1, int(n * ratio * 0.01))
+    sample = torch.empty(ns, dtype=F32, device=t.device)
+    _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
+    _, top, _ = topk_compress(sample, min(ks, ns))
+    ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
+    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    return ws
+
+
+def dgc_write_capped(t, ws, cap):
+    """This rank's exchange record {count, cap | vals f32[cap] | idx i32[cap]} (int32 words)."""
+    t = dev_f32(t)
+    rec = torch.empty(exchange_record_words(cap), dtype=torch.int32, device=t.device)
+    _lib.call("grace_dgc_write_capped", _p(t), t.numel(), _p(ws), _p(rec), int(cap), _stream())
+    return rec
+
+
+def dgc_mask_update_capped(rec, cap, residual, accum):
+    _lib.call("grace_dgc_mask_update_capped", _p(rec), int(cap), _p(residual), _p(accum), _stream())
+
+
 def dgc_select(t, ratio, sample_idx=None, seed=0):
     """The sampled threshold and its adjustment loop only (grace_dgc_select); returns the DGC
     workspace whose first 16 bytes are the meta grace_dgc_step_w1 / dgc_mask_update read."""

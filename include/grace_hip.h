@@ -72,7 +72,9 @@ grace_status_t grace_div_scalar(const float* x, float divisor, float* out, int64
 grace_status_t grace_fill(float* x, float value, int64_t n, void* stream);
 /* HBM ceiling probe for bench.py (no reference counterpart): r = r + g, o = 0 with non-temporal 16-B
    loads / stores (the top-k step's 2-read / 2-write dense traffic, none of its arithmetic).
-   variant 0: 16384-element chunks per workgroup; 1: grid-stride.  n % 16384 == 0. */
+   variant 0-2: chunks of 8192 / 12288 / 16384 elements per workgroup; 3-5: grid-stride over
+   1024 / 2048 / 4096 workgroups.  grace_hbm_probe_elems: the elements a launch covers (-1: bad). */
+int64_t grace_hbm_probe_elems(int64_t n, int32_t variant);
 grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream);
 /* Compressor.aggregate = Python sum() in rank order (grace_dl/dist/__init__.py:32-34):
  * first != 0: acc = 0.0f + x (so -0 -> +0), else acc = acc + x. */
@@ -405,6 +407,15 @@ grace_status_t grace_dgc_sample(const float* t, int64_t n, const int64_t* sample
 grace_status_t grace_dgc_threshold(const float* t, int64_t n, const float* top_vals, int64_t ks, double ratio,
                                    void* ws, void* stream);
 grace_status_t grace_dgc_write(const float* t, int64_t n, const void* ws, float* vals, int64_t* idx, void* stream);
+/* Capacity-bounded exchange (no reference counterpart; replaces the size round trip of
+   grace_dl/dist/communicator/allgather.py:15-38 for DGC): after grace_dgc_threshold, write this rank's
+   record {count, cap, 0, 0 | vals f32[cap] | idx i32[cap]} (grace_exchange_record_words(cap) words),
+   entries past cap dropped; aggregate the gathered records with grace_sparse_aggregate_capped. */
+grace_status_t grace_dgc_write_capped(const float* t, int64_t n, const void* ws, uint32_t* rec, int64_t cap,
+                                      void* stream);
+/* DgcMemory.update (grace_dl/dist/memory/dgc.py:21-28) over the record's entries: r[i] *= 0, a[i] *= 0. */
+grace_status_t grace_dgc_mask_update_capped(const uint32_t* rec, int64_t cap, float* residual, float* accum,
+                                            void* stream);
 /* memory: r = m r + g, a = a + r (has_state 0: r = a = g);  update: r *= keep, a *= keep with
  * keep = !(|t| >= thr) (t may alias a) */
 grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accum, int32_t has_state,

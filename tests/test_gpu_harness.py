@@ -98,3 +98,47 @@ def test_segmented_resnet50_set_full():
             _, _, _, res[j], o = O.topk_residual_step(g, res[j], 0.01)
             assert same_bits(out[off:off + g.size], o), (s, j)
             off += g.size
+
+
+def test_harness_real_backward_resnet9():
+    """SURVEY.md §8f.1 with a real model: the DAWN example's ResNet-9 (harness.ResNet9, torch.nn
+    layers) on synthetic CIFAR-shaped batches; ``loss.backward()`` writes every gradient into the
+    GradBucket's .grad views, then (a) the reference's per-parameter loop
+    (examples/dist/CIFAR10-dawndist/core.py:204-208, ``step_parameters``) on one copy of the model
+    and (b) ``step_segmented`` on a second copy compress them.  Both must equal the per-tensor
+    oracle top-k + residual step applied to the gradients autograd produced, over two iterations,
+    and (b) must leave its results in the .grad views in place."""
+    from grace_amd.dist.helper import grace_from_params
+    from grace_amd.dist.segmented import SegmentedTopK
+    from grace_amd.harness import GradBucket, ResNet9, step_parameters, step_segmented
+    torch.manual_seed(0)
+    m1 = ResNet9().cuda()
+    m2 = ResNet9().cuda()
+    m2.load_state_dict(m1.state_dict())
+    b1, b2 = GradBucket(m1), GradBucket(m2)
+    assert len(b1.params) == 25 and sum(b1.sizes) == 6_573_120
+    grc = grace_from_params({"compressor": "topk", "compress_ratio": 0.01, "memory": "residual",
+                             "communicator": "allgather", "world_size": 1})
+    eng = SegmentedTopK(0.01)
+    gen = torch.Generator().manual_seed(3)
+    res = [[None] * len(b1.params), [None] * len(b2.params)]
+    for s in range(2):
+        x = torch.randn(16, 3, 32, 32, generator=gen).cuda()
+        y = torch.randint(0, 10, (16,), generator=gen).cuda()
+        grads = []
+        for m, b in ((m1, b1), (m2, b2)):
+            b.zero_()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            grads.append(b.flat.cpu().numpy())
+        offs = np.cumsum([0] + b2.sizes)
+        for b in (b1, b2):                                       # .grad still views of the bucket
+            assert all(p.grad.data_ptr() == b.flat[int(o):].data_ptr() for p, o in zip(b.params, offs))
+        for g in grads:
+            assert np.count_nonzero(g) > 0.9 * g.size            # autograd wrote the bucket
+        step_parameters(m1, grc)
+        step_segmented(b2, eng)
+        for which, b in enumerate((b1, b2)):
+            for j, p in enumerate(b.params):
+                gj = grads[which][offs[j]:offs[j + 1]]
+                _, _, _, res[which][j], out = O.topk_residual_step(gj, res[which][j], 0.01)
+                assert same_bits(p.grad.detach().cpu().numpy().ravel(), out), (("loop", "segmented")[which], s, j)
