@@ -191,23 +191,36 @@ struct SignStepOp {
 // World-1 sign step without codes (the launch-bound 4 MiB configs[0] step): U float4 per thread,
 // every load issued before any store (one HBM latency per thread), no grid-stride loop; the scalar
 // tail (n % 4) is handled by the first workgroup.
+#ifndef GRACE_SIGN_NT
+#define GRACE_SIGN_NT 0
+#endif
+#ifndef GRACE_SIGN_BLOCK
+#define GRACE_SIGN_BLOCK 256
+#endif
+constexpr int kSignBlock = GRACE_SIGN_BLOCK;
+typedef float sf4v __attribute__((ext_vector_type(4)));
 template <int U>
-__global__ __launch_bounds__(kBlock) void sign_step_w1_kernel(const float* __restrict__ x, float* __restrict__ o,
-                                                             int64_t n) {
+__global__ __launch_bounds__(kSignBlock) void sign_step_w1_kernel(const float* __restrict__ x, float* __restrict__ o,
+                                                                 int64_t n) {
   const int64_t n4 = n >> 2;
-  const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
-  float4 v[U];
+  const int64_t base = (int64_t)blockIdx.x * kSignBlock * U + threadIdx.x;
+  sf4v v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int64_t i = base + (int64_t)u * kBlock;
-    v[u] = reinterpret_cast<const float4*>(x)[i < n4 ? i : 0];
+    const int64_t i = base + (int64_t)u * kSignBlock;
+    const sf4v* src = reinterpret_cast<const sf4v*>(x) + (i < n4 ? i : 0);
+    if constexpr (GRACE_SIGN_NT & 1) v[u] = __builtin_nontemporal_load(src);
+    else v[u] = *src;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int64_t i = base + (int64_t)u * kBlock;
-    if (i < n4)
-      reinterpret_cast<float4*>(o)[i] = make_float4(v[u].x >= 0.f ? 1.f : -1.f, v[u].y >= 0.f ? 1.f : -1.f,
-                                                    v[u].z >= 0.f ? 1.f : -1.f, v[u].w >= 0.f ? 1.f : -1.f);
+    const int64_t i = base + (int64_t)u * kSignBlock;
+    if (i < n4) {
+      const sf4v r = {v[u].x >= 0.f ? 1.f : -1.f, v[u].y >= 0.f ? 1.f : -1.f, v[u].z >= 0.f ? 1.f : -1.f,
+                      v[u].w >= 0.f ? 1.f : -1.f};
+      if constexpr (GRACE_SIGN_NT & 2) __builtin_nontemporal_store(r, reinterpret_cast<sf4v*>(o) + i);
+      else reinterpret_cast<sf4v*>(o)[i] = r;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t i = (n4 << 2) + threadIdx.x;
@@ -478,8 +491,8 @@ grace_status_t grace_sign_step_w1(const float* x, uint8_t* codes, float* out, in
 #define GRACE_SIGN_U 1   // A/B over 200 steps: U = 1, 2 -> 5.1 us/step, U = 4 -> 5.7, U = 8 -> 5.5
 #endif
     constexpr int U = GRACE_SIGN_U;
-    const int64_t grid = ((n >> 2) + kBlock * U - 1) / (kBlock * U);
-    sign_step_w1_kernel<U><<<(unsigned)grid, kBlock, 0, as_stream(stream)>>>(x, out, n);
+    const int64_t grid = ((n >> 2) + kSignBlock * U - 1) / (kSignBlock * U);
+    sign_step_w1_kernel<U><<<(unsigned)grid, kSignBlock, 0, as_stream(stream)>>>(x, out, n);
     GRACE_CHECK_LAUNCH("grace_sign_step_w1");
     return GRACE_OK;
   }
