@@ -138,6 +138,10 @@ constexpr int kSampleBlock = 1024;
 // (twice the workgroups, each still one per CU for the 136 KB of LDS histograms), 256 -> 256
 constexpr int kBracketBlock = GRACE_BRACKET_BLOCK;
 constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-octave bins
+#ifndef GRACE_SAMPLE_RUN
+#define GRACE_SAMPLE_RUN 1
+#endif
+constexpr int kBracketRun = GRACE_SAMPLE_RUN;              // adjacent elements per sampling thread
 constexpr int kCoarseBins = 2048;                          // key >> 20: 1/8-octave bins
 constexpr int kHistStride = 1;
 
@@ -451,15 +455,28 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   STAMP(w.ctl, 0);
   const uint32_t st = (uint32_t)a.stratum;
   const int64_t sidx = (int64_t)blockIdx.x * kBracketBlock + tid;
-  const bool valid = sidx < a.sample_n;
-  float t = 0.f;
+  // kBracketRun > 1 (A/B builds): every thread takes a run of adjacent elements at a hashed,
+  // run-aligned offset in a stratum of kBracketRun * stratum elements -- fewer DRAM rows opened
+  // per sample, at the price of samples that are no longer independent on correlated buckets
+  const bool valid = sidx * kBracketRun < a.sample_n;
+  float t[kBracketRun];
+#pragma unroll
+  for (int q = 0; q < kBracketRun; ++q) t[q] = 0.f;
   if (valid) {
-    const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+    if constexpr (kBracketRun == 1) {
+      const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
 #ifdef GRACE_SAMPLE_SEQ   // diagnostic A/B build only: contiguous sample positions
-    t = compensate<HAS_RES>(a, sidx + 0 * off);
+      t[0] = compensate<HAS_RES>(a, sidx + 0 * off);
 #else
-    t = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+      t[0] = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
 #endif
+    } else {
+      const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32) *
+                           kBracketRun;
+      const int64_t i0 = sidx * (int64_t)st * kBracketRun + off;
+#pragma unroll
+      for (int q = 0; q < kBracketRun; ++q) t[q] = compensate<HAS_RES>(a, i0 + q);
+    }
   }
   // counters of this step's main / finalize passes (their previous users have completed)
   if (blockIdx.x == 0 && tid >= 3 && tid < 12) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
@@ -470,9 +487,12 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   __syncthreads();
   STAMP(w.ctl, 1);
   if (valid) {
-    const uint32_t key = abs_key(t);
-    atomicAdd(&lh[key >> 16], 1u);
-    atomicAdd(&lc[key >> 20], 1u);
+#pragma unroll
+    for (int q = 0; q < kBracketRun; ++q) {
+      const uint32_t key = abs_key(t[q]);
+      atomicAdd(&lh[key >> 16], 1u);
+      atomicAdd(&lc[key >> 20], 1u);
+    }
   }
   __syncthreads();
   for (int b = tid; b < kBracketBins; b += kBracketBlock)
@@ -1445,7 +1465,14 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   a.stratum = a.n / a.sample_n;
   // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
   static_assert(kSmallN >= kHistBins, "bracket grid covers the histogram zeroing");
-  topk_bracket<HAS_RES><<<(unsigned)((a.sample_n + kBracketBlock - 1) / kBracketBlock), kBracketBlock, 0, s>>>(a, w);
+  // runs of kBracketRun samples only when the sample tiles the bucket into whole runs
+  static_assert(kSampleMax % (kBracketRun * kBracketBlock) == 0, "sample runs tile the grid");
+  if (kBracketRun > 1 && a.sample_n != kSampleMax) {
+    set_error_msg("grace_topk: sample runs need n >= the sample size (A/B build)");
+    return GRACE_ERR_ARG;
+  }
+  topk_bracket<HAS_RES><<<(unsigned)((a.sample_n / kBracketRun + kBracketBlock - 1) / kBracketBlock), kBracketBlock, 0,
+                          s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
   const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>);
   if (vec)
