@@ -135,7 +135,7 @@ SIGNATURES = {
     "grace_powersgd_outer": (ST, [P, P, I64, I64, I32, P, P, P, P]),
     "grace_powersgd_w1_ok": (I32, [I64, I64, I32]),
     "grace_powersgd_w1_workspace_bytes": (SZ, [I64, I64]),
-    "grace_powersgd_w1_compress": (ST, [P, I64, I64, P, U64, P, P, P, SZ, P]),
+    "grace_powersgd_w1_compress": (ST, [P, I64, I64, P, U64, P, P, P, SZ, P, P]),
     "grace_normal_fill": (ST, [P, I64, U64, P]),
 }
 

@@ -10,6 +10,8 @@
 // load of M is a 16-B (float4) load and M is read exactly once per product.
 #include <math.h>
 
+#include <atomic>
+
 #include "common.h"
 
 namespace grace {
@@ -1146,7 +1148,8 @@ constexpr uint32_t kW1SpinMax = 1u << 22;     // bounded waits (never expected t
 struct W1Ws {
   uint32_t* arr;      // [S] exchange arrivals
   uint32_t* done;     // [S] exchange reads
-  uint32_t* ctl;      // [0] robust-path flag, [1] its reads, [2] status (1 = a wait ran out)
+  uint32_t* ctl;      // [0] robust-path flag (= this call's tag), [2] waits that ran out (count)
+  uint32_t* status;   // optional host-mapped word: bit 1 = a wait ran out (the call's P, Q invalid)
   uint64_t* dbg;      // diagnostic stamps (GRACE_STAMPS builds only)
   f32x4v* xp;         // [S][G][64] partial P rows
   double* qpart;      // [S][m][4] one f64 partial of Qraw per slab
@@ -1161,16 +1164,23 @@ __device__ __forceinline__ float row16_sum_f32(float v) {
   return v;
 }
 
-__device__ __forceinline__ bool spin_until(const uint32_t* p, uint32_t target, uint32_t* status) {
+// bounded wait for *p >= target (or == target when EQ); a wait that runs out is counted in ctl[2]
+// and flagged in the host-mapped status word (bit `bit`): the call's P and Q are then not valid and
+// the host raises (grace_amd/ops.py).  Never expected: the grid is one workgroup per CU
+// (occupancy-checked) and the Python layer never lets two of these grids run at once.
+template <bool EQ = false>
+__device__ __forceinline__ bool spin_until(const uint32_t* p, uint32_t target, const W1Ws& ws, uint32_t bit) {
   uint32_t spins = 0;
-  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  while (true) {
+    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (EQ ? v == target : v >= target) return true;
     __builtin_amdgcn_s_sleep(2);
     if (++spins > kW1SpinMax) {
-      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ws.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ws.status) __hip_atomic_fetch_or(ws.status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
   }
-  return true;
 }
 
 template <bool DRAWQ>
@@ -1290,7 +1300,7 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
       __syncthreads();
       if (t == 0) {
         __hip_atomic_fetch_add(ws.arr + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spin_until(ws.arr + s, (uint32_t)G, ws.ctl + 2);
+        spin_until(ws.arr + s, (uint32_t)G, ws, 2u);   // runs out: flagged invalid (status bit 1)
       }
       __syncthreads();
       W1_STAMP(ws, 2);
@@ -1315,13 +1325,14 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
       if (cg == 0) {
         // group 0 writes P_raw and the slab's Gram partials: wave 0 holds the 64 slab rows, each
         // DPP row of 16 sums its rows' products (f64, symmetric butterflies) -> 4 partials per slab
-        if (row < n) *reinterpret_cast<f32x4v*>(P + row * 4) = part;
+        const f32x4v pr = part;
+        if (row < n) *reinterpret_cast<f32x4v*>(P + row * 4) = pr;
         double gv[10];
         int e = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int c2 = c; c2 < 4; ++c2, ++e) gv[e] = row < n ? (double)part[c] * (double)part[c2] : 0.0;
+          for (int c2 = c; c2 < 4; ++c2, ++e) gv[e] = row < n ? (double)pr[c] * (double)pr[c2] : 0.0;
 #pragma unroll
         for (int k = 0; k < 10; ++k) gv[k] = row16_sum(gv[k]);
         if ((t & 15) == 0) {
@@ -1463,7 +1474,7 @@ __device__ void w1_direct_q(const float* __restrict__ M, const float* __restrict
 
 __global__ __launch_bounds__(kW1FinBlock) void psgd_w1_fin(const float* __restrict__ M, float* __restrict__ P,
                                                           int64_t n, int64_t m, float* __restrict__ Q, W1Ws ws,
-                                                          int S) {
+                                                          int S, uint32_t tag) {
   __shared__ double Gs[10];
   __shared__ double Rs[4][4];
   __shared__ double Rinv[4];
@@ -1575,22 +1586,19 @@ __global__ __launch_bounds__(kW1FinBlock) void psgd_w1_fin(const float* __restri
       if (t == 0 && NB > 1) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(ws.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.ctl, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {
       if (t == 0) {
-        spin_until(ws.ctl, 1u, ws.ctl + 2);
+        // the flag holds the tag of the call that set it, so a flag left by an earlier call never
+        // matches and nothing has to reset it (a run-out wait is flagged to the host: bit 1)
+        spin_until<true>(ws.ctl, tag, ws, 2u);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
     }
     w1_direct_q(M, P, n, m, q0, q1, Q);
-    if (b != 0 && t == 0 &&
-        __hip_atomic_fetch_add(ws.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)NB - 2) {
-      __hip_atomic_store(ws.ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // last reader
-      __hip_atomic_store(ws.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     return;
   }
   FIN_STAMP(ws, 3);
@@ -1852,6 +1860,7 @@ static size_t w1_bytes(int64_t n, int64_t m) {
 static W1Ws w1_carve(void* base, int64_t n, int64_t m) {
   char* p = reinterpret_cast<char*>(base);
   W1Ws w;
+  w.status = nullptr;
   w.ctl = reinterpret_cast<uint32_t*>(p); p += 256;
   w.arr = reinterpret_cast<uint32_t*>(p); p += w1_align(4 * kW1MaxSlabs);
   w.done = reinterpret_cast<uint32_t*>(p); p += w1_align(4 * kW1MaxSlabs);
@@ -1891,7 +1900,8 @@ int32_t grace_powersgd_w1_ok(int64_t n, int64_t m, int32_t r) {
 size_t grace_powersgd_w1_workspace_bytes(int64_t n, int64_t m) { return w1_bytes(n, m); }
 
 grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, const float* q, uint64_t seed,
-                                          float* P, float* Q, void* ws, size_t ws_bytes, void* stream) {
+                                          float* P, float* Q, void* ws, size_t ws_bytes, uint32_t* status_host,
+                                          void* stream) {
   GRACE_REQUIRE(M && P && Q && ws && grace_powersgd_w1_ok(n, m, 4), "grace_powersgd_w1_compress: bad arguments");
   GRACE_REQUIRE(((reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(P) |
                   reinterpret_cast<uintptr_t>(Q) | reinterpret_cast<uintptr_t>(ws)) & 15u) == 0,
@@ -1901,7 +1911,17 @@ grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, 
     return GRACE_ERR_WORKSPACE;
   }
   const hipStream_t st = as_stream(stream);
-  const W1Ws w = w1_carve(ws, n, m);
+  W1Ws w = w1_carve(ws, n, m);
+  w.status = nullptr;
+  if (status_host) {   // pinned host word; the kernels write it through its device mapping
+    void* dp = nullptr;
+    w.status = hipHostGetDevicePointer(&dp, status_host, 0) == hipSuccess && dp ? reinterpret_cast<uint32_t*>(dp)
+                                                                                 : status_host;
+  }
+  // per-call tag of the robust path's flag: never equal to a flag an earlier call left behind
+  static std::atomic<uint32_t> g_w1_tag{0};
+  uint32_t tag = ++g_w1_tag;
+  if (tag == 0) tag = ++g_w1_tag;
   const int G = w1_G(m);
   const int64_t S = w1_S(n);
   int64_t SG = min((int64_t)w1_cus() / G, w1_SG_max(n, m));   // one workgroup per CU: co-resident
@@ -1913,7 +1933,7 @@ grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, 
   int64_t nb = (max(n, m) + 15) / 16;
   nb = min(nb, min((int64_t)256, (int64_t)w1_cus()));   // one per CU at most: co-resident (robust path)
   if (nb < 1) nb = 1;
-  psgd_w1_fin<<<(unsigned)nb, kW1FinBlock, 0, st>>>(M, P, n, m, Q, w, (int)S);   // one partial per slab
+  psgd_w1_fin<<<(unsigned)nb, kW1FinBlock, 0, st>>>(M, P, n, m, Q, w, (int)S, tag);   // one partial per slab
   GRACE_CHECK_LAUNCH("psgd_w1_fin");
   return GRACE_OK;
 }

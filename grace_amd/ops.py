@@ -728,9 +728,64 @@ def powersgd_w1_compress(M2d, q=None, seed=0):
     P = torch.empty(n, 4, dtype=F32, device=dev)
     Q = torch.empty(m, 4, dtype=F32, device=dev)
     ws = workspace("powersgd_w1", _lib.query("grace_powersgd_w1_workspace_bytes", n, m), dev)
+    status = _w1_status(dev)
+    _w1_order(dev)
     _lib.call("grace_powersgd_w1_compress", _p(M2d), n, m, _p(require_dev(q)) if q is not None else None,
-              int(seed) & (2 ** 64 - 1), _p(P), _p(Q), _p(ws), ws.numel(), _stream())
+              int(seed) & (2 ** 64 - 1), _p(P), _p(Q), _p(ws), ws.numel(), status.data_ptr(), _stream())
     return P, Q
+
+
+_w1_last = {}
+
+
+def _w1_order(dev):
+    """The one-pass kernels spin on a grid of one workgroup per CU: two such grids running at once
+    (calls on two streams) could each hold CUs the other waits for.  So a call issued on a stream
+    other than the previous call's first waits for everything already queued there (an event
+    recorded only when the stream changes: no cost for one-stream callers)."""
+    key = str(dev)
+    cur = torch.cuda.current_stream(dev)
+    last = _w1_last.get(key)
+    if last is not None and last.cuda_stream != cur.cuda_stream:
+        ev = torch.cuda.Event()
+        ev.record(last)
+        cur.wait_event(ev)
+    _w1_last[key] = cur
+
+
+class PowerSGDWaitError(RuntimeError):
+    """A wait of the one-pass PowerSGD kernels ran out in an earlier call: that call's P and Q were
+    not valid (grace_powersgd_w1_compress, status bit 1)."""
+
+
+_w1_st = {}
+
+
+def _w1_status(dev):
+    """The pinned status word the one-pass PowerSGD kernels write (include/grace_hip.h), checked
+    here at every call: it covers the earlier calls whose kernels have finished since.  Bit 1 (a
+    wait ran out: that call's P and Q were not valid) raises PowerSGDWaitError."""
+    key = str(dev)
+    hit = _w1_st.get(key)
+    if hit is None:
+        st = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        hit = _w1_st[key] = (st, st.numpy())     # numpy view: a plain host read per call
+    st, view = hit
+    v = int(view[0])
+    if v:
+        view[0] = 0
+        if v & 2:
+            raise PowerSGDWaitError("grace_amd: a one-pass PowerSGD wait ran out in an earlier call; its P and Q "
+                                    "were not valid (never expected: another kernel kept its workgroups from "
+                                    "becoming resident)")
+    return st
+
+
+def powersgd_w1_check():
+    """Wait for the device and check the one-pass PowerSGD status word (raises on bit 1)."""
+    torch.cuda.synchronize()
+    for key in list(_w1_st):
+        _w1_status(key)
 
 
 def orthogonalize_(A):

@@ -348,11 +348,18 @@ grace_status_t grace_powersgd_outer(const float* P, const float* Q, int64_t n, i
  * not be orthogonalised).  Qraw = M^T (M q) is accumulated in f64 and solved by the R of P's QR.
  * Eligibility (grace_powersgd_w1_ok): r == 4, m % 4 == 0, m <= 16384, n <= 1 Mi rows; 16-B aligned
  * pointers.  The workspace (grace_powersgd_w1_workspace_bytes) is zeroed once at allocation and
- * left with its counters zeroed by every call. */
+ * left with its counters zeroed by every call.
+ * The kernels hand data between workgroups with bounded waits on a grid of one workgroup per CU;
+ * two such calls must not run concurrently (on two streams), or their grids could each hold CUs
+ * the other one waits for.  `status_host` (optional, pinned host memory, never cleared by the
+ * library) receives bit 1 when a wait ran out: that call's P and Q must not be used.  The caller
+ * reads it after the stream has passed the call (grace_amd/ops.py checks it at every call and
+ * orders calls issued on different streams). */
 int32_t grace_powersgd_w1_ok(int64_t n, int64_t m, int32_t r);
 size_t grace_powersgd_w1_workspace_bytes(int64_t n, int64_t m);
 grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, const float* q, uint64_t seed,
-                                          float* P, float* Q, void* ws, size_t ws_bytes, void* stream);
+                                          float* P, float* Q, void* ws, size_t ws_bytes, uint32_t* status_host,
+                                          void* stream);
 /* standard normal fill (q draws, powersgd.py:41 / memory/powersgd.py:27), device generator */
 grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* stream);
 

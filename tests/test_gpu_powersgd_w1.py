@@ -39,9 +39,12 @@ def _close(a, b, m, scale=None):
 
 
 def _counters_zero():
+    """Arrival / read counters and the run-out count left zero.  Word 0 is the robust path's flag:
+    it keeps the tag of the last call that set it (each call waits for its own tag), so it is not
+    a counter and is not reset."""
     ws = ops.workspace("powersgd_w1", 256, torch.device(DEV))
     head = _np(ws[: 256 + 2 * 4 * 16384].view(torch.int32))
-    return not head.any()
+    return not head[1:].any()
 
 
 @pytest.mark.parametrize("shape", [(4096, 4096), (256, 300), (100, 1000), (4097, 1028), (64, 16384), (9000, 256),
@@ -150,3 +153,41 @@ def test_compressor_takes_the_w1_path_and_matches_reference_algorithm():
     Pe, Qe = _expect(M, q0)
     assert _close(_np(p), Pe, 2048, scale=1.0)
     assert _close(_np(q), Qe, 1024)
+
+
+def test_w1_two_streams_ordered_and_exact():
+    """two one-pass compresses issued on two streams at once.  Their grids (one
+    workgroup per CU, spinning exchanges) must never run concurrently: ops orders a call on a new
+    stream behind the previous call's stream.  Both results equal the one-stream results bit for
+    bit, and the status word reports no wait that ran out."""
+    rng = np.random.default_rng(31)
+    Ms = [_t(rng.standard_normal((4096, 4096)).astype(np.float32)) for _ in range(4)]
+    qs = [_t(rng.standard_normal((4096, 4)).astype(np.float32)) for _ in range(4)]
+    ref = [tuple(_np(x) for x in ops.powersgd_w1_compress(M, q)) for M, q in zip(Ms, qs)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for rep in range(3):
+        for j, (M, q) in enumerate(zip(Ms, qs)):
+            with torch.cuda.stream(streams[j % 2]):
+                outs.append((j, ops.powersgd_w1_compress(M, q)))
+    torch.cuda.synchronize()
+    for j, (P, Q) in outs:
+        assert np.array_equal(_np(P), ref[j][0]) and np.array_equal(_np(Q), ref[j][1]), j
+    ops.powersgd_w1_check()              # raises if any wait ran out
+    assert _counters_zero()
+
+
+def test_w1_status_word_raises():
+    """A wait that ran out (status bit 1, written by the kernels into the pinned word) makes the
+    next call raise instead of returning silently wrong P / Q."""
+    M = _t(np.random.default_rng(2).standard_normal((512, 256)).astype(np.float32))
+    ops.powersgd_w1_compress(M)
+    torch.cuda.synchronize()
+    st, view = ops._w1_st[str(M.device)]
+    view[0] = 2
+    with pytest.raises(ops.PowerSGDWaitError):
+        ops.powersgd_w1_compress(M)
+    assert int(view[0]) == 0
+    ops.powersgd_w1_compress(M)          # cleared: the next call runs
+    ops.powersgd_w1_check()
