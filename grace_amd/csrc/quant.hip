@@ -686,6 +686,14 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
 // Stage 1 writes f64 partials per work unit (16384 elements); stage 2 (encode) reduces its
 // segment's partials with the whole workgroup in a fixed order (every unit of a segment derives
 // the identical scale), then encodes its unit.  Both stages move 16 B per lane.
+// Where the segment scale is reduced (A/B knob): 0 = the last stats unit of each segment to arrive
+// (agent-scope partials + arrival ticket), 1 = every encode unit of the segment, from the stats
+// kernel's plain partials, at the start of the encode while its first x loads are in flight (the
+// stats kernel then has no arrival tail).  Both sum the partials in unit order: identical scales.
+#ifndef GRACE_TERN_ENC_REDUCE
+#define GRACE_TERN_ENC_REDUCE 1
+#endif
+constexpr bool kTernEncReduce = GRACE_TERN_ENC_REDUCE != 0;
 #ifndef GRACE_TERN_UNIT
 #define GRACE_TERN_UNIT 16384   // A/B, ResNet-50 set compress: 4096 / 8192 / 16384 / 32768 -> 64.7 /
 #endif                          // 56.5 / 54.0 / 60.6 us (tools/ab_quant.py, one process)
@@ -783,6 +791,11 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
   }
   const TernPartial p = block_tern_reduce(sum, sq, amax, nan);
   uint64_t* pw = reinterpret_cast<uint64_t*>(&w[unit].part);
+  if constexpr (kTernEncReduce) {
+    // the encode kernel reduces the segment's partials itself (next launch: plain stores suffice)
+    if (t == 0) w[unit].part = p;
+    return;
+  }
   if (t == 0) {
     __hip_atomic_store(pw, (uint64_t)__double_as_longlong(p.sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(pw + 1, (uint64_t)__double_as_longlong(p.sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -834,11 +847,15 @@ constexpr int kTernBlock = GRACE_TERN_BLOCK;
 
 // FUSED: the world-1 Allgather step in the same pass -- out = 0 + code * scalar (the decoder's
 // arithmetic, division by 1 omitted) written instead of the codes: bit-identical to encode + decode.
-template <bool FUSED = false>
+// HAS_U: an injected uniform stream (parity tests); a separate instantiation, so the device-
+// generator path has no load under a branch (hipcc would wait vmcnt(0) at the join, i.e. also for
+// the prefetched next sub-chunk)
+template <bool FUSED = false, bool HAS_U = false>
 __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
     int nseg, const TernSlot* __restrict__ w, const float* __restrict__ u, uint64_t seed,
-    int8_t* __restrict__ codes, float* __restrict__ out = nullptr) {
+    int8_t* __restrict__ codes, float* __restrict__ out, const float* __restrict__ clip_in,
+    float* __restrict__ scalars) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
   const int64_t unit = blockIdx.x;
@@ -866,8 +883,34 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
   };
   f4v cur[kTernSub], nxt[kTernSub];
   load_sub(0, cur);
-  const TernScale sc = w[sv.sub[s]].scale;   // published by the segment's last stats unit
-  const float c = sc.c, scalar = sc.scalar;
+  float c, scalar;
+  if constexpr (kTernEncReduce) {
+    // the segment's statistics from its units' partials, in unit order (every unit of the segment
+    // computes the identical scale); the first unit publishes the scalar
+    double ps = 0.0, pq = 0.0;
+    float pm = 0.f;
+    uint32_t pn = 0;
+    for (int64_t j = sv.sub[s] + t; j < sv.sub[s + 1]; j += kTernBlock) {
+      const TernPartial pj = w[j].part;
+      ps += pj.sum; pq += pj.sq; pm = fmaxf(pm, pj.amax); pn |= pj.nan;
+    }
+    const TernPartial q = block_tern_reduce<kTernBlock>(ps, pq, pm, pn);
+    if (clip_in) {
+      c = clip_in[s];
+    } else {
+      const double nn = (double)(sv.seg[s + 1] - sv.seg[s]);
+      const double mean = q.sum / nn;
+      double var = q.sq / nn - mean * mean;
+      if (var < 0.0) var = 0.0;
+      c = (float)(2.5 * (double)(float)sqrt(var));
+    }
+    scalar = q.nan ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
+    if (t == 0 && unit == sv.sub[s]) scalars[s] = scalar;
+  } else {
+    const TernScale sc = w[sv.sub[s]].scale;   // published by the segment's last stats unit
+    c = sc.c;
+    scalar = sc.scalar;
+  }
 
   auto enc = [&](float xv, float ui) -> int8_t {
     const float cl = fminf(fmaxf(xv, -c), c);
@@ -886,43 +929,63 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
   };
   if (base + t < qs.a0) {
     const int64_t i = base + t;
-    put1(i, enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i)));
+    put1(i, enc(x[i], HAS_U ? u[i] : uniform01(seed, (uint64_t)i)));
   }
   if (qs.a1 + t < end) {
     const int64_t i = qs.a1 + t;
-    put1(i, enc(x[i], u ? u[i] : uniform01(seed, (uint64_t)i)));
+    put1(i, enc(x[i], HAS_U ? u[i] : uniform01(seed, (uint64_t)i)));
   }
+  // The quads: the same codes as enc() with fewer instructions.  With s = scalar > 0 (then
+  // c >= scalar > 0): enc() is sign(x) where u s < min(|x|, c) and 0 elsewhere (x = +-0 never
+  // passes the test; NaN x cannot occur, it makes the scalar NaN).  With scalar 0 or NaN every code
+  // is 0: using NaN for the product makes the test fail there too.  The code byte of a selected x is
+  // 0x01 or 0xFF from its sign bit.  32-bit quad offsets; the generator key is hoisted
+  // (uniform01x4_k = uniform01x4 for element indices below 2^32).
+  const float sc_eff = scalar > 0.f ? scalar : __int_as_float(0x7FC00000);
+  const bool key32 = qs.a1 <= ((int64_t)1 << 32);
+  const uint64_t key = mix64(seed);
+  auto codes4 = [&](const f4v& v, const f4v& uu) -> uint32_t {
+    uint32_t cw = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool sel = uu[j] * sc_eff < fminf(fabsf(v[j]), c);
+      const uint32_t byte = ((uint32_t)((int32_t)__float_as_uint(v[j]) >> 31) | 1u) & 0xFFu;
+      cw |= (sel ? byte : 0u) << (8 * j);   // (the shifts fold into v_lshl_or)
+    }
+    return cw;
+  };
+  auto encode_quad = [&](int jq, const f4v& v) {
+    const int64_t i = qs.a0 + 4 * (int64_t)jq;
+    f4v uu;
+    if constexpr (HAS_U) {
+      uu = *reinterpret_cast<const f4v*>(u + i);
+    } else {
+      float r4[4];
+      if (key32) uniform01x4_k(key, (uint32_t)i, r4);
+      else uniform01x4(seed, (uint64_t)i, r4);
+      uu = f4v{r4[0], r4[1], r4[2], r4[3]};
+    }
+    const uint32_t cw = codes4(v, uu);
+    if constexpr (FUSED) {
+      f4v o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = 0.f + (float)(int8_t)(uint8_t)(cw >> (8 * j)) * scalar;
+      __builtin_nontemporal_store(o, reinterpret_cast<f4v*>(out + i));
+    } else {
+      *reinterpret_cast<uint32_t*>(codes + i) = cw;
+    }
+  };
+  // two sub-chunk buffers, used alternately in the fully unrolled loop (static registers, no copies)
+  const int nqi = (int)nq;
 #pragma unroll
   for (int st = 0; st < kTernSteps; ++st) {
-    if (st + 1 < kTernSteps) load_sub(st + 1, nxt);
+    f4v (&curb)[kTernSub] = (st & 1) ? nxt : cur;
+    f4v (&nxtb)[kTernSub] = (st & 1) ? cur : nxt;
+    if (st + 1 < kTernSteps) load_sub(st + 1, nxtb);
 #pragma unroll
     for (int k = 0; k < kTernSub; ++k) {
-      const int64_t j = t + (int64_t)(st * kTernSub + k) * kTernBlock;
-      if (j < nq) {
-        const int64_t i = qs.a0 + 4 * j;
-        const f4v v = cur[k];
-        f4v uu;
-        if (u) {
-          uu = *reinterpret_cast<const f4v*>(u + i);
-        } else {
-          float r4[4];
-          uniform01x4(seed, (uint64_t)i, r4);
-          uu = f4v{r4[0], r4[1], r4[2], r4[3]};
-        }
-        if constexpr (FUSED) {
-          __builtin_nontemporal_store(f4v{0.f + (float)enc(v.x, uu.x) * scalar, 0.f + (float)enc(v.y, uu.y) * scalar,
-                                          0.f + (float)enc(v.z, uu.z) * scalar, 0.f + (float)enc(v.w, uu.w) * scalar},
-                                      reinterpret_cast<f4v*>(out + i));
-        } else {
-          const uint32_t cw = (uint32_t)(uint8_t)enc(v.x, uu.x) | ((uint32_t)(uint8_t)enc(v.y, uu.y) << 8) |
-                              ((uint32_t)(uint8_t)enc(v.z, uu.z) << 16) | ((uint32_t)(uint8_t)enc(v.w, uu.w) << 24);
-          *reinterpret_cast<uint32_t*>(codes + i) = cw;
-        }
-      }
-    }
-    if (st + 1 < kTernSteps) {
-#pragma unroll
-      for (int k = 0; k < kTernSub; ++k) cur[k] = nxt[k];
+      const int jq = t + (st * kTernSub + k) * kTernBlock;
+      if (jq < nqi) encode_quad(jq, curb[k]);
     }
   }
 }
@@ -1588,8 +1651,12 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
   tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
                                                                        scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
-  tern_encode_kernel<<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w,
-                                                                         u, seed, codes);
+  if (u)
+    tern_encode_kernel<false, true><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, scalars);
+  else
+    tern_encode_kernel<false, false><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
   return GRACE_OK;
 }
@@ -1604,8 +1671,12 @@ grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, co
   tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
                                                                        scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_step_w1");
-  tern_encode_kernel<true><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, w,
-                                                                               u, seed, nullptr, out);
+  if (u)
+    tern_encode_kernel<true, true><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, nullptr, out, clip_in, scalars);
+  else
+    tern_encode_kernel<true, false><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, nullptr, out, clip_in, scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_step_w1");
   return GRACE_OK;
 }
