@@ -309,6 +309,34 @@ def measured_copy_gbs(dev, n=1 << 26, sets=3, reps=7):
     return round(best, 1), best_v
 
 
+def measured_encode_gbs(dev, n, sets=4, reps=7):
+    """The box's ceiling for the encoders' traffic mix (QSGD / TernGrad compress: read 4 B, write 1 B
+    per element): ``grace_hbm_probe`` variants 6-9 (non-temporal 16-B loads, one byte stored per
+    element, no arithmetic) over `sets` rotated buffer sets of `n` floats, the fastest variant's
+    median over `reps` launches.  Returns (GB/s counting 5 B per element, variant)."""
+    from grace_amd import _lib, ops
+    bufs = [(torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(n // 4 + 16, dtype=torch.float32, device=dev))
+            for _ in range(sets)]
+    best, best_v = 0.0, None
+    for variant in range(6, 10):
+        elems = int(_lib.query("grace_hbm_probe_elems", n, variant))
+        ts = []
+        for i in range(reps + sets):
+            g, o = bufs[i % sets]
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            _lib.call("grace_hbm_probe", g.data_ptr(), g.data_ptr(), o.data_ptr(), n, variant, ops._stream())
+            b.record()
+            b.synchronize()
+            if i >= sets:
+                ts.append(a.elapsed_time(b) * 1e-3)
+        gbs = 5.0 * elems / sorted(ts)[len(ts) // 2] / 1e9
+        if gbs > best:
+            best, best_v = gbs, variant
+    del bufs
+    return round(best, 1), best_v
+
+
 def host_cores():
     """(threads to use, how they were chosen): the physical cores of the CPUs this process may run
     on (its affinity mask, SMT siblings counted once), capped by OMP_NUM_THREADS when the box sets
@@ -585,6 +613,10 @@ def bench_quant(args, world, rank, dev):
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
+    # the encoders' own ceiling: the same read-4-B / write-1-B mix streamed with no arithmetic
+    enc_gbs, enc_v = measured_encode_gbs(dev, total)
+    line["roofline"].update({"measured_encode_mix_gbs": enc_gbs, "measured_encode_mix_variant": enc_v,
+                             "encode_floor_us": round(5.0 * total / enc_gbs / 1e3, 2)})
     return line
 
 

@@ -389,8 +389,33 @@ __global__ __launch_bounds__(256) void probe_2r2w_stride(f32x4v* __restrict__ r,
     __builtin_nontemporal_store(f32x4v{0.f, 0.f, 0.f, 0.f}, o + i);
   }
 }
-constexpr int kProbeVariants = 6;
-static int64_t probe_chunk(int variant) { return variant == 0 ? 8192 : variant == 1 ? 12288 : variant == 2 ? 16384 : 0; }
+// Variants 6-9: the encoders' mix (QSGD / TernGrad / natural compress: read f32, write one byte per
+// element) -- read g, write o's bytes (the top byte of each element).  6 / 7: one chunk of
+// 256 x 4 x VEC elements per workgroup (VEC 8 / 16), every load issued first; 8 / 9: grid-stride over
+// 2048 / 4096 workgroups.
+__device__ __forceinline__ uint32_t probe_pack(const f32x4v v) {
+  return __builtin_amdgcn_perm(__builtin_amdgcn_perm(__float_as_uint(v.w), __float_as_uint(v.z), 0x0c0c0703u),
+                               __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0c0c0703u),
+                               0x05040100u);
+}
+template <int VEC>
+__global__ __launch_bounds__(256) void probe_4r1w_chunk(const f32x4v* __restrict__ g, uint32_t* __restrict__ o) {
+  const int64_t base = (int64_t)blockIdx.x * (256 * VEC) + threadIdx.x;
+  f32x4v a[VEC];
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) a[u] = __builtin_nontemporal_load(g + base + u * 256);
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) __builtin_nontemporal_store(probe_pack(a[u]), o + base + u * 256);
+}
+__global__ __launch_bounds__(256) void probe_4r1w_stride(const f32x4v* __restrict__ g, uint32_t* __restrict__ o,
+                                                        int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(probe_pack(__builtin_nontemporal_load(g + i)), o + i);
+}
+constexpr int kProbeVariants = 10;
+static int64_t probe_chunk(int variant) {
+  return variant == 0 ? 8192 : variant == 1 ? 12288 : variant == 2 ? 16384 : variant == 6 ? 8192 : variant == 7 ? 16384 : 0;
+}
 
 }  // namespace grace
 
@@ -430,7 +455,7 @@ int64_t grace_hbm_probe_elems(int64_t n, int32_t variant) {
 grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream) {
   GRACE_REQUIRE(r && g && o && n >= 16384 && variant >= 0 && variant < kProbeVariants && aligned16(r) &&
                     aligned16(g) && aligned16(o),
-                "grace_hbm_probe: bad arguments (n >= 16384, 16-B aligned buffers, variant 0..5)");
+                "grace_hbm_probe: bad arguments (n >= 16384, 16-B aligned buffers, variant 0..9)");
   f32x4v* r4 = reinterpret_cast<f32x4v*>(r);
   const f32x4v* g4 = reinterpret_cast<const f32x4v*>(g);
   f32x4v* o4 = reinterpret_cast<f32x4v*>(o);
@@ -440,6 +465,9 @@ grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, in
     case 0: probe_2r2w_chunk<8><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
     case 1: probe_2r2w_chunk<12><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
     case 2: probe_2r2w_chunk<16><<<chunks, 256, 0, s>>>(r4, g4, o4); break;
+    case 6: probe_4r1w_chunk<8><<<chunks, 256, 0, s>>>(g4, reinterpret_cast<uint32_t*>(o)); break;
+    case 7: probe_4r1w_chunk<16><<<chunks, 256, 0, s>>>(g4, reinterpret_cast<uint32_t*>(o)); break;
+    case 8: case 9: probe_4r1w_stride<<<2048u << (variant - 8), 256, 0, s>>>(g4, reinterpret_cast<uint32_t*>(o), n / 4); break;
     default: probe_2r2w_stride<<<1024u << (variant - 3), 256, 0, s>>>(r4, g4, o4, n / 4); break;
   }
   GRACE_CHECK_LAUNCH("grace_hbm_probe");

@@ -364,6 +364,337 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
   }
 }
 
+// The device-generator fast path of qsgd_encode128_kernel (no injected u, no injected norms): the
+// same codes and norms bit for bit (tests/test_gpu_quant.py feeds the injected-stream kernel the
+// generator's uniforms, tests/device_rng.py).  Per element the non-pipelined kernel spent ~38 VALU
+// instructions (SQ_INSTS_VALU): the kernel is issue-bound, its 128 MB moving at 3.5 TB/s against
+// the 5.5 TB/s the same read-4-B / write-1-B mix streams at (grace_hbm_probe variants 6-9: 20.8 us).
+// What this kernel removes:
+//  * the per-stage segment walk: each workgroup tabulates its buckets' base offsets in LDS once;
+//  * f2i16_x86's NaN / range selects on the int8 path: with a finite norm and scale every level is
+//    <= q (1 + 3 eps), so the code is the low byte of the exact integer (rows with a non-finite
+//    scale take qsgd_code);
+//  * half the bucket scalar work: even lanes of a row compute bucket 0's correctly rounded sqrt and
+//    divisions, odd lanes bucket 1's, and quad_perm DPP moves hand every lane both;
+//  * the index multiply of the generator (formed once per bucket).
+// Software pipelined as well: a row owns buckets row, row + 16, ... of the workgroup's range, kQNB
+// per stage, and stage i + 1's loads are issued before stage i is reduced, encoded and stored.
+// Every load is unconditional (a stage past the range loads x[0..3] and is discarded), so hipcc never
+// has to assume a skipped load and wait vmcnt(0) for the prefetched stage.  Buckets that are not
+// whole, 16-B aligned 128-element blocks (a segment's partial last bucket, unaligned segments) are
+// skipped by the pipeline and encoded afterwards by their row with per-element loads.
+// ResNet-50 set (25.5 M elements, 199,672 buckets): 36.7 -> 34.2 us.
+#ifndef GRACE_QENC_PIPE
+#define GRACE_QENC_PIPE 1
+#endif
+#ifndef GRACE_QENC_PIPE_GRID
+#define GRACE_QENC_PIPE_GRID 4096   // A/B on the ResNet-50 set: 1024 35.6, 2048 34.6, 4096 34.2 us
+#endif
+constexpr int kQEncPipeGridCap = GRACE_QENC_PIPE_GRID;
+#ifndef GRACE_QENC_PIPE_FUSED
+#define GRACE_QENC_PIPE_FUSED 0
+#endif
+constexpr int kQBkMax = 1024;   // buckets per workgroup of the pipelined encoder (its LDS table)
+#ifndef GRACE_QENC_NT
+#define GRACE_QENC_NT 1
+#endif
+
+template <typename CodeT, int VARIANT, bool FUSED>
+struct QsgdPipe {
+  static constexpr bool kStage16 = !FUSED && sizeof(CodeT) == 1;
+  static constexpr int kRows = kQBlock / 16;
+  struct Tile {
+    f4v v[kQNB][2];
+    int32_t base[kQNB], bb[kQNB];
+    bool full[kQNB];
+  };
+
+  // uniform01x4_k with i * 0x9E3779B1 supplied (the kernel forms it from a per-bucket product)
+  __device__ static __forceinline__ void uniform4(uint32_t ic, uint32_t klo, uint32_t khi, float (&u)[4]) {
+    uint32_t h = fmix32((ic ^ klo) + khi);
+    u[0] = (float)(h >> 8) * (1.0f / 16777216.0f);
+    h = h ? h : 0x9E3779B9u;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      h ^= h << 13;
+      h ^= h >> 17;
+      h ^= h << 5;
+      u[j] = (float)(h >> 8) * (1.0f / 16777216.0f);
+    }
+  }
+
+  __device__ static __forceinline__ float bucket_norm(double acc) {
+    acc = row16_sum(acc);
+    return VARIANT == 0 ? sqrtf((float)acc) : (float)sqrt(acc);
+  }
+
+  __device__ static __forceinline__ double sq_acc(const float (&v)[4], double acc) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (VARIANT == 0 || isfinite(v[j])) acc = fma((double)v[j], (double)v[j], acc);
+    return acc;
+  }
+};
+
+template <typename CodeT, int VARIANT, bool FUSED = false>
+__global__ __launch_bounds__(kQBlock) void qsgd_encode128_pipe_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
+    int nseg, int32_t nbuckets, float qf, uint64_t seed, float* __restrict__ norms_out,
+    CodeT* __restrict__ codes, float* __restrict__ fused_out) {
+  using P = QsgdPipe<CodeT, VARIANT, FUSED>;
+  using Tile = typename P::Tile;
+  constexpr int kRows = P::kRows;
+  constexpr int kStride = kQNB * kRows;
+  constexpr bool kStage16 = P::kStage16;
+  constexpr bool kI8 = VARIANT == 0 && sizeof(CodeT) == 1;
+  constexpr uint32_t kC = 0x9E3779B1u;
+  __shared__ SegTables32 tab;
+  __shared__ uint32_t cst[kStage16 ? kRows : 1][kQNB * 32];
+  // the workgroup's buckets: base element offset, bit 31 set when not a whole 16-B-aligned bucket
+  // (one binary search per bucket here instead of a segment walk in every stage)
+  __shared__ int32_t bkt[kQBkMax];
+  stage_tables32(tab, seg_off, bkt_off, nseg);
+  const bool codes16 = (reinterpret_cast<uintptr_t>(codes) & 15) == 0;
+  const int l16 = threadIdx.x & 15;
+  const int row = threadIdx.x >> 4;
+  const bool odd = (l16 & 1) != 0;
+  const uint64_t key = mix64(seed);
+  const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+  const uint32_t lane_c = (uint32_t)(4 * l16) * kC;
+  int32_t blo, bhi;
+  block_range32(nbuckets, kRows, blo, bhi);
+  const int32_t nbk = bhi - blo;   // <= kQBkMax (host grid)
+  if (nbk <= 0) return;
+  for (int32_t j = threadIdx.x; j < nbk; j += kQBlock) {
+    const int32_t b = blo + j;
+    const int sj = find_seg32(tab.sub, nseg, b);
+    const int32_t base = tab.seg[sj] + (b - tab.sub[sj]) * 128;
+    const bool full = (base & 3) == 0 && base + 128 <= tab.seg[sj + 1];
+    bkt[j] = full ? base : (int32_t)((uint32_t)base | 0x80000000u);
+  }
+  __syncthreads();
+
+  auto issue = [&](int32_t j0, Tile& T) {   // j0: the stage's first bucket, relative to blo
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      const int32_t j = j0 + row + h * kRows;
+      const bool ok = j < nbk;
+      const int32_t ent = bkt[ok ? j : 0];
+      const bool full = ok && ent >= 0;
+      const int32_t base = ent & 0x7FFFFFFF;
+      T.bb[h] = blo + j;
+      T.base[h] = base;
+      T.full[h] = full;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        int32_t e = full ? base + 4 * l16 + 64 * q : 0;
+        asm volatile("" : "+v"(e));   // opaque: hipcc would otherwise split the load into a branch
+#if GRACE_QENC_NT
+        T.v[h][q] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + e));
+#else
+        T.v[h][q] = *reinterpret_cast<const f4v*>(x + e);
+#endif
+      }
+    }
+  };
+
+  auto encode = [&](Tile& T) {
+    double acc[kQNB];
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {   // all 16 lanes of every row take part in the row reductions
+      acc[h] = 0.0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float v4[4] = {T.v[h][q][0], T.v[h][q][1], T.v[h][q][2], T.v[h][q][3]};
+#ifdef GRACE_DIAG_NONORM   // diagnostic A/B build only: no bucket reduction
+        acc[h] += (double)v4[0];
+#else
+        acc[h] = P::sq_acc(v4, acc[h]);
+#endif
+      }
+      acc[h] = row16_sum(acc[h]);
+    }
+    // bucket scalars: norm, scale (level = scale |x|, the same expression as qsgd_code's callers)
+    // and the decoder's norm / q.  With two buckets a stage, the even lanes of a row compute bucket
+    // 0's and the odd lanes bucket 1's (one correctly rounded sqrt and divisions per lane instead of
+    // two), then quad_perm DPP moves hand each lane both.
+    float norm[kQNB], scale[kQNB], dsc[kQNB];
+    auto scalars = [&](double a, float& nm, float& sc, float& ds) {
+      nm = VARIANT == 0 ? sqrtf((float)a) : (float)sqrt(a);
+      sc = VARIANT == 0 ? (1.0f / nm) * qf : qf / nm;
+      ds = nm / qf;
+    };
+    if constexpr (kQNB == 2) {
+      float nm, sc, ds;
+      scalars(odd ? acc[1] : acc[0], nm, sc, ds);
+      auto even = [](float v) {   // quad_perm [0,0,2,2]
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xA0, 0xF, 0xF, false));
+      };
+      auto oddl = [](float v) {   // quad_perm [1,1,3,3]
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xF, 0xF, false));
+      };
+      norm[0] = even(nm); norm[1] = oddl(nm);
+      scale[0] = even(sc); scale[1] = oddl(sc);
+      if constexpr (FUSED) { dsc[0] = even(ds); dsc[1] = oddl(ds); }
+      if (!FUSED && l16 < 2) {   // lane h of the row stores bucket h's norm
+        const bool f = odd ? T.full[1] : T.full[0];
+        if (f) norms_out[odd ? T.bb[1] : T.bb[0]] = nm;
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < kQNB; ++h) {
+        scalars(acc[h], norm[h], scale[h], dsc[h]);
+        if (!FUSED && l16 == 0 && T.full[h]) norms_out[T.bb[h]] = norm[h];
+      }
+    }
+#ifdef GRACE_DIAG_NONORM
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) { norm[h] = (float)acc[h] + 1.f; scale[h] = qf / norm[h]; dsc[h] = norm[h] / qf; }
+#endif
+#pragma unroll
+    for (int h = 0; h < kQNB; ++h) {
+      if (!T.full[h]) continue;   // row-uniform
+      const int32_t base = T.base[h];
+      const bool st16 = kStage16 && codes16 && (base & 15) == 0;
+      const bool fin = scale[h] < __builtin_inff() && norm[h] < __builtin_inff();   // row-uniform
+      const uint32_t bc = (uint32_t)base * kC + lane_c;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int32_t eq = base + 4 * l16 + 64 * q;
+        float uu[4];
+#ifdef GRACE_DIAG_NORNG   // diagnostic A/B build only: constant u
+        uu[0] = uu[1] = uu[2] = uu[3] = 0.5f + 0.f * (float)bc;
+#else
+        P::uniform4(bc + (uint32_t)(64 * q) * kC, klo, khi, uu);
+#endif
+        CodeT c[4];
+        uint32_t cw = 0;   // the int8 codes packed (kI8)
+        float cf[4];       // the codes as floats (FUSED)
+        if (kI8 && fin) {
+          // qsgd_code<int8, 0> for a finite norm and scale: then every x is finite and
+          // level <= q (1 + 3 eps), so f2i16_x86's NaN / range test never fires and the codeword
+          // is the low byte of the exact integer copysign(nl, x)
+          int32_t ni[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xv = T.v[h][q][j];
+            const float level = scale[h] * fabsf(xv);
+            const float prev = floorf(level);
+            const float nl = uu[j] < level - prev ? prev + 1.0f : prev;
+            ni[j] = (int32_t)copysignf(nl, xv);
+            cf[j] = (float)(int8_t)ni[j];
+          }
+          cw = __builtin_amdgcn_perm(__builtin_amdgcn_perm((uint32_t)ni[3], (uint32_t)ni[2], 0x0c0c0400u),
+                                     __builtin_amdgcn_perm((uint32_t)ni[1], (uint32_t)ni[0], 0x0c0c0400u),
+                                     0x05040100u);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xv = T.v[h][q][j];
+            const float level = scale[h] * fabsf(xv);   // VARIANT 1: scale = q / norm
+            c[j] = qsgd_code<CodeT, VARIANT>(xv, level, uu[j], norm[h]);
+            cf[j] = (float)c[j];
+          }
+          if constexpr (sizeof(CodeT) == 1)
+            cw = (uint32_t)(uint8_t)c[0] | ((uint32_t)(uint8_t)c[1] << 8) | ((uint32_t)(uint8_t)c[2] << 16) |
+                 ((uint32_t)(uint8_t)c[3] << 24);
+        }
+        if constexpr (FUSED) {
+          f4v o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float d = dsc[h] * cf[j];
+            if (VARIANT == 1 && cf[j] == -128.0f) d = __int_as_float(0x7FC00000);
+            o[j] = 0.f + d;
+          }
+          __builtin_nontemporal_store(o, reinterpret_cast<f4v*>(fused_out + eq));
+        } else if (kStage16 && st16) {
+#ifdef GRACE_DIAG_NOSTORE   // diagnostic A/B build only: no code stores (a never-true runtime guard)
+          if (norm[h] < 0.f)
+#endif
+          cst[row][h * 32 + q * 16 + l16] = cw;
+        } else if constexpr (sizeof(CodeT) == 1) {
+          *reinterpret_cast<uint32_t*>(codes + eq) = cw;
+        } else {
+          store_codes4(codes, eq, eq + 4, true, c);
+        }
+      }
+    }
+    if constexpr (kStage16) {   // the row's staged buckets, 16 B per lane (same wave wrote them)
+#pragma unroll
+      for (int h0 = 0; h0 < kQNB; h0 += 2) {
+        const bool hi = (l16 >> 3) != 0;   // lanes 8..15 store bucket h0 + 1 (selects, not an index)
+        const bool has = h0 + 1 < kQNB;
+        const bool fl = hi ? (has && T.full[has ? h0 + 1 : h0]) : T.full[h0];
+        const int32_t bs = hi ? T.base[has ? h0 + 1 : h0] : T.base[h0];
+        if (fl && codes16 && (bs & 15) == 0) {
+          const uint4 wv = *reinterpret_cast<const uint4*>(&cst[row][(h0 + (hi ? 1 : 0)) * 32 + 4 * (l16 & 7)]);
+#ifdef GRACE_DIAG_NOSTORE
+          if (wv.x == 0x12345678u && wv.y == 0x9abcdef0u)
+#endif
+          *reinterpret_cast<uint4*>(codes + bs + 16 * (l16 & 7)) = wv;
+        }
+      }
+    }
+  };
+
+  // block-uniform trip count; two tiles used alternately (static registers, no copies)
+  Tile A, B;
+  issue(0, A);
+  for (int32_t j0 = 0; j0 < nbk; j0 += 2 * kStride) {
+    issue(j0 + kStride, B);
+    encode(A);
+    issue(j0 + 2 * kStride, A);
+    encode(B);
+  }
+
+  // the buckets the pipeline skipped: partial or unaligned, per-element loads (no prefetch pending)
+  for (int32_t j = row; j < nbk; j += kRows) {
+    if (bkt[j] >= 0) continue;   // row-uniform: done by the pipeline
+    const int32_t bb = blo + j;
+    const int sj = find_seg32(tab.sub, nseg, bb);
+    const int32_t base = tab.seg[sj] + (bb - tab.sub[sj]) * 128;
+    const int32_t end = min(base + 128, tab.seg[sj + 1]);
+    float v[2][4];
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int32_t eq = base + 4 * l16 + 64 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[q][j] = eq + j < end ? x[eq + j] : 0.f;
+      acc = P::sq_acc(v[q], acc);
+    }
+    const float norm = P::bucket_norm(acc);
+    if (!FUSED && l16 == 0) norms_out[bb] = norm;
+    const float scale = VARIANT == 0 ? (1.0f / norm) * qf : qf / norm;
+    const float dsc = norm / qf;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int32_t eq = base + 4 * l16 + 64 * q;
+      float uu[4];
+      P::uniform4((uint32_t)eq * kC, klo, khi, uu);
+      CodeT c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float level = VARIANT == 0 ? scale * fabsf(v[q][j]) : qf / norm * fabsf(v[q][j]);
+        c[j] = qsgd_code<CodeT, VARIANT>(v[q][j], level, uu[j], norm);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (eq + j >= end) continue;
+        if constexpr (FUSED) {
+          const float cf = (float)c[j];
+          float d = dsc * cf;
+          if (VARIANT == 1 && cf == -128.0f) d = __int_as_float(0x7FC00000);
+          fused_out[eq + j] = 0.f + d;
+        } else {
+          codes[eq + j] = c[j];
+        }
+      }
+    }
+  }
+}
+
 template <typename CodeT, int VARIANT>
 __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
@@ -1496,6 +1827,13 @@ __global__ __launch_bounds__(kQBlock) void qsgd_global_encode_kernel(const float
 
 using namespace grace;
 
+// the pipelined encoder's grid: the cap, or more workgroups when a workgroup's bucket range would
+// outgrow its LDS table (block_range32 rounds a range up to a multiple of 16 rows)
+static unsigned qenc_pipe_grid(int64_t nbuckets) {
+  const int64_t need = (nbuckets + (kQBkMax - 32) - 1) / (kQBkMax - 32);
+  return (unsigned)std::max<int64_t>(stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncPipeGridCap), need);
+}
+
 extern "C" {
 
 grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg,
@@ -1507,11 +1845,18 @@ grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const 
                 "grace_qsgd_step_w1: bad arguments (bucket 128, <= kSegLds segments)");
   if (nbuckets == 0) return GRACE_OK;
   hipStream_t st = as_stream(stream);
-  const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
+  // the fused step keeps the non-pipelined kernel: it writes 4 B per element, and the A/B on the
+  // ResNet-50 set had the pipelined one slower there (43.1 / 40.6 us at 1024 / 2048 workgroups vs 40.3)
+  const bool pipe = GRACE_QENC_PIPE_FUSED && !u;
+  const unsigned grid16 = pipe ? qenc_pipe_grid(nbuckets) : stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
 #define GRACE_QSTEP128(CT, V)                                                                        \
-  qsgd_encode128_kernel<CT, V, true><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
-                                                              (float)quantum_num, u, seed, nullptr, nullptr, \
-                                                              nullptr, out)
+  do { if (pipe)                                                                                          \
+    qsgd_encode128_pipe_kernel<CT, V, true><<<grid16, kQBlock, 0, st>>>(                             \
+        x, seg_off, bkt_off, nseg, (int32_t)nbuckets, (float)quantum_num, seed, nullptr, nullptr, out); \
+  else                                                                                               \
+    qsgd_encode128_kernel<CT, V, true><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
+                                                                (float)quantum_num, u, seed, nullptr, nullptr, \
+                                                                nullptr, out); } while (0)
   if (variant == 1) GRACE_QSTEP128(int8_t, 1);
   else if (quantum_num < 128) GRACE_QSTEP128(int8_t, 0);
   else GRACE_QSTEP128(__half, 0);
@@ -1534,11 +1879,17 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
   const unsigned grid = stream_grid(nbuckets, kQNB * kQBlock / 32, kQGridCap);
   hipStream_t st = as_stream(stream);
   if (bucket_size == 128 && nseg <= kSegLds && nbuckets < (int64_t(1) << 24)) {   // n < 2^31
-    const unsigned grid16 = stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
+    const bool pipe = GRACE_QENC_PIPE && !u && !norms_in;
+    const unsigned grid16 = pipe ? qenc_pipe_grid(nbuckets) : stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
 #define GRACE_QENC128(CT, V)                                                                         \
-  qsgd_encode128_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
-                                                        (float)quantum_num, u, seed, norms_in,        \
-                                                        norms_out, reinterpret_cast<CT*>(codes))
+  do { if (pipe)                                                                                          \
+    qsgd_encode128_pipe_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
+                                                               (float)quantum_num, seed, norms_out,  \
+                                                               reinterpret_cast<CT*>(codes), nullptr); \
+  else                                                                                               \
+    qsgd_encode128_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
+                                                          (float)quantum_num, u, seed, norms_in,      \
+                                                          norms_out, reinterpret_cast<CT*>(codes)); } while (0)
     if (variant == 1) GRACE_QENC128(int8_t, 1);
     else if (quantum_num < 128) GRACE_QENC128(int8_t, 0);
     else GRACE_QENC128(__half, 0);

@@ -73,7 +73,9 @@ grace_status_t grace_fill(float* x, float value, int64_t n, void* stream);
 /* HBM ceiling probe for bench.py (no reference counterpart): r = r + g, o = 0 with non-temporal 16-B
    loads / stores (the top-k step's 2-read / 2-write dense traffic, none of its arithmetic).
    variant 0-2: chunks of 8192 / 12288 / 16384 elements per workgroup; 3-5: grid-stride over
-   1024 / 2048 / 4096 workgroups.  grace_hbm_probe_elems: the elements a launch covers (-1: bad). */
+   1024 / 2048 / 4096 workgroups.  variant 6-9: the encoders' mix, read g and write one byte per
+   element to o (r unused): chunks of 8192 / 16384 elements, grid-stride over 2048 / 4096 workgroups.
+   grace_hbm_probe_elems: the elements a launch covers (-1: bad). */
 int64_t grace_hbm_probe_elems(int64_t n, int32_t variant);
 grace_status_t grace_hbm_probe(float* r, const float* g, float* o, int64_t n, int32_t variant, void* stream);
 /* Compressor.aggregate = Python sum() in rank order (grace_dl/dist/__init__.py:32-34):

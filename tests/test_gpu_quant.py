@@ -123,6 +123,37 @@ def test_qsgd_device_rng_properties():
     assert torch.equal(codes, codes2)
 
 
+@pytest.mark.parametrize("q,variant", [(127, 0), (255, 0), (127, 1)])
+def test_qsgd_device_rng_fast_path_bit_exact(q, variant):
+    """The device-generator encoder (qsgd_encode128_pipe_kernel: pipelined, partial / unaligned
+    buckets encoded afterwards) against the injected-stream encoder fed the same uniforms
+    (tests/device_rng.py), and against the oracle; the fused world-1 step against its decode.
+    Segments: whole buckets, a partial last bucket, unaligned starts, a 2-element segment."""
+    from tests.device_rng import qsgd_bucket128_uniforms
+    rng = np.random.default_rng(11 + q + variant)
+    sizes = [128 * 300, 1001, 4099, 2, 128 * 37, 64, 3, 128 * 21 + 5, 7777]
+    flat = (rng.standard_normal(sum(sizes)) * 0.01).astype(np.float32)
+    if variant == 1:
+        flat[[5, 40000, 45000]] = [np.inf, np.nan, -np.inf]
+    seed = 0xC0FFEE + q
+    u = qsgd_bucket128_uniforms(seed, sizes)
+    codes, norms = ops.qsgd_compress(_t(flat), q, 128, sizes=sizes, variant=variant, seed=seed)
+    codes_u, norms_u = ops.qsgd_compress(_t(flat), q, 128, sizes=sizes, variant=variant, u=_t(u))
+    assert same_bits(_np(norms), _np(norms_u))
+    assert same_bits(_np(codes), _np(codes_u))
+    if variant == 0:
+        off, noff = 0, 0
+        norms_np = _np(norms)
+        for n in sizes:
+            nb = (n + 127) // 128
+            exp_c, _ = O.qsgd_compress(flat[off:off + n], u[off:off + n], q, 128, norms=norms_np[noff:noff + nb])
+            assert same_bits(_np(codes)[off:off + n], exp_c), (n, off)
+            off, noff = off + n, noff + nb
+    dec = ops.qsgd_decompress(codes, norms, q, 128, flat.size, sizes=sizes, variant=variant)
+    fused = ops.qsgd_step_w1(_t(flat), q, sizes=sizes, variant=variant, seed=seed)
+    assert same_bits(_np(fused), _np(dec))
+
+
 def test_natural_vs_oracle():
     rng = np.random.default_rng(2)
     x = np.concatenate([rng.standard_normal(100000).astype(np.float32) * 3,
