@@ -149,15 +149,24 @@ def main():
         dist.destroy_process_group()
 
 
+# GRACE_BENCH_NO_PROBE=1: skip the in-bench HBM probes (profiling passes, whose per-dispatch
+# counters would otherwise include the probe kernels)
+NO_PROBE = os.environ.get("GRACE_BENCH_NO_PROBE", "0") not in ("", "0")
+
+
 def pmc_traffic(workload, alg_bytes):
     """HBM bytes per step of a secondary workload's kernels from the committed rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes (tools/prof_r02.sh -> tools/pmc_all.py), with the ratio to the algorithmic
     bytes; None when that workload was not profiled."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_secondary.json")
-    try:
-        with open(path) as f:
-            wl = json.load(f)["workloads"][workload]
-    except (OSError, ValueError, KeyError):
+    wl = None
+    for tag in ("r03", "r02"):   # the newest committed passes that cover the workload
+        try:
+            with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_secondary.json")) as f:
+                wl = json.load(f)["workloads"][workload]
+            break
+        except (OSError, ValueError, KeyError):
+            continue
+    if wl is None:
         return None, None
     t = wl["hbm_bytes_per_step"]
     return t, round(t / alg_bytes, 3)
@@ -231,7 +240,7 @@ def bench_topk(args, world, rank, dev):
         except (OSError, ValueError, KeyError):
             pass
     # the fraction against a copy bandwidth measured on this box as well
-    copy_gbs, variant = measured_copy_gbs(dev)
+    copy_gbs, variant = measured_copy_gbs(dev) if not NO_PROBE else (None, None)
     roofline["measured_copy_gbs"] = copy_gbs
     roofline["measured_copy_kind"] = ("grace_hbm_probe: 2-read / 2-write non-temporal 16-B stream (the step's "
                                       "dense traffic mix, no arithmetic) over 256 MiB arrays, 3 rotated sets, "
@@ -614,9 +623,10 @@ def bench_quant(args, world, rank, dev):
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
     # the encoders' own ceiling: the same read-4-B / write-1-B mix streamed with no arithmetic
-    enc_gbs, enc_v = measured_encode_gbs(dev, total)
-    line["roofline"].update({"measured_encode_mix_gbs": enc_gbs, "measured_encode_mix_variant": enc_v,
-                             "encode_floor_us": round(5.0 * total / enc_gbs / 1e3, 2)})
+    if not NO_PROBE:
+        enc_gbs, enc_v = measured_encode_gbs(dev, total)
+        line["roofline"].update({"measured_encode_mix_gbs": enc_gbs, "measured_encode_mix_variant": enc_v,
+                                 "encode_floor_us": round(5.0 * total / enc_gbs / 1e3, 2)})
     return line
 
 
