@@ -17,6 +17,11 @@ namespace grace {
 
 constexpr int kWave = 64;
 
+// aux operand of the raw buffer load / store builtins for the sc1 cache policy: 16-B write-through
+// stores (one fabric write per 16 B instead of one per dword) and loads that bypass the
+// (non-coherent) local L2 -- the agent-scope hand-offs of DESIGN.md §4
+constexpr int kSc1 = 16;
+
 // ------------------------------------------------------------------------------------------------
 // host-side error plumbing
 void set_error(const char* where, hipError_t e);

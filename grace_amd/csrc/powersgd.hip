@@ -98,9 +98,7 @@ __device__ __forceinline__ void sum_partials4(const float* __restrict__ p, int64
   }
 }
 
-// 16-B write-through partials (buffer ops with the sc1 cache policy, aux = 16): one fabric write per
-// 16 B instead of one per dword, and loads that bypass the (non-coherent) local L2
-constexpr int kSc1 = 16;
+// 16-B write-through partials: buffer ops with the sc1 cache policy (common.h kSc1)
 // elementwise sum over k < cnt (in order) of the 16-B runs at byte offset off + k * sb of `rs`,
 // 8 loads in flight
 __device__ __forceinline__ f32x4v sum_partials_v4(__amdgpu_buffer_rsrc_t rs, int sb, int cnt, int off) {

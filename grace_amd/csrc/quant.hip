@@ -1161,7 +1161,9 @@ __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __rest
       if (var < 0.0) var = 0.0;
       c = (float)(2.5 * (double)(float)sqrt(var));
     }
-    const float scalar = q.nan ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
+    // torch.clamp propagates a NaN bound (an injected NaN clip, or std = NaN when x holds an inf):
+    // every clamped element and the scalar are then NaN, as for a NaN element
+    const float scalar = (q.nan || c != c) ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
     w[first].scale = TernScale{c, scalar};
     scalars[s] = scalar;
     w[first].tick = 0u;   // left zeroed for the next call
@@ -1235,7 +1237,7 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
       if (var < 0.0) var = 0.0;
       c = (float)(2.5 * (double)(float)sqrt(var));
     }
-    scalar = q.nan ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
+    scalar = (q.nan || c != c) ? __int_as_float(0x7FC00000) : fminf(q.amax, c);   // (NaN bound: NaN)
     if (t == 0 && unit == sv.sub[s]) scalars[s] = scalar;
   } else {
     const TernScale sc = w[sv.sub[s]].scale;   // published by the segment's last stats unit

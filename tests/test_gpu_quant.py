@@ -299,6 +299,37 @@ def test_qsgd_bucket_decoder_multi_rank_aggregate(world):
     assert same_bits(out, exp)
 
 
+def test_terngrad_nan_clamp_bound_propagates():
+    """terngrad.py:13-16: torch.clamp with a NaN bound gives NaN everywhere, so the scalar is NaN and
+    every code 0.  The bound is NaN when the clip is injected as NaN or when the tensor holds an inf
+    (std = NaN).  Ragged segments around an inf segment, oracle bit-exact (scalars and codes)."""
+    rng = np.random.default_rng(21)
+    sizes = [5, 4099, 13, 70001, 7]
+    xs = [(rng.standard_normal(n) * 0.01).astype(np.float32) for n in sizes]
+    xs[1][17] = np.inf
+    xs[3][0] = -np.inf
+    flat = np.concatenate(xs)
+    u = rng.random(flat.size, dtype=np.float32)
+    offs = np.cumsum([0] + sizes[:-1])
+    clips = np.array([O.terngrad_clip(x) for x in xs], dtype=np.float32)
+    assert np.isnan(clips[1]) and np.isnan(clips[3]) and not np.isnan(clips[0])
+    for clip in (None, clips):
+        codes, scal = ops.terngrad_compress(_t(flat), sizes=sizes, u=_t(u), clip=None if clip is None else _t(clip))
+        exp = [O.terngrad_compress(x, u[o:o + n], clip=None if clip is None else clip[i])
+               for i, (x, n, o) in enumerate(zip(xs, sizes, offs))]
+        exp_s = np.concatenate([e[1] for e in exp])
+        s = _np(scal)
+        assert np.isnan(s[1]) and np.isnan(s[3])
+        if clip is None:   # device statistics: NaN where the oracle is NaN, else within 4 ulp
+            fin = ~np.isnan(exp_s)
+            assert same_bits(s[~fin], exp_s[~fin]) and ops.isclose_f32_ulps(s[fin], exp_s[fin], 4)
+        else:
+            assert same_bits(s, exp_s)
+            assert np.array_equal(_np(codes), np.concatenate([e[0] for e in exp]))
+        c = _np(codes)
+        assert not c[offs[1]:offs[1] + sizes[1]].any() and not c[offs[3]:offs[3] + sizes[3]].any()
+
+
 def test_terngrad_workspace_many_units_alternating():
     """A call with hundreds of units alternating with 3-unit calls on the same workspace: each
     segment's arrival counter must not share memory with a smaller call's partials (the
