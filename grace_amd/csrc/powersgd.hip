@@ -1125,10 +1125,20 @@ constexpr int kW1Cols = 1024;                 // columns per workgroup
 constexpr int kW1MaxG = 16;                   // m <= 16384
 constexpr int kW1FinBlock = 1024;
 constexpr uint32_t kW1SpinMax = 1u << 22;     // bounded waits (never expected to run out)
+#ifndef GRACE_W1_SPLIT
+#define GRACE_W1_SPLIT 0   // A/B knob (0: all 16 rows' loads in flight at once)
+#endif
+#ifndef GRACE_W1_NT
+#define GRACE_W1_NT 1      // non-temporal loads of M (A/B, one process: compress 34.9 -> 33.7 us)
+#endif
+#ifndef GRACE_W1_QNT
+#define GRACE_W1_QNT 1     // non-temporal stores of the Qraw partials (A/B: compress 34.0 -> 32.9 us)
+#endif
 
 #ifdef GRACE_STAMPS   // diagnostic build only: s_memrealtime phase stamps of psgd_w1_pass
 #define W1_STAMP(ws, slot) do { if (threadIdx.x == 0) { if (blockIdx.x == 0 && blockIdx.y == 0) (ws).dbg[slot] = __builtin_amdgcn_s_memrealtime(); \
-    if ((slot) >= 1 && (slot) <= 4) (ws).dbg[8 + 4 * (blockIdx.y * gridDim.x + blockIdx.x) + (slot) - 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+    if ((slot) >= 1 && (slot) <= 4) (ws).dbg[8 + 4 * (blockIdx.y * gridDim.x + blockIdx.x) + (slot) - 1] = __builtin_amdgcn_s_memrealtime(); \
+    if ((slot) == 0 && blockIdx.y * gridDim.x + blockIdx.x < 512) (ws).dbg[1200 + blockIdx.y * gridDim.x + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); } } while (0)
 #define W1_SPAN(ws) do { if (threadIdx.x == 0) { atomicMin((unsigned long long*)&(ws).dbg[6], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
 #define W1_END(ws) do { if (threadIdx.x == 0) { atomicMax((unsigned long long*)&(ws).dbg[7], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
 #define FIN_STAMP(ws, slot) do { if (threadIdx.x == 0 && blockIdx.x == 0) (ws).dbg[1800 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -1212,7 +1222,14 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
       // wave-uniform row base (scalar) + 32-bit lane offset; a row past n re-reads row n - 1
       const int64_t row = lrow + L * d;
       const float* rowp = M + (row < n ? row : n - 1) * m;
+#if GRACE_W1_SPLIT > 0   // A/B knob: issue the first rows, wait for them, then the rest
+      if (d == GRACE_W1_SPLIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#if GRACE_W1_NT
+      v[d] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(rowp + jo));
+#else
       v[d] = *reinterpret_cast<const f32x4v*>(rowp + jo);
+#endif
     }
     if (!qstaged) {   // q rows of the group into LDS (drawn or loaded) while M's loads are in flight
       qstaged = true;
@@ -1406,8 +1423,14 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
         const int qp = threadIdx.x + 1024 * h, jl = qp >> 1;
         if ((int64_t)cg * kW1Cols + jl < m) {
           const int cwl = 64 * (jl >> 8) + ((jl & 255) >> 2), e0 = 4 * (jl & 3) + 2 * (qp & 1);
+#if GRACE_W1_QNT   // A/B knob: non-temporal stores of the Qraw partials
+          typedef double f64x2v __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(f64x2v{qred[1][e0 * 256 + cwl], qred[1][(e0 + 1) * 256 + cwl]},
+                                      reinterpret_cast<f64x2v*>(ws.qpart + gbase + 2 * qp));
+#else
           *reinterpret_cast<double2*>(ws.qpart + gbase + 2 * qp) =
               make_double2(qred[1][e0 * 256 + cwl], qred[1][(e0 + 1) * 256 + cwl]);
+#endif
         }
       }
     }

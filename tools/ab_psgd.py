@@ -11,7 +11,7 @@ import torch
 P_, I64, SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t
 libs = [ctypes.CDLL(p) for p in sys.argv[1:]]
 for L in libs:
-    L.grace_powersgd_w1_compress.argtypes = [P_, I64, I64, P_, ctypes.c_uint64, P_, P_, P_, SZ, P_]
+    L.grace_powersgd_w1_compress.argtypes = [P_, I64, I64, P_, ctypes.c_uint64, P_, P_, P_, SZ, P_, P_]
     L.grace_powersgd_w1_workspace_bytes.restype = SZ
     L.grace_powersgd_w1_workspace_bytes.argtypes = [I64, I64]
 n = m = 4096
@@ -24,7 +24,7 @@ stream = torch.cuda.current_stream().cuda_stream
 outs = []
 for i, L in enumerate(libs):
     rc = L.grace_powersgd_w1_compress(Ms[0].data_ptr(), n, m, None, 7, P.data_ptr(), Q.data_ptr(),
-                                      wss[i].data_ptr(), wss[i].numel(), stream)
+                                      wss[i].data_ptr(), wss[i].numel(), None, stream)
     assert rc == 0, rc
     torch.cuda.synchronize()
     outs.append((P.clone(), Q.clone()))
@@ -36,7 +36,7 @@ for rnd in range(8):
         e0.record()
         for s in range(20):
             L.grace_powersgd_w1_compress(Ms[s % 5].data_ptr(), n, m, None, s, P.data_ptr(), Q.data_ptr(),
-                                         wss[i].data_ptr(), wss[i].numel(), stream)
+                                         wss[i].data_ptr(), wss[i].numel(), None, stream)
         e1.record()
         torch.cuda.synchronize()
         if rnd > 0:

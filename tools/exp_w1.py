@@ -38,7 +38,9 @@ for it in range(12):
     fin = {"fin_prefetch": (f[1] - f[0]) / 100, "fin_gram": (f[2] - f[1]) / 100, "fin_chol": (f[3] - f[2]) / 100,
            "fin_solve": (f[4] - f[3]) / 100, "fin_wg0": (f[4] - f[0]) / 100, "fin_span": (f[11] - f[10]) / 100,
            "gap_pass_fin": (f[10] - d[7]) / 100}
-    rows.append({**fin, "ld_min": ld.min(), "ld_med": float(np.median(ld)), "ld_max": ld.max(),
+    stt = (d[1200:1200 + nwg] - t0) / 100.0   # per-workgroup start
+    rows.append({**fin, "start_med": float(np.median(stt)), "start_max": stt.max(),
+                 "load_dur_med": float(np.median(ld - stt)), "load_dur_max": (ld - stt).max(), "ld_min": ld.min(), "ld_med": float(np.median(ld)), "ld_max": ld.max(),
                  "wait_med": float(np.median(ex)), "wait_max": ex.max(), "end_min": en.min(), "end_max": en.max(),"to_pphase_done": us(0, 1), "exchange_wait": us(1, 2), "to_qraw": us(2, 3), "qraw_to_end": us(3, 4),
                  "wg00_total": us(0, 4), "grid_span": (d[7] - d[6]) / 100.0, "two_kernels_event": e0.elapsed_time(e1) * 1e3})
 print({k: round(statistics.median(r[k] for r in rows[2:]), 2) for k in rows[0]})
