@@ -1513,6 +1513,20 @@ __global__ __launch_bounds__(kW1FinBlock) void psgd_w1_fin(const float* __restri
   const int64_t pper = (n + NB - 1) / NB;
   const int64_t prow_i = (int64_t)b * pper + t;
   const bool pv_ok = t < pper && prow_i < n;
+  // The Gram partials' loads go first: vmcnt is in order, so the Gram sum below waits for them
+  // only, not for the 8 MB of Qraw partials prefetched after them (A/B in the stamps build).
+  // Gram: wave e < 10 sums slot e, lane k taking slabs k, k + 64, ... (loads in flight together),
+  // then a fixed-order butterfly over the lanes
+  const int ge = t >> 6, gk = t & 63;
+  const int NG = 4 * S;   // 4 Gram partials per slab
+  double gv[4];
+  if (ge < 10) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int su = gk + u * kWave;
+      gv[u] = ws.gpart[(int64_t)(su < NG ? su : 0) * 16 + ge];   // clamped to partial 0
+    }
+  }
   const f32x4v pv = *reinterpret_cast<const f32x4v*>(P + (pv_ok ? prow_i : 0) * 4);
   const int col = t >> 6, sl = t & 63;
   double2 pre_lo[4], pre_hi[4];
@@ -1535,26 +1549,22 @@ __global__ __launch_bounds__(kW1FinBlock) void psgd_w1_fin(const float* __restri
     }
   }
   FIN_STAMP(ws, 1);
-  // Gram partials: wave e < 10 sums slot e, lane k taking slabs k, k + 64, ... (loads in flight
-  // together), then a fixed-order butterfly over the lanes
-  {
-    const int e = t >> 6, k = t & 63;
-    if (e < 10) {
-      double g = 0.0;
-      const int NG = 4 * S;   // 4 Gram partials per slab
-      for (int s0 = k; s0 < NG; s0 += 4 * kWave) {
-        double v[4];
+  if (ge < 10) {
+    double g = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int su = s0 + u * kWave;
-          v[u] = ws.gpart[(int64_t)(su < NG ? su : 0) * 16 + e];   // clamped to partial 0
-        }
+    for (int u = 0; u < 4; ++u) g += gk + u * kWave < NG ? gv[u] : 0.0;
+    for (int s0 = gk + 4 * kWave; s0 < NG; s0 += 4 * kWave) {   // S > 64: further rounds
+      double v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g += s0 + u * kWave < NG ? v[u] : 0.0;
+      for (int u = 0; u < 4; ++u) {
+        const int su = s0 + u * kWave;
+        v[u] = ws.gpart[(int64_t)(su < NG ? su : 0) * 16 + ge];
       }
-      g = wave_sum(g);
-      if (k == 0) Gs[e] = g;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g += s0 + u * kWave < NG ? v[u] : 0.0;
     }
+    g = wave_sum(g);
+    if (gk == 0) Gs[ge] = g;
   }
   __syncthreads();
   FIN_STAMP(ws, 2);
