@@ -272,7 +272,18 @@ struct StepArgs {
   int64_t sample_n;    // stratified sample size (<= kSampleMax)
   int64_t stratum;     // n / sample_n
   int64_t idx_base;    // sharded mode: global index of this shard's element 0 (payload indices)
+  // residual-sample carry (grace_topk_residual_step_carry), f32[sample_n + 2]: the bracket writes
+  // the step's t[pos(s)] to rs_out[s] (it computes them anyway), the finalize writes the step's
+  // composite selection threshold (selected <=> comp_key >= T) as a u64 at rs_out + sample_n;
+  // rs_in = the previous step's rs_out for this residual: the next bracket derives r'[pos(s)] from
+  // it instead of reading r (half the sample's random DRAM reads).  Either may be null; both are
+  // only used when kCarryMinStratum <= stratum.
+  const float* rs_in;
+  float* rs_out;
 };
+
+// the carry is for large buckets, where the bracket's random reads cost (stratum >= 256)
+constexpr int64_t kCarryMinStratum = 256;
 
 template <bool HAS_RES>
 __device__ __forceinline__ float compensate(const StepArgs& a, int64_t i) {
@@ -293,6 +304,12 @@ __device__ __forceinline__ float compensate(const StepArgs& a, int64_t i) {
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;
+}
+
+// element index of sample sidx: a hashed offset inside its stratum [sidx * st, sidx * st + st)
+__device__ __forceinline__ int64_t sample_pos(int64_t sidx, uint32_t st) {
+  const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
+  return sidx * (int64_t)st + off;
 }
 
 #ifndef GRACE_SAMPLE_PER
@@ -464,11 +481,23 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   for (int q = 0; q < kBracketRun; ++q) t[q] = 0.f;
   if (valid) {
     if constexpr (kBracketRun == 1) {
-      const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
 #ifdef GRACE_SAMPLE_SEQ   // diagnostic A/B build only: contiguous sample positions
-      t[0] = compensate<HAS_RES>(a, sidx + 0 * off);
+      t[0] = compensate<HAS_RES>(a, sidx);
 #else
-      t[0] = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
+      const int64_t pos = sample_pos(sidx, st);
+      if (HAS_RES && a.rs_in) {
+        // carried t'(pos) of this residual's previous step and that step's selection threshold:
+        // r'(pos) exactly as its main pass + finalize left it, from one random DRAM read (g) per
+        // sample instead of two
+        const float tp = a.rs_in[sidx];
+        const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + a.sample_n);
+        const float gv = a.g[pos];
+        const float rp = comp_key(abs_key(tp), (uint32_t)pos) >= Tp ? tp - tp : tp;
+        t[0] = a.beta * rp + a.gamma * gv;
+      } else {
+        t[0] = compensate<HAS_RES>(a, pos);
+      }
+      if (a.rs_out) a.rs_out[sidx] = t[0];   // this step's t(pos), for the next step's bracket
 #endif
     } else {
       const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32) *
@@ -942,6 +971,11 @@ struct MainTs {
   }
 };
 
+// the step's composite selection threshold into the residual-sample carry (selected <=> comp >= T)
+__device__ __forceinline__ void carry_threshold(const StepArgs& a, uint64_t T) {
+  if (a.rs_out) *reinterpret_cast<uint64_t*>(a.rs_out + a.sample_n) = T;
+}
+
 // the boundary list into LDS (pairwise-ranking case); issued by the last workgroup BEFORE its own
 // deferred scattered writes, so the in-order vmcnt wait for these loads does not also wait for them
 template <int BLOCK>
@@ -973,7 +1007,10 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
                               FinShared<BLOCK>& fs, bool preloaded, uint32_t mid) {
   const uint32_t k = (uint32_t)a.k;
   if (ok) {
-    if (need == 0) return;
+    if (need == 0) {   // exactly k sure elements: selected <=> key > thr_hi
+      if (threadIdx.x == 0) carry_threshold(a, ((uint64_t)w.ctl->thr_hi + 1) << 32);
+      return;
+    }
     const uint32_t pos0 = k - need;
     if (nb <= (uint32_t)kPairCap) {
       // rank by pairwise comparison of unique composites; G adjacent lanes share one entry's
@@ -991,6 +1028,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
         for (int o = 1; o < G; o <<= 1) rank += __shfl_xor(rank, o, 64);
         if (part == 0) {
           const int2 e = fs.s_ent[el];
+          if (rank == need - 1) carry_threshold(a, me);
           if (rank < need) emit<MODE>(a, pos0 + rank, e.x, u2f((uint32_t)e.y));
           else unselect<MODE>(a, e, mid);
         }
@@ -1003,7 +1041,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
       return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
     };
     const uint64_t T = block_select_comp<BLOCK>(src, nb, need, fs.hist, fs.s_w, fs.s_res);
-    if (threadIdx.x == 0) fs.s_pos = 0;
+    if (threadIdx.x == 0) { fs.s_pos = 0; carry_threshold(a, T); }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += BLOCK) {
       const int2 e = ld_agent_i2(bnd + j);
@@ -1021,6 +1059,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
   const MainTs<MODE, AG> f{a.g, a.r, a.out};
   auto src = [f](int64_t i) { return comp_key(abs_key(f(i)), (uint32_t)i); };
   const uint64_t T = block_select_comp<BLOCK>(src, a.n, k, fs.hist, fs.s_w, fs.s_res);
+  if (threadIdx.x == 0) carry_threshold(a, T);
   block_write_selected<MODE, BLOCK>(a, f, a.n, T, 0u, fs.s_w);
 }
 
@@ -1153,6 +1192,7 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     pmask |= dmask << shift;
   }
   const uint32_t T = prefix, need_eq = rem;    // take every key > T and the need_eq lowest-index == T
+  if (need_eq == 0 && fi == 0 && t == 0) carry_threshold(a, ((uint64_t)T + 1) << 32);
   // 2. per-slice counts
   uint32_t ngt = 0, neq = 0;
   for_keys([&](uint32_t key, bool in) {
@@ -1207,6 +1247,7 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
         const uint32_t key = abs_key(v[u]);
         const bool gt = key > T, eq = key == T;
         if (gt || (eq && e_before < need_eq)) {
+          if (eq && e_before == need_eq - 1) carry_threshold(a, comp_key(T, (uint32_t)i));   // the last tie taken
           const uint32_t pos = g_before + min(e_before, need_eq);
           a.vals[pos] = v[u];
           a.idx[pos] = (int32_t)i;
@@ -1463,6 +1504,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
   a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
   a.stratum = a.n / a.sample_n;
+  if (a.stratum < kCarryMinStratum) a.rs_in = a.rs_out = nullptr;   // (grace_topk_carry_size says 0)
   // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
   static_assert(kSmallN >= kHistBins, "bracket grid covers the histogram zeroing");
   // runs of kBracketRun samples only when the sample tiles the bucket into whole runs
@@ -1849,6 +1891,33 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
                 "grace_topk_residual_step: bad arguments");
   GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_residual_step: workspace required");
   StepArgs a{g, residual, beta, gamma, n, k, vals, idx, out};
+  hipStream_t s = as_stream(stream);
+  if (out) {
+    return has_residual ? run_topk<true, kDenseFused>(a, ws, ws_bytes_, s)
+                        : run_topk<false, kDenseFused>(a, ws, ws_bytes_, s);
+  }
+  return has_residual ? run_topk<true, kDenseRes>(a, ws, ws_bytes_, s)
+                      : run_topk<false, kDenseRes>(a, ws, ws_bytes_, s);
+}
+
+int64_t grace_topk_carry_size(int64_t n, int64_t k) {
+  if (n <= kSmallN || k >= n || n >= (int64_t)1 << 31) return 0;   // no sampled bracket on these paths
+  const int64_t sn = n < kSampleMax ? n : kSampleMax;
+  return n / sn >= kCarryMinStratum ? sn + 2 : 0;   // t at the sample positions + the u64 threshold
+}
+
+grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, int32_t has_residual,
+                                              float beta, float gamma, int64_t n, int64_t k, float* vals,
+                                              int32_t* idx, float* out, float* carry, int32_t carry_valid,
+                                              void* ws, size_t ws_bytes_, void* stream) {
+  GRACE_REQUIRE(g && residual && vals && idx && n > 0 && k >= 1 && k <= n && n < (int64_t)1 << 31,
+                "grace_topk_residual_step_carry: bad arguments");
+  GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_residual_step_carry: workspace required");
+  StepArgs a{g, residual, beta, gamma, n, k, vals, idx, out};
+  if (carry && grace_topk_carry_size(n, k) > 0) {
+    a.rs_out = carry;
+    a.rs_in = has_residual && carry_valid ? carry : nullptr;   // read by the bracket, rewritten by main
+  }
   hipStream_t s = as_stream(stream);
   if (out) {
     return has_residual ? run_topk<true, kDenseFused>(a, ws, ws_bytes_, s)

@@ -66,15 +66,18 @@ class TopKCompressor(Compressor):
         if not has:
             res = torch.empty_like(g)
         world = int(communicator.world_size)
+        carry, carry_valid = mem.carry_for(name, res, has, k)
         if world == 1:
             out = torch.empty_like(g)
-            ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out)
+            ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out, carry=carry,
+                                   carry_valid=carry_valid)
             mem.residuals[name] = res
-            if not self.average:
-                return out.view(tensor.shape)
+            mem.carry_written(name, res, carry)
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
-        buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None)
+        buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None, carry=carry,
+                                                carry_valid=carry_valid)
         mem.residuals[name] = res
+        mem.carry_written(name, res, carry)
         divisor = world if self.average else 1
         if n > ops.SORT_PAYLOAD_MAX_N:
             # beyond the index-sorted grouping's range (payload.hip): gather as-is and decode with

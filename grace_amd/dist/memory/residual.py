@@ -1,5 +1,9 @@
 """Residual error feedback (grace_dl/dist/memory/residual.py:4-20) with device-resident
 residual buffers keyed by name, like the reference's ``residuals`` dict."""
+import weakref
+
+import torch
+
 from grace_amd import ops
 from grace_amd.dist import Memory
 
@@ -9,6 +13,25 @@ class ResidualMemory(Memory):
         self.residuals = {}
         self.beta = beta
         self.gamma = gamma
+        self._carries = {}   # name -> (carry, weakref to the residual that wrote it, its _version then)
+
+    def carry_for(self, name, residual, has_residual, k):
+        """The residual-sample carry of the fused top-k step (ops.topk_residual_step): the buffer,
+        and whether it still holds the samples of `residual` as the last step left it (same tensor
+        object, no in-place change since: torch's version counter)."""
+        size = ops.topk_carry_size(residual.numel(), k)
+        if size == 0:
+            return None, False
+        ent = getattr(self, "_carries", {}).get(name)
+        if ent is None or ent[0].numel() != size or ent[0].device != residual.device:
+            return torch.empty(size, dtype=torch.float32, device=residual.device), False
+        return ent[0], bool(has_residual) and ent[1]() is residual and ent[2] == residual._version
+
+    def carry_written(self, name, residual, carry):
+        if carry is not None:
+            if not hasattr(self, "_carries"):
+                self._carries = {}
+            self._carries[name] = (carry, weakref.ref(residual), residual._version)
 
     def compensate(self, tensor, name):
         """t = beta * r + gamma * g; the first step returns the tensor itself (residual.py:10-14)."""
@@ -28,3 +51,4 @@ class ResidualMemory(Memory):
 
     def load_state_dict(self, state):
         self.residuals = {k: v.clone() for k, v in state.items()}
+        self._carries = {}

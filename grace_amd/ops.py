@@ -4,6 +4,7 @@ Every function takes torch tensors that live on the GPU (torch provides device m
 current HIP stream only; all arithmetic runs in libgrace_hip.so), validates dtype / contiguity,
 allocates outputs and launches on ``torch.cuda.current_stream()``.
 """
+import functools
 import math
 
 import torch
@@ -249,14 +250,28 @@ def topk_step_dense(x, k, out=None):
     return buf, vals, idx, out
 
 
-def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payload=None):
+def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payload=None, carry=None,
+                       carry_valid=False):
+    """carry: f32[topk_carry_size(n, k)] kept with `residual` (grace_topk_residual_step_carry);
+    carry_valid: it holds the samples the previous step of this residual wrote."""
     g = dev_f32(g)
     n = g.numel()
     buf, vals, idx = new_payload(k, g.device) if payload is None else payload
     ws = topk_workspace(n, k, g.device)
-    _lib.call("grace_topk_residual_step", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
-              float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
+    if carry is None:
+        _lib.call("grace_topk_residual_step", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
+                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
+    else:
+        _lib.call("grace_topk_residual_step_carry", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
+                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(carry), 1 if carry_valid else 0, _p(ws),
+                  ws.numel(), _stream())
     return buf, vals, idx
+
+
+@functools.lru_cache(maxsize=256)
+def topk_carry_size(n, k):
+    """Length of the residual-sample carry for an (n, k) step, 0 where the step has none."""
+    return int(_lib.query("grace_topk_carry_size", n, k))
 
 
 class MainEvent:
