@@ -1908,10 +1908,12 @@ int64_t grace_topk_carry_size(int64_t n, int64_t k) {
 
 grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, int32_t has_residual,
                                               float beta, float gamma, int64_t n, int64_t k, float* vals,
-                                              int32_t* idx, float* out, float* carry, int32_t carry_valid,
-                                              void* ws, size_t ws_bytes_, void* stream) {
+                                              int32_t* idx, float* out, float* carry, int64_t carry_len,
+                                              int32_t carry_valid, void* ws, size_t ws_bytes_, void* stream) {
   GRACE_REQUIRE(g && residual && vals && idx && n > 0 && k >= 1 && k <= n && n < (int64_t)1 << 31,
                 "grace_topk_residual_step_carry: bad arguments");
+  GRACE_REQUIRE(!carry || carry_len >= grace_topk_carry_size(n, k),
+                "grace_topk_residual_step_carry: carry shorter than grace_topk_carry_size(n, k)");
   GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_residual_step_carry: workspace required");
   StepArgs a{g, residual, beta, gamma, n, k, vals, idx, out};
   if (carry && grace_topk_carry_size(n, k) > 0) {

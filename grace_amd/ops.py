@@ -258,13 +258,15 @@ def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payl
     n = g.numel()
     buf, vals, idx = new_payload(k, g.device) if payload is None else payload
     ws = topk_workspace(n, k, g.device)
+    if carry is not None and (carry.dtype != F32 or not carry.is_contiguous()):
+        raise ValueError("grace_amd: the top-k carry is a contiguous float32 device tensor")
     if carry is None:
         _lib.call("grace_topk_residual_step", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
                   float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
     else:
         _lib.call("grace_topk_residual_step_carry", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
-                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(carry), 1 if carry_valid else 0, _p(ws),
-                  ws.numel(), _stream())
+                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(carry), carry.numel(), 1 if carry_valid else 0,
+                  _p(ws), ws.numel(), _stream())
     return buf, vals, idx
 
 

@@ -137,7 +137,7 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
                                         int32_t* idx, float* out, void* ws, size_t ws_bytes,
                                         void* stream);
 /* grace_topk_residual_step plus a residual-sample carry (same results, bit for bit): `carry`
- * (f32[grace_topk_carry_size(n, k)], owned by the caller next to the residual) receives t at the
+ * (f32[carry_len >= grace_topk_carry_size(n, k)], owned by the caller next to the residual) receives t at the
  * sampled bracket's positions and the step's selection threshold; on the next step of the SAME
  * residual, with carry_valid != 0, the bracket derives r' at those positions from it instead of
  * reading r (half its random DRAM reads; the same sample bit for bit).  A stale carry (the residual
@@ -146,8 +146,8 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
 int64_t grace_topk_carry_size(int64_t n, int64_t k);
 grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, int32_t has_residual,
                                               float beta, float gamma, int64_t n, int64_t k, float* vals,
-                                              int32_t* idx, float* out, float* carry, int32_t carry_valid,
-                                              void* ws, size_t ws_bytes, void* stream);
+                                              int32_t* idx, float* out, float* carry, int64_t carry_len,
+                                              int32_t carry_valid, void* ws, size_t ws_bytes, void* stream);
 /* zeros(n).scatter_(idx, vals)  (topk.py:45-49; threshold.py:25-26; randomk.py:39-40). */
 grace_status_t grace_sparse_decode(const float* vals, const int32_t* idx, int64_t count, float* out,
                                    int64_t n, void* stream);

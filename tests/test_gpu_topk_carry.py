@@ -147,6 +147,16 @@ def test_fused_step_carry_tracks_residual_identity_and_version():
         assert same_bits(_np(mem.residuals["b"]), r_host), step
 
 
+def test_short_carry_refused():
+    from grace_amd import ops
+    from grace_amd._lib import GraceNativeError
+    n = 1 << 25
+    k = O.ratio_k(n, 0.01)
+    g = torch.randn(n, device=DEV)
+    with pytest.raises(GraceNativeError):
+        ops.topk_residual_step(g, torch.empty_like(g), False, 1.0, 1.0, k, carry=torch.empty(1000, device=DEV))
+
+
 def test_carry_size_zero_where_no_bracket():
     from grace_amd import ops
     assert ops.topk_carry_size(1000, 10) == 0            # single-workgroup path
