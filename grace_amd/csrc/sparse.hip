@@ -175,34 +175,48 @@ __global__ __launch_bounds__(kSBlock) void thr_stats_kernel(const float* __restr
 }
 
 // World-1 Allgather(Threshold, Residual|None).step without a payload (threshold.py:12-27,
-// residual.py:10-20, allgather.py:40-45): pass A computes t (beta r + gamma g, or g) into the buffer
-// that becomes the residual and the per-chunk stats of thr_stats_kernel in the same read; the bound
-// kernel picks min(thr, max t); pass B writes out = (|t| >= bound ? 0 + t : 0) and, with memory,
-// r' = t - decode = (selected ? t - t : t) in place.  MODE 0: no memory (t = g, read-only);
-// 1: residual memory, first step (t = g); 2: residual memory.
+// residual.py:10-20, allgather.py:40-45): out = (0 + decompress) / 1 and, with memory,
+// r' = t - decompress, where the selection bound is min(thr, max t) (signed max; a NaN max keeps
+// thr).  Any tensor with an element >= thr has bound = thr, so ONE streaming pass selects at thr
+// speculatively (16 B per element with memory, 8 without) while it reduces max t; the workgroup
+// that arrives last at the per-chunk partials decides whether the speculation held.  If it did not
+// (max t < thr), a fix-up pass recomputes every element at bound = max t: t is recovered exactly
+// from what the first pass wrote (|out| >= thr ? out : r'; without memory g is only read), and the
+// fix-up kernel returns at once when nothing needs fixing.  Two launches and one read of the
+// inputs in the common case, against three launches and t written then re-read before.
+// MODE 0: no memory (t = g, read-only); 1: residual memory, first step (t = g); 2: residual memory.
 typedef float f4s __attribute__((ext_vector_type(4)));
 constexpr int kThrU = 4;   // quads per lane per round (all loads first)
+
+__device__ __forceinline__ void thr_sel(float t, float bound, float& o, float& rr) {
+  const bool sel = fabsf(t) >= bound;
+  o = sel ? 0.f + t : 0.f;
+  rr = sel ? t - t : t;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(kSBlock) void thr_comp_stats_kernel(const float* __restrict__ g, float* r, float beta,
-                                                                float gamma, int64_t n, float thr,
-                                                                ThrPart* __restrict__ part) {
+__global__ __launch_bounds__(kSBlock) void thr_spec_kernel(const float* __restrict__ g, float* __restrict__ r,
+                                                          float beta, float gamma, int64_t n, float thr,
+                                                          float* __restrict__ out, ThrPart* __restrict__ part,
+                                                          uint32_t* __restrict__ meta) {
+  __shared__ float sm[kSBlock / kWave];
+  __shared__ uint32_t sn[kSBlock / kWave];
+  __shared__ uint32_t s_last;
   const int64_t base = (int64_t)blockIdx.x * kThrChunk;
   const int64_t end = min(base + (int64_t)kThrChunk, n);
-  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r)) & 15u) == 0;
+  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r) |
+                     reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   const int64_t qe = vec ? base + ((end - base) & ~(int64_t)3) : base;   // [base, qe) in quads
   float mx = -INFINITY;
-  uint32_t nan = 0, cnt = 0;
-  auto acc = [&](float v) {
-    if (v != v) nan = 1; else mx = fmaxf(mx, v);
-    cnt += fabsf(v) >= thr;
-  };
+  uint32_t nan = 0;
+  auto acc = [&](float v) { if (v != v) nan = 1; else mx = fmaxf(mx, v); };
   for (int64_t e0 = base + 4 * (int64_t)threadIdx.x; e0 < qe; e0 += 4 * (int64_t)kSBlock * kThrU) {
     f4s gv[kThrU], rv[kThrU];
 #pragma unroll
     for (int u = 0; u < kThrU; ++u) {
       const int64_t e = e0 + 4 * (int64_t)u * kSBlock < qe ? e0 + 4 * (int64_t)u * kSBlock : e0;
       gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + e));
-      if (MODE == 2) rv[u] = *reinterpret_cast<const f4s*>(r + e);
+      if (MODE == 2) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(r + e));
     }
 #pragma unroll
     for (int u = 0; u < kThrU; ++u) {
@@ -211,64 +225,89 @@ __global__ __launch_bounds__(kSBlock) void thr_comp_stats_kernel(const float* __
       f4s t = gv[u];
       if (MODE == 2) t = f4s{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
                              beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
-      if (MODE != 0) *reinterpret_cast<f4s*>(r + e) = t;   // plain stores: pass B re-reads t
-      acc(t.x); acc(t.y); acc(t.z); acc(t.w);
+      f4s o, rr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc(t[j]);
+        float oj, rj;
+        thr_sel(t[j], thr, oj, rj);
+        o[j] = oj;
+        rr[j] = rj;
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<f4s*>(out + e));
+      if (MODE != 0) __builtin_nontemporal_store(rr, reinterpret_cast<f4s*>(r + e));
     }
   }
   for (int64_t i = qe + threadIdx.x; i < end; i += kSBlock) {
     const float t = MODE == 2 ? beta * r[i] + gamma * g[i] : g[i];
-    if (MODE != 0) r[i] = t;
     acc(t);
+    float o, rr;
+    thr_sel(t, thr, o, rr);
+    out[i] = o;
+    if (MODE != 0) r[i] = rr;
   }
-  __shared__ float sm[kSBlock / kWave];
-  __shared__ uint32_t sn[kSBlock / kWave], sc[kSBlock / kWave];
+  // the chunk's (max, NaN) partial, write-through; the last workgroup to arrive decides the bound
   mx = wave_max(mx);
-  cnt = wave_sum(cnt);
   nan = __ballot(nan != 0) != 0;
   const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sm[w] = mx; sn[w] = nan; sc[w] = cnt; }
+  if ((threadIdx.x & 63) == 0) { sm[w] = mx; sn[w] = nan; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    ThrPart p{-INFINITY, 0u, 0u, 0u};
-    for (int j = 0; j < kSBlock / kWave; ++j) { p.mx = fmaxf(p.mx, sm[j]); p.nan |= sn[j]; p.cnt += sc[j]; }
-    part[blockIdx.x] = p;
+    float pm = -INFINITY;
+    uint32_t pn = 0;
+    for (int j = 0; j < kSBlock / kWave; ++j) { pm = fmaxf(pm, sm[j]); pn |= sn[j]; }
+    uint32_t* pw = reinterpret_cast<uint32_t*>(&part[blockIdx.x]);
+    __hip_atomic_store(pw, __float_as_uint(pm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pw + 1, pn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = atomicAdd(&meta[4], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  mx = -INFINITY;
+  nan = 0;
+  for (int64_t j = threadIdx.x; j < (int64_t)gridDim.x; j += kSBlock) {
+    const uint32_t* pj = reinterpret_cast<const uint32_t*>(&part[j]);
+    const float m = __uint_as_float(__hip_atomic_load(pj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    nan |= __hip_atomic_load(pj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mx = fmaxf(mx, m);
+  }
+  mx = wave_max(mx);
+  nan = __ballot(nan != 0) != 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) { sm[w] = mx; sn[w] = nan; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float gm = -INFINITY;
+    uint32_t gn = 0;
+    for (int j = 0; j < kSBlock / kWave; ++j) { gm = fmaxf(gm, sm[j]); gn |= sn[j]; }
+    // torch.max propagates NaN; Python min(thr, NaN) returns thr (NaN < thr is False)
+    const bool use_max = !gn && gm < thr;
+    meta[0] = __float_as_uint(use_max ? gm : thr);
+    meta[2] = use_max ? 1u : 0u;   // the speculative pass selected at thr: fix up at max t
+    meta[4] = 0u;                  // ticket left zeroed for the next call
   }
 }
 
-template <bool RES>
-__global__ __launch_bounds__(kSBlock) void thr_step_w1_kernel(float* t, int64_t n, const uint32_t* __restrict__ meta,
-                                                             float* __restrict__ out) {
+// fix-up pass: only when the speculative pass was wrong (max t < thr); returns at once otherwise
+template <int MODE>
+__global__ __launch_bounds__(kSBlock) void thr_fix_kernel(const float* __restrict__ g, float* __restrict__ r,
+                                                         int64_t n, float thr, const uint32_t* __restrict__ meta,
+                                                         float* __restrict__ out) {
+  if (meta[2] == 0u) return;
   const float bound = __uint_as_float(meta[0]);
-  const int64_t stride = (int64_t)gridDim.x * kSBlock;
-  const bool vec = ((reinterpret_cast<uintptr_t>(t) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
-  const int64_t nq = vec ? n >> 2 : 0;
-  for (int64_t q0 = (int64_t)blockIdx.x * kSBlock + threadIdx.x; q0 < nq; q0 += stride * kThrU) {
-    f4s tv[kThrU];
-#pragma unroll
-    for (int u = 0; u < kThrU; ++u) {
-      const int64_t q = q0 + u * stride < nq ? q0 + u * stride : q0;
-      tv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(t) + q);
+  for (int64_t i = (int64_t)blockIdx.x * kSBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kSBlock) {
+    float t;
+    if (MODE == 0) {
+      t = g[i];
+    } else {   // what the speculative pass wrote: out = 0 + t where it selected, r' = t elsewhere
+      const float o = out[i], rv = r[i];
+      t = fabsf(o) >= thr ? o : rv;
     }
-#pragma unroll
-    for (int u = 0; u < kThrU; ++u) {
-      if (q0 + u * stride >= nq) break;
-      f4s o, rr;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = tv[u][j];
-        const bool sel = fabsf(v) >= bound;
-        o[j] = sel ? 0.f + v : 0.f;
-        rr[j] = sel ? v - v : v;
-      }
-      __builtin_nontemporal_store(o, reinterpret_cast<f4s*>(out) + q0 + u * stride);
-      if (RES) __builtin_nontemporal_store(rr, reinterpret_cast<f4s*>(t) + q0 + u * stride);
-    }
-  }
-  for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kSBlock + threadIdx.x; i < n; i += stride) {
-    const float v = t[i];
-    const bool sel = fabsf(v) >= bound;
-    out[i] = sel ? 0.f + v : 0.f;
-    if (RES) t[i] = sel ? v - v : v;
+    float o, rr;
+    thr_sel(t, bound, o, rr);
+    out[i] = o;
+    if (MODE != 0) r[i] = rr;
   }
 }
 
@@ -531,16 +570,23 @@ grace_status_t grace_threshold_step_w1(const float* g, float* residual, int32_t 
   uint32_t* meta = reinterpret_cast<uint32_t*>(p);
   ThrPart* part = reinterpret_cast<ThrPart*>(p + 64);
   uint32_t* offs = reinterpret_cast<uint32_t*>(p + 64 + sizeof(ThrPart) * nch);
+  (void)offs;
   hipStream_t s = as_stream(stream);
-  if (mode == 0) thr_comp_stats_kernel<0><<<(unsigned)nch, kSBlock, 0, s>>>(g, nullptr, beta, gamma, n, thr, part);
-  else if (mode == 1) thr_comp_stats_kernel<1><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, part);
-  else thr_comp_stats_kernel<2><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, part);
-  GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
-  thr_bound_kernel<<<1, 1024, 0, s>>>(part, nch, thr, offs, meta, 1, 0);
-  GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
-  const unsigned grid = stream_grid((n + 3) / 4, kSBlock * kThrU, 4096);
-  if (mode == 0) thr_step_w1_kernel<false><<<grid, kSBlock, 0, s>>>(const_cast<float*>(g), n, meta, out);
-  else thr_step_w1_kernel<true><<<grid, kSBlock, 0, s>>>(residual, n, meta, out);
+  GRACE_REQUIRE(nch < (int64_t)1 << 31, "grace_threshold_step_w1: too many chunks");
+  const unsigned fgrid = stream_grid(n, kSBlock, 1024);
+  if (mode == 0) {
+    thr_spec_kernel<0><<<(unsigned)nch, kSBlock, 0, s>>>(g, nullptr, beta, gamma, n, thr, out, part, meta);
+    GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
+    thr_fix_kernel<0><<<fgrid, kSBlock, 0, s>>>(g, nullptr, n, thr, meta, out);
+  } else if (mode == 1) {
+    thr_spec_kernel<1><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, out, part, meta);
+    GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
+    thr_fix_kernel<1><<<fgrid, kSBlock, 0, s>>>(g, residual, n, thr, meta, out);
+  } else {
+    thr_spec_kernel<2><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, thr, out, part, meta);
+    GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
+    thr_fix_kernel<2><<<fgrid, kSBlock, 0, s>>>(g, residual, n, thr, meta, out);
+  }
   GRACE_CHECK_LAUNCH("grace_threshold_step_w1");
   return GRACE_OK;
 }

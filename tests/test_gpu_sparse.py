@@ -131,6 +131,47 @@ def test_threshold_fused_one_read_step_sequence(n, thr, memory):
             assert same_bits(_np(comm.memory.residuals["w"]), res), s
 
 
+@pytest.mark.parametrize("case", ["nan", "neg_inf_all_negative", "neg_zero", "thr_nonpositive", "big_unaligned"])
+@pytest.mark.parametrize("memory", ["none", "residual"])
+def test_threshold_world1_speculative_pass_special_values(case, memory):
+    """The world-1 step selects at thr in one pass and fixes up at max t only when max t < thr
+    (grace_threshold_step_w1): NaN (bound stays thr), -inf in an all-negative tensor (fix-up path,
+    t recovered from the first pass's out / r'), signed zeros, thresholds <= 0 and a multi-chunk
+    unaligned tensor, two steps each, bit-exact against the oracle sequence."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.threshold import ThresholdCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    from grace_amd.dist.memory.residual import ResidualMemory
+    rng = np.random.default_rng(len(case))
+    n = (1 << 22) + 3 if case == "big_unaligned" else 40000
+    thr = -0.5 if case == "thr_nonpositive" else 1.5
+    comm = Allgather(ThresholdCompressor(thr), ResidualMemory() if memory == "residual" else NoneMemory(), 1)
+    res = None
+    for s in range(2):
+        x = rng.standard_normal(n).astype(np.float32)
+        if case == "nan":
+            x[rng.choice(n, 3, replace=False)] = np.nan
+            x = -np.abs(x) * np.float32(0.1)                 # max < thr, but NaN keeps the bound at thr
+        elif case == "neg_inf_all_negative":
+            x = -np.abs(x) - np.float32(0.25)
+            x[rng.choice(n, 4, replace=False)] = -np.inf
+        elif case == "neg_zero":
+            x[rng.choice(n, 500, replace=False)] = -0.0
+            if s == 1:
+                x = -np.abs(x)
+        elif case == "thr_nonpositive":
+            x = -np.abs(x) - np.float32(1.0)                  # every element < thr <= 0
+            x[rng.choice(n, 7, replace=False)] = -0.0 if s == 0 else -3.0
+        out = _np(comm.step(_t(x), "w"))
+        t = O.residual_compensate(x, res) if memory == "residual" else x
+        ov, oi = O.threshold_select(t, thr)
+        dec = O.sparse_decode(ov, oi, n)
+        assert same_bits(out, (O.python_sum([dec]) / np.float32(1)).astype(np.float32)), (case, s)
+        if memory == "residual":
+            res = O.residual_update(t, dec)
+            assert same_bits(_np(comm.memory.residuals["w"]), res), (case, s)
+
+
 @pytest.mark.parametrize("memory", ["none", "residual"])
 def test_threshold_capacity_exchange_retry_bit_exact(memory):
     """exchange='capacity', overflow='retry': the first step learns the capacity through the counts
