@@ -25,4 +25,5 @@ for wl in ${PMC_WL:-qsgd terngrad powersgd sign256 qsgd_step terngrad_step}; do
   done
   args="$args $wl=gpurun_out/pmc_r03_${wl}_FETCH_SIZE,gpurun_out/pmc_r03_${wl}_WRITE_SIZE"
 done
-python3 tools/pmc_all.py gpurun_out/r03_pmc_secondary.json --last 3 $args
+# first-step variants (no residual yet) are not the steady-state step
+python3 tools/pmc_all.py gpurun_out/r03_pmc_secondary.json --last 3 --exclude "threshold:<1>" --exclude "randomk:<false>" $args
