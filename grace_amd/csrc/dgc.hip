@@ -25,6 +25,7 @@ namespace grace {
 
 constexpr int kDBlock = 256;
 constexpr int kDChunk = 4096;          // elements per compaction chunk
+constexpr int kDChunkW1 = 16384;       // elements per workgroup of the world-1 speculative pass
 constexpr int kDepth = 10;              // dgc.py:26 range(10)
 constexpr int kNodes = (1 << (kDepth + 1)) - 1;   // 2047 thresholds the loop can visit
 constexpr int kTab = 2048;              // sorted table (padded with +inf)
@@ -36,8 +37,11 @@ struct DgcMeta {
   uint32_t thr;       // bits of the final threshold
   uint32_t total;     // selected count at the final threshold
   uint32_t nan0;      // thr0 is NaN
-  uint32_t pad[12];
+  uint32_t fix;       // world-1 fused step: the speculative pass at thr0 was wrong, the gated fix-up runs
+  uint32_t ticket;    // world-1 fused step: arrivals of the speculative pass (left zeroed)
+  uint32_t pad[10];
 };
+static_assert(sizeof(DgcMeta) == 64, "DgcMeta layout");
 
 constexpr int kLutShift = 18;                         // coarse key bins: 1/32 octave
 constexpr int kLut = (0x7F800000 >> kLutShift) + 2;   // every finite / inf key's bin, plus its end
@@ -77,6 +81,12 @@ static size_t dgc_ws_bytes(int64_t n) {
          al256(sizeof(uint16_t) * kLut) + 2 * al256(sizeof(uint32_t) * nch);
 }
 
+// compensate: r = m r + g (r = g first), a = a + r (a = g first); returns a in `acc`
+__device__ __forceinline__ void dgc_comp1(float gv, float& rv, float& av, int has_state, float m) {
+  if (has_state) { rv = m * rv + gv; av = av + rv; } else { rv = gv; av = gv; }
+}
+__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
 // ------------------------------------------------------------------------------------------------
 // sample: |t[idx_j]|, idx from the caller (parity: torch's CPU uniform_(0, numel).long()) or the
 // counter-based generator (uniform integer in [0, numel))
@@ -92,6 +102,29 @@ __global__ __launch_bounds__(kDBlock) void dgc_sample_kernel(const float* __rest
       i = (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
     }
     out[j] = fabsf(t[i]);
+  }
+}
+
+// the same sample of the compensated tensor t = a + (m r + g) (t = g on a name's first step), read
+// from the memory state BEFORE compensation: the world-1 fused step samples without materialising t
+__global__ __launch_bounds__(kDBlock) void dgc_sample_comp_kernel(const float* __restrict__ g,
+                                                                 const float* __restrict__ r,
+                                                                 const float* __restrict__ a, int has_state,
+                                                                 float momentum, int64_t n,
+                                                                 const int64_t* __restrict__ sidx, uint64_t seed,
+                                                                 int64_t ns, float* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * kDBlock + threadIdx.x; j < ns; j += (int64_t)gridDim.x * kDBlock) {
+    int64_t i;
+    if (sidx) {
+      i = sidx[j];
+    } else {
+      const uint64_t h = ((uint64_t)rand32(seed, (uint64_t)j) << 32) | rand32(seed ^ 0xD6E8FEB86659FD93ull, (uint64_t)j);
+      i = (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
+    }
+    const float gv = g[i];
+    float rv = has_state ? r[i] : 0.f, av = has_state ? a[i] : 0.f;
+    dgc_comp1(gv, rv, av, has_state, momentum);
+    out[j] = fabsf(av);
   }
 }
 
@@ -194,7 +227,9 @@ __device__ __forceinline__ int tab_bin_lut(const float* tab, const uint16_t* lut
 }
 
 // one pass: histogram of |t| over the table (elements below the smallest entry skip the search)
+template <bool GATED>
 __global__ __launch_bounds__(kDBlock) void dgc_count_kernel(const float* __restrict__ t, int64_t n, DgcWs w) {
+  if constexpr (GATED) { if (w.meta->fix == 0u) return; }
   __shared__ float tab[kTab];
   __shared__ uint32_t h[kTab + 1];
   __shared__ uint16_t lut[kLut];
@@ -236,7 +271,9 @@ __global__ __launch_bounds__(kDBlock) void dgc_count_kernel(const float* __restr
 
 // replay dgc.py:23-36 on the exact counts (one thread): count(|t| >= x) for a table value x at
 // lower-bound position p is the number of elements whose bin is > p
+template <bool GATED>
 __global__ void dgc_replay_kernel(int64_t n, double ratio, DgcWs w) {
+  if constexpr (GATED) { if (w.meta->fix == 0u) return; }
   __shared__ uint32_t suf[kTab + 2];
   __shared__ float tab[kTab];
   // the histogram and the table into LDS by every lane (the single-thread replay below then reads
@@ -401,17 +438,16 @@ __global__ __launch_bounds__(kDBlock) void dgc_rec_mask_kernel(const uint32_t* _
 // Elementwise memory kernels: a thread owns kDQ quads per round (16-B loads, all issued before use)
 // when every buffer is 16-B aligned; the scalar loop covers the rest.  (One 4-B access per thread
 // per element made the 256 MiB DGC step 1.36 ms.)
-__device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-// compensate: r = m r + g (r = g first), a = a + r (a = g first); returns a in `acc`
-__device__ __forceinline__ void dgc_comp1(float gv, float& rv, float& av, int has_state, float m) {
-  if (has_state) { rv = m * rv + gv; av = av + rv; } else { rv = gv; av = gv; }
-}
-__global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __restrict__ g, float* __restrict__ r,
-                                                                float* __restrict__ a, int has_state,
-                                                                float momentum, int64_t n) {
+// compensate in place (r, a) or, for the world-1 fused step's fix-up, from (r, a) into (ro, ao)
+// (GATED: only when that step's speculative pass flagged meta->fix)
+template <bool GATED>
+__global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __restrict__ g, const float* r,
+                                                                const float* a, int has_state,
+                                                                float momentum, int64_t n, float* ro, float* ao,
+                                                                const DgcMeta* __restrict__ gate) {
+  if constexpr (GATED) { if (gate->fix == 0u) return; }
   const int64_t stride = (int64_t)gridDim.x * kDBlock;
-  const int64_t nq = (al16(g) && al16(r) && al16(a)) ? n >> 2 : 0;
+  const int64_t nq = (al16(g) && al16(r) && al16(a) && al16(ro) && al16(ao)) ? n >> 2 : 0;
   for (int64_t q0 = (int64_t)blockIdx.x * kDBlock + threadIdx.x; q0 < nq; q0 += stride * kDQ) {
     f4d gv[kDQ], rv[kDQ], av[kDQ];
 #pragma unroll
@@ -433,15 +469,119 @@ __global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __
         rv[u][j] = rj;
         av[u][j] = aj;
       }
-      __builtin_nontemporal_store(rv[u], reinterpret_cast<f4d*>(r) + q0 + u * stride);
-      __builtin_nontemporal_store(av[u], reinterpret_cast<f4d*>(a) + q0 + u * stride);
+      __builtin_nontemporal_store(rv[u], reinterpret_cast<f4d*>(ro) + q0 + u * stride);
+      __builtin_nontemporal_store(av[u], reinterpret_cast<f4d*>(ao) + q0 + u * stride);
     }
   }
   for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kDBlock + threadIdx.x; i < n; i += stride) {
     float rv = has_state ? r[i] : 0.f, av = has_state ? a[i] : 0.f;
     dgc_comp1(g[i], rv, av, has_state, momentum);
-    r[i] = rv;
-    a[i] = av;
+    ro[i] = rv;
+    ao[i] = av;
+  }
+}
+
+// World-1 Allgather(DgcCompressor, DgcMemory).step in ONE streaming pass (memory/dgc.py:15-39 with
+// compressor/dgc.py:12-50, allgather.py:40-45): compensate, select at the sampled threshold thr0,
+// mask the memory and write (0 + decompress) / 1, from the old state (g, r, a) into NEW buffers
+// (ro, ao) -- 24 B per element against compensate 20 + threshold count 4 + mask / output 20.  The
+// reference's adjustment loop keeps thr0 whenever count(|t| >= thr0) is within [0.7, 1.3] k (the
+// sampled estimate: almost always), so the pass selects at thr0 speculatively while it counts;
+// the workgroup that arrives last checks the loop's first test on the exact count.  If thr0 does
+// not stand, meta->fix is set and the gated fix-up launches (compensate from the untouched old
+// state, count, replay, mask) redo the step exactly; otherwise they return at once.
+template <bool HAS>
+__global__ __launch_bounds__(kDBlock) void dgc_w1_spec_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                                                             const float* __restrict__ a, float momentum, int64_t n,
+                                                             double ratio, DgcMeta* __restrict__ meta,
+                                                             uint32_t* __restrict__ part, float* __restrict__ ro,
+                                                             float* __restrict__ ao, float* __restrict__ out) {
+  __shared__ uint32_t sc[kDBlock / kWave];
+  __shared__ uint32_t s_last;
+  const float thr = __uint_as_float(meta->thr0);
+  const int64_t base = (int64_t)blockIdx.x * kDChunkW1;
+  const int64_t end = min(base + (int64_t)kDChunkW1, n);
+  const bool vec = al16(g) && al16(r) && al16(a) && al16(ro) && al16(ao) && al16(out);
+  const int64_t qe = vec ? base + ((end - base) & ~(int64_t)3) : base;
+  uint32_t cnt = 0;
+  auto one = [&](float gv, float rv, float av, float& rn, float& an, float& o) {
+    dgc_comp1(gv, rv, av, HAS ? 1 : 0, momentum);   // av = t
+    const bool sel = fabsf(av) >= thr;
+    const float keep = sel ? 0.f : 1.f;
+    cnt += sel;
+    o = sel ? 0.f + av : 0.f;
+    rn = rv * keep;
+    an = av * keep;
+  };
+  for (int64_t e0 = base + 4 * (int64_t)threadIdx.x; e0 < qe; e0 += 4 * (int64_t)kDBlock * kDQ) {
+    f4d gv[kDQ], rv[kDQ], av[kDQ];
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      const int64_t e = e0 + 4 * (int64_t)u * kDBlock < qe ? e0 + 4 * (int64_t)u * kDBlock : e0;
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(g + e));
+      if (HAS) {
+        rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(r + e));
+        av[u] = __builtin_nontemporal_load(reinterpret_cast<const f4d*>(a + e));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kDQ; ++u) {
+      const int64_t e = e0 + 4 * (int64_t)u * kDBlock;
+      if (e >= qe) break;
+      f4d rn, an, o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x, y, z;
+        one(gv[u][j], HAS ? rv[u][j] : 0.f, HAS ? av[u][j] : 0.f, x, y, z);
+        rn[j] = x;
+        an[j] = y;
+        o[j] = z;
+      }
+      __builtin_nontemporal_store(rn, reinterpret_cast<f4d*>(ro + e));
+      __builtin_nontemporal_store(an, reinterpret_cast<f4d*>(ao + e));
+      __builtin_nontemporal_store(o, reinterpret_cast<f4d*>(out + e));
+    }
+  }
+  for (int64_t i = qe + threadIdx.x; i < end; i += kDBlock) {
+    float x, y, z;
+    one(g[i], HAS ? r[i] : 0.f, HAS ? a[i] : 0.f, x, y, z);
+    ro[i] = x;
+    ao[i] = y;
+    out[i] = z;
+  }
+  // the chunk's count, write-through; the last workgroup to arrive decides whether thr0 stands
+  cnt = wave_sum(cnt);
+  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int j = 0; j < kDBlock / kWave; ++j) c += sc[j];
+    __hip_atomic_store(&part[blockIdx.x], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = atomicAdd(&meta->ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  uint32_t tot = 0;
+  for (int64_t j = threadIdx.x; j < (int64_t)gridDim.x; j += kDBlock)
+    tot += __hip_atomic_load(&part[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tot = wave_sum(tot);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sel = 0;
+    for (int j = 0; j < kDBlock / kWave; ++j) sel += sc[j];
+    // dgc_replay_kernel's first test: the loop breaks at once iff the count is within the bounds
+    const float hi = (float)(1.3 * (double)n * ratio);
+    const float lo = (float)(0.7 * (double)n * ratio);
+    const bool stands = !((float)sel > hi) && !((float)sel < lo);
+    meta->fix = stands ? 0u : 1u;
+    if (stands) {
+      meta->thr = meta->thr0;
+      meta->total = sel;
+    }
+    meta->ticket = 0u;
   }
 }
 
@@ -449,9 +589,10 @@ __global__ __launch_bounds__(kDBlock) void dgc_compensate_kernel(const float* __
 // (t is the compensated tensor the mask came from; it may alias a).  OUT: the world-1 Allgather
 // result in the same pass, out = 0 + t where selected and 0 elsewhere -- (0 + decompress) / 1
 // of the payload grace_dgc_write would have produced (dgc.py:45-50, allgather.py:40-45).
-template <bool OUT>
+template <bool OUT, bool GATED = false>
 __global__ __launch_bounds__(kDBlock) void dgc_mask_kernel(const float* t, float* r, float* a, int64_t n,
                                                           const DgcMeta* __restrict__ meta, float* out) {
+  if constexpr (GATED) { if (meta->fix == 0u) return; }
   const float thr = __uint_as_float(meta->thr);
   const bool alias = t == a;
   const int64_t stride = (int64_t)gridDim.x * kDBlock;
@@ -554,9 +695,9 @@ grace_status_t grace_dgc_threshold(const float* t, int64_t n, const float* top_v
   const int64_t nch = (n + kDChunk - 1) / kDChunk;
   dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);
   GRACE_CHECK_LAUNCH("grace_dgc_threshold");
-  dgc_count_kernel<<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
+  dgc_count_kernel<false><<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
   GRACE_CHECK_LAUNCH("grace_dgc_threshold");
-  dgc_replay_kernel<<<1, 64, 0, s>>>(n, ratio, w);
+  dgc_replay_kernel<false><<<1, 64, 0, s>>>(n, ratio, w);
   GRACE_CHECK_LAUNCH("grace_dgc_threshold");
   dgc_chunk_kernel<<<(unsigned)nch, kDBlock, 0, s>>>(t, n, w);
   GRACE_CHECK_LAUNCH("grace_dgc_threshold");
@@ -599,8 +740,8 @@ grace_status_t grace_dgc_compensate(const float* g, float* residual, float* accu
                                     float momentum, int64_t n, void* stream) {
   GRACE_REQUIRE(g && residual && accum && n >= 0, "grace_dgc_compensate: bad arguments");
   if (n == 0) return GRACE_OK;
-  dgc_compensate_kernel<<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(g, residual, accum,
-                                                                                         has_state, momentum, n);
+  dgc_compensate_kernel<false><<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(
+      g, residual, accum, has_state, momentum, n, residual, accum, nullptr);
   GRACE_CHECK_LAUNCH("grace_dgc_compensate");
   return GRACE_OK;
 }
@@ -622,9 +763,9 @@ grace_status_t grace_dgc_select(const float* t, int64_t n, const float* top_vals
   DgcWs w = dgc_carve(ws, n);
   dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);
   GRACE_CHECK_LAUNCH("grace_dgc_select");
-  dgc_count_kernel<<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
+  dgc_count_kernel<false><<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(t, n, w);
   GRACE_CHECK_LAUNCH("grace_dgc_select");
-  dgc_replay_kernel<<<1, 64, 0, s>>>(n, ratio, w);
+  dgc_replay_kernel<false><<<1, 64, 0, s>>>(n, ratio, w);
   GRACE_CHECK_LAUNCH("grace_dgc_select");
   return GRACE_OK;
 }
@@ -636,6 +777,57 @@ grace_status_t grace_dgc_step_w1(const float* t, float* residual, float* accum, 
   dgc_mask_kernel<true><<<stream_grid((n + 3) / 4, kDBlock * kDQ, 4096), kDBlock, 0, as_stream(stream)>>>(
       t, residual, accum, n, reinterpret_cast<const DgcMeta*>(ws), out);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1");
+  return GRACE_OK;
+}
+
+grace_status_t grace_dgc_sample_comp(const float* g, const float* residual, const float* accum, int32_t has_state,
+                                     float momentum, int64_t n, const int64_t* sample_idx, uint64_t seed, int64_t ns,
+                                     float* sample_abs, void* stream) {
+  GRACE_REQUIRE(g && sample_abs && n >= 1 && ns >= 1 && (!has_state || (residual && accum)),
+                "grace_dgc_sample_comp: bad arguments");
+  dgc_sample_comp_kernel<<<stream_grid(ns, kDBlock, 1024), kDBlock, 0, as_stream(stream)>>>(
+      g, residual, accum, has_state, momentum, n, sample_idx, seed, ns, sample_abs);
+  GRACE_CHECK_LAUNCH("grace_dgc_sample_comp");
+  return GRACE_OK;
+}
+
+size_t grace_dgc_step_w1_fused_workspace_bytes(int64_t n) {
+  return dgc_ws_bytes(n < 1 ? 1 : n) + 256 + sizeof(uint32_t) * (size_t)((n + kDChunkW1 - 1) / kDChunkW1);
+}
+
+grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, const float* accum, int32_t has_state,
+                                       float momentum, int64_t n, const float* top_vals, int64_t ks, double ratio,
+                                       void* ws, float* residual_out, float* accum_out, float* out, void* stream) {
+  GRACE_REQUIRE(g && top_vals && ws && residual_out && accum_out && out && n >= 1 && ks >= 1 &&
+                    (!has_state || (residual && accum)) && n < ((int64_t)1 << 40),
+                "grace_dgc_step_w1_fused: bad arguments");
+  GRACE_REQUIRE(residual_out != residual && accum_out != accum && residual_out != accum_out,
+                "grace_dgc_step_w1_fused: the new state must not alias the old");
+  hipStream_t s = as_stream(stream);
+  DgcWs w = dgc_carve(ws, n);
+  uint32_t* part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + dgc_ws_bytes(n) + 256);
+  const int64_t nch = (n + kDChunkW1 - 1) / kDChunkW1;
+  GRACE_REQUIRE(nch < ((int64_t)1 << 31), "grace_dgc_step_w1_fused: too many chunks");
+  dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);   // thr0, the adjustment table, zeroed counts
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  if (has_state)
+    dgc_w1_spec_kernel<true><<<(unsigned)nch, kDBlock, 0, s>>>(g, residual, accum, momentum, n, ratio, w.meta, part,
+                                                             residual_out, accum_out, out);
+  else
+    dgc_w1_spec_kernel<false><<<(unsigned)nch, kDBlock, 0, s>>>(g, residual, accum, momentum, n, ratio, w.meta, part,
+                                                              residual_out, accum_out, out);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  // gated fix-up (returns at once unless thr0 did not stand): the reference's full adjustment loop
+  const unsigned sg = stream_grid((n + 3) / 4, kDBlock * kDQ, 4096);
+  dgc_compensate_kernel<true><<<sg, kDBlock, 0, s>>>(g, residual, accum, has_state, momentum, n, residual_out,
+                                                     accum_out, w.meta);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  dgc_count_kernel<true><<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(accum_out, n, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  dgc_replay_kernel<true><<<1, 64, 0, s>>>(n, ratio, w);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  dgc_mask_kernel<true, true><<<sg, kDBlock, 0, s>>>(accum_out, residual_out, accum_out, n, w.meta, out);
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
   return GRACE_OK;
 }
 

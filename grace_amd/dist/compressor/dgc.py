@@ -85,6 +85,17 @@ class DgcCompressor(Compressor):
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
             return None
         W = int(communicator.world_size)
+        if W == 1 and not mem.gradient_clipping:
+            # one streaming pass from the old state into new buffers (the reference rebinds new
+            # tensors too, memory/dgc.py:36-39): compensate + select + mask + (0 + decompress) / 1
+            g = ops.dev_f32(tensor)
+            res, acc = mem.residuals.get(name), mem.gradients.get(name)
+            has = res is not None and acc is not None and res.numel() == g.numel() and acc.numel() == g.numel()
+            sidx, seed = self._sampling(g, name)
+            out, r_new, a_new = ops.dgc_step_w1_fused(g, res if has else None, acc if has else None, has,
+                                                      mem.momentum, self.compress_ratio, sample_idx=sidx, seed=seed)
+            mem.residuals[name], mem.gradients[name] = r_new, a_new
+            return out.view(tensor.shape)
         t = ops.dev_f32(mem.compensate(tensor, name))
         sidx, seed = self._sampling(t, name)
         if W == 1:

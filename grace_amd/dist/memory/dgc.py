@@ -2,8 +2,9 @@
 
 compensate: (optional clipping) r = momentum r + g, a = a + r, returns a (first step: r = a = g);
 update: r = r * ~mask, a = a * ~mask with mask = |t| >= the compressor's final threshold.
-The residual / accumulator buffers are owned by the memory and updated in place (the reference
-rebinds new tensors; the values are identical).  gradient_clipping=True implements the documented
+The residual / accumulator buffers are owned by the memory and updated in place by compensate /
+update; the world-1 fused step (DgcCompressor.fused_step) writes the new state into new buffers
+and rebinds them, as the reference rebinds new tensors (the values are identical either way).  gradient_clipping=True implements the documented
 intent -- clamp to sqrt(all_reduce(sum(g*g)) / world_size) -- where the reference itself raises a
 TypeError (``dist.all_reduce`` returns None, memory/dgc.py:17-18).
 """

@@ -965,6 +965,27 @@ def dgc_step_w1(t, residual, accum, ws, out=None):
     return out
 
 
+def dgc_step_w1_fused(g, residual, accum, has_state, momentum, ratio, sample_idx=None, seed=0):
+    """World-1 Allgather(DGC, DgcMemory).step from the OLD memory state (grace_dgc_sample_comp +
+    grace_dgc_step_w1_fused): returns (out, new residual, new accumulator); the old buffers are only
+    read.  Same values as compensate + select + step_w1."""
+    g = dev_f32(g)
+    n = g.numel()
+    ns = max(1, int(n * 0.01))
+    ks = max(1, int(n * ratio * 0.01))
+    sample = torch.empty(ns, dtype=F32, device=g.device)
+    _lib.call("grace_dgc_sample_comp", _p(g), _p(residual) if has_state else None,
+              _p(accum) if has_state else None, 1 if has_state else 0, float(momentum), n, _opt(sample_idx),
+              int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
+    _, top, _ = topk_compress(sample, min(ks, ns))
+    ws = workspace("dgc_w1", _lib.query("grace_dgc_step_w1_fused_workspace_bytes", n), g.device)
+    r_new, a_new, out = torch.empty_like(g), torch.empty_like(g), torch.empty_like(g)
+    _lib.call("grace_dgc_step_w1_fused", _p(g), _p(residual) if has_state else None,
+              _p(accum) if has_state else None, 1 if has_state else 0, float(momentum), n, _p(top), min(ks, ns),
+              float(ratio), _p(ws), _p(r_new), _p(a_new), _p(out), _stream())
+    return out, r_new, a_new
+
+
 def dgc_compensate(g, residual, accum, has_state, momentum):
     _lib.call("grace_dgc_compensate", _p(dev_f32(g)), _p(residual), _p(accum), 1 if has_state else 0,
               float(momentum), g.numel(), _stream())

@@ -452,6 +452,23 @@ grace_status_t grace_dgc_select(const float* t, int64_t n, const float* top_vals
  * pass; the payload and its host-read size are never materialised.  t may alias accum. */
 grace_status_t grace_dgc_step_w1(const float* t, float* residual, float* accum, int64_t n, const void* ws, float* out,
                                  void* stream);
+/* World-1 Allgather(DgcCompressor, DgcMemory(momentum, clipping off)).step from the OLD memory
+ * state in one streaming pass (compressor/dgc.py:12-50, memory/dgc.py:15-39, allgather.py:40-45):
+ * grace_dgc_sample_comp samples |t| of t = a + (m r + g) (t = g when has_state == 0) without
+ * materialising t; with top_vals = the ks largest sampled magnitudes, grace_dgc_step_w1_fused
+ * writes the new residual / accumulator (residual_out, accum_out: new buffers, the old state is
+ * only read) and out = (0 + decompress) / 1.  It selects at the sampled threshold and checks the
+ * reference's adjustment loop on the exact count; when that threshold does not stand, gated
+ * launches redo the step with the full loop (same results as grace_dgc_compensate +
+ * grace_dgc_select + grace_dgc_step_w1, bit for bit).  ws: grace_dgc_step_w1_fused_workspace_bytes,
+ * zeroed once at allocation. */
+grace_status_t grace_dgc_sample_comp(const float* g, const float* residual, const float* accum, int32_t has_state,
+                                     float momentum, int64_t n, const int64_t* sample_idx, uint64_t seed, int64_t ns,
+                                     float* sample_abs, void* stream);
+size_t grace_dgc_step_w1_fused_workspace_bytes(int64_t n);
+grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, const float* accum, int32_t has_state,
+                                       float momentum, int64_t n, const float* top_vals, int64_t ks, double ratio,
+                                       void* ws, float* residual_out, float* accum_out, float* out, void* stream);
 /* gradient clipping (memory/dgc.py:16-19): s = sum(x*x) (f64 accumulate) into out_dev; after the
  * caller's all_reduce of s: out = clamp(x, -c, c), c = sqrt(s / world) */
 size_t grace_sumsq_workspace_bytes(void);

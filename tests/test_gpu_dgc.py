@@ -129,3 +129,47 @@ def test_dgc_world1_fused_step_equals_unfused(n, rng):
         assert same_bits(fo[s], uo[s]), s
     assert same_bits(fr, ur) and same_bits(fa, ua)
     assert np.count_nonzero(fo[-1]) > 0
+
+
+def _unfused_w1(g, r, a, has, m, ratio, sidx):
+    """compensate (in place, on copies) + select + step_w1: the multi-pass world-1 step."""
+    r, a = (r.clone(), a.clone()) if has else (torch.empty_like(g), torch.empty_like(g))
+    ops.dgc_compensate(g, r, a, has, m)
+    ws = ops.dgc_select(a, ratio, sample_idx=sidx)
+    out = ops.dgc_step_w1(a, r, a, ws)
+    return out, r, a
+
+
+@pytest.mark.parametrize("case", ["normal", "sample_top", "sample_nan", "specials", "unaligned"])
+def test_dgc_w1_speculative_pass_equals_multipass(case):
+    """grace_dgc_step_w1_fused selects at the sampled threshold in one pass and redoes the step
+    through the gated full adjustment loop when that threshold does not stand: a sample of the
+    largest element (count far below 0.7 k: the loop runs), a NaN sample, inf / NaN / -0 in the
+    gradient, an unaligned length; three steps with the momentum state carried, out and both
+    memory states bit-identical to the multi-pass step."""
+    n = (1 << 20) + (3 if case == "unaligned" else 0)
+    ratio, m = 0.01, 0.9
+    rng = np.random.default_rng(len(case))
+    r = a = None
+    for s in range(3):
+        g0 = rng.standard_normal(n).astype(np.float32)
+        if case == "specials":
+            g0[rng.choice(n, 5, replace=False)] = np.inf
+            g0[rng.choice(n, 5, replace=False)] = -np.inf
+            g0[rng.choice(n, 3, replace=False)] = np.nan
+            g0[rng.choice(n, 50, replace=False)] = -0.0
+        g = _t(g0)
+        ns = max(1, int(n * 0.01))
+        sidx = rng.integers(0, n, ns).astype(np.int64)
+        if case == "sample_top":
+            sidx[:] = int(np.argmax(np.abs(g0)))
+        if case == "sample_nan":
+            g0[7] = np.nan
+            g = _t(g0)
+            sidx[:] = 7
+        has = s > 0
+        eo, er, ea = _unfused_w1(g, r, a, has, m, ratio, _t(sidx))
+        out, r_new, a_new = ops.dgc_step_w1_fused(g, r, a, has, m, ratio, sample_idx=_t(sidx))
+        assert same_bits(_np(out), _np(eo)), (case, s)
+        assert same_bits(_np(r_new), _np(er)) and same_bits(_np(a_new), _np(ea)), (case, s)
+        r, a = r_new, a_new
