@@ -132,7 +132,9 @@ __global__ __launch_bounds__(kDBlock) void dgc_sample_comp_kernel(const float* _
 // table: thr0 = min of the top-k_s sampled magnitudes (torch.min propagates NaN), then every
 // threshold of the adjustment tree (node = path bits from the root, 1 -> *1.3, 0 -> *0.7, the
 // multiplications in loop order), bitonic-sorted ascending; the counts are zeroed.
+template <bool GATED = false>
 __global__ __launch_bounds__(1024) void dgc_table_kernel(const float* __restrict__ topv, int64_t ks, DgcWs w) {
+  if constexpr (GATED) { if (w.meta->fix == 0u) return; }
   __shared__ float s[kTab];
   __shared__ float s_min;
   __shared__ uint32_t s_nan;
@@ -200,6 +202,31 @@ __global__ __launch_bounds__(1024) void dgc_table_kernel(const float* __restrict
       if (__float_as_uint(s[mid]) < kb) lo = mid + 1; else hi = mid;
     }
     w.lut[b] = (uint16_t)lo;
+  }
+}
+
+// thr0 alone (the world-1 fused step needs the table only on its fix-up path): min of the top-k_s
+// sampled magnitudes, NaN if any is NaN -- dgc_table_kernel's reduction
+__global__ __launch_bounds__(1024) void dgc_thr0_kernel(const float* __restrict__ topv, int64_t ks, DgcWs w) {
+  __shared__ float sm[1024 / kWave];
+  __shared__ uint32_t sn[1024 / kWave];
+  const int t = threadIdx.x;
+  float mn = INFINITY;
+  uint32_t nan = 0;
+  for (int64_t j = t; j < ks; j += 1024) {
+    const float v = topv[j];
+    if (v != v) nan = 1; else mn = fminf(mn, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+  nan = __ballot(nan != 0) != 0;
+  if ((t & 63) == 0) { sm[t >> 6] = mn; sn[t >> 6] = nan; }
+  __syncthreads();
+  if (t == 0) {
+    float m = INFINITY;
+    uint32_t nn = 0;
+    for (int j = 0; j < 1024 / kWave; ++j) { m = fminf(m, sm[j]); nn |= sn[j]; }
+    w.meta->thr0 = nn ? 0x7FC00000u : __float_as_uint(m);
+    w.meta->nan0 = nn;
   }
 }
 
@@ -808,7 +835,7 @@ grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, co
   uint32_t* part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + dgc_ws_bytes(n) + 256);
   const int64_t nch = (n + kDChunkW1 - 1) / kDChunkW1;
   GRACE_REQUIRE(nch < ((int64_t)1 << 31), "grace_dgc_step_w1_fused: too many chunks");
-  dgc_table_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);   // thr0, the adjustment table, zeroed counts
+  dgc_thr0_kernel<<<1, 1024, 0, s>>>(top_vals, ks, w);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
   if (has_state)
     dgc_w1_spec_kernel<true><<<(unsigned)nch, kDBlock, 0, s>>>(g, residual, accum, momentum, n, ratio, w.meta, part,
@@ -817,12 +844,15 @@ grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, co
     dgc_w1_spec_kernel<false><<<(unsigned)nch, kDBlock, 0, s>>>(g, residual, accum, momentum, n, ratio, w.meta, part,
                                                               residual_out, accum_out, out);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
-  // gated fix-up (returns at once unless thr0 did not stand): the reference's full adjustment loop
-  const unsigned sg = stream_grid((n + 3) / 4, kDBlock * kDQ, 4096);
+  // gated fix-up (returns at once unless thr0 did not stand): the reference's full adjustment loop,
+  // on grids small enough that the no-op launches cost little
+  dgc_table_kernel<true><<<1, 1024, 0, s>>>(top_vals, ks, w);   // the adjustment table, zeroed counts
+  GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
+  const unsigned sg = stream_grid((n + 3) / 4, kDBlock * kDQ, 1024);
   dgc_compensate_kernel<true><<<sg, kDBlock, 0, s>>>(g, residual, accum, has_state, momentum, n, residual_out,
                                                      accum_out, w.meta);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
-  dgc_count_kernel<true><<<stream_grid((n + 3) / 4, kDBlock, 2048), kDBlock, 0, s>>>(accum_out, n, w);
+  dgc_count_kernel<true><<<stream_grid((n + 3) / 4, kDBlock, 1024), kDBlock, 0, s>>>(accum_out, n, w);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
   dgc_replay_kernel<true><<<1, 64, 0, s>>>(n, ratio, w);
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");

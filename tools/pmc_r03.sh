@@ -26,4 +26,4 @@ for wl in ${PMC_WL:-qsgd terngrad powersgd sign256 qsgd_step terngrad_step}; do
   args="$args $wl=gpurun_out/pmc_r03_${wl}_FETCH_SIZE,gpurun_out/pmc_r03_${wl}_WRITE_SIZE"
 done
 # first-step variants (no residual yet) are not the steady-state step
-python3 tools/pmc_all.py gpurun_out/r03_pmc_secondary.json --last 3 --exclude "threshold:<1>" --exclude "randomk:<false>" $args
+python3 tools/pmc_all.py gpurun_out/r03_pmc_secondary.json --last 3 --exclude "threshold:<1>" --exclude "randomk:<false>" --exclude "dgc:spec_kernel<false>" $args
