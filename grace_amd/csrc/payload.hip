@@ -9,7 +9,9 @@
 // finds every rank's sub-range of that chunk from a boundary table, accumulates the ranks in
 // order in LDS -- ((0 + d0) + d1) + ... exactly as Python's sum -- divides, and writes the chunk
 // densely, which also replaces the zero-fill.  Each rank's chunk end offsets (a by-product of the
-// grouping) travel with its payload, so the receiver needs no pass to find the sub-ranges.
+// grouping) travel with its payload, so the receiver needs no pass to find the sub-ranges.  The
+// grouped payload carries each entry's offset inside its chunk as a u16 (13 bits) instead of the
+// int32 index: 6 B per entry on the wire instead of 8.
 
 #include "common.h"
 
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
                                                                    const int32_t* __restrict__ idx, int64_t k,
                                                                    int64_t nchunks, uint32_t* __restrict__ cursor,
                                                                    float* __restrict__ vals_out,
-                                                                   int32_t* __restrict__ idx_out) {
+                                                                   uint16_t* __restrict__ off_out) {
   extern __shared__ uint32_t h[];
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
   __syncthreads();
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
     if (ii[e] < 0) continue;
     const uint32_t pos = atomicAdd(&h[ii[e] >> kPChunkLog], 1u);
     vals_out[pos] = vv[e];
-    idx_out[pos] = ii[e];
+    off_out[pos] = (uint16_t)(ii[e] & (kPChunk - 1));   // the offset inside its chunk (13 bits)
   }
 }
 
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
 constexpr int kRankBatch = 8;
 constexpr int kMaxRanks = 1024;
 __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* __restrict__ vals,
-                                                                  const int32_t* __restrict__ idx,
+                                                                  const uint16_t* __restrict__ off,
                                                                   const int32_t* __restrict__ ends, int64_t stride,
                                                                   int world, float divisor,
                                                                   float* __restrict__ out, int64_t n) {
@@ -175,9 +177,9 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
       const int32_t p = s_b[2 * w] + t;
       const bool ok = w0 + q < world && p < s_b[2 * w + 1];
       const int64_t pc = (int64_t)w * stride + (ok ? p : 0);
-      const int32_t li = idx[pc];
+      const int32_t li = off[2 * (int64_t)w * stride + (ok ? p : 0)];   // rank w's u16 offsets: 2 w stride on
       v[q] = vals[pc];
-      l[q] = ok ? (int32_t)(li - c0) : -1;
+      l[q] = ok ? li : -1;
     }
 #pragma unroll
     for (int q = 0; q < kRankBatch; ++q) {
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
       if (l[q] >= 0) tile[l[q]] = tile[l[q]] + v[q];
       const int32_t s1 = s_b[2 * w + 1];
       for (int32_t p = s_b[2 * w] + kPBlock + t; p < s1; p += kPBlock) {   // rare: > 256 entries
-        const int32_t lp = (int32_t)(idx[(int64_t)w * stride + p] - c0);
+        const int32_t lp = off[2 * (int64_t)w * stride + p];
         tile[lp] = tile[lp] + vals[(int64_t)w * stride + p];
       }
       __syncthreads();
@@ -220,9 +222,9 @@ size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is
 // unspecified -- the aggregate does not depend on it); ends_out[c] = end of chunk c's entries
 grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t k, int64_t n, float* vals_out,
-                                  int32_t* idx_out, uint32_t* ends_out, void* ws, size_t ws_bytes, void* stream) {
+                                  uint16_t* off_out, uint32_t* ends_out, void* ws, size_t ws_bytes, void* stream) {
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  GRACE_REQUIRE(vals && idx && vals_out && idx_out && ends_out && ws && k >= 0 && k < ((int64_t)1 << 31) &&
+  GRACE_REQUIRE(vals && idx && vals_out && off_out && ends_out && ws && k >= 0 && k < ((int64_t)1 << 31) &&
                     n >= 1 && nchunks <= kMaxGroupChunks && ws_bytes >= grace_sort_payload_workspace_bytes(k, n),
                 "grace_sort_payload: bad arguments (n <= 2^28)");
   hipStream_t s = as_stream(stream);
@@ -235,20 +237,20 @@ grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t
   const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
   group_hist_kernel<<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
   GRACE_CHECK_LAUNCH("grace_sort_payload");
-  group_scatter_kernel<<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, idx_out);
+  group_scatter_kernel<<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out);
   GRACE_CHECK_LAUNCH("grace_sort_payload");
   return GRACE_OK;
 }
 
-grace_status_t grace_sparse_aggregate_sorted(const float* vals, const int32_t* idx, const uint32_t* ends,
+grace_status_t grace_sparse_aggregate_sorted(const float* vals, const uint16_t* off, const uint32_t* ends,
                                              int64_t stride, int32_t world, float divisor, float* out, int64_t n,
                                              void* stream) {
-  GRACE_REQUIRE(vals && idx && ends && out && world >= 1 && world <= kMaxRanks && n >= 1 &&
+  GRACE_REQUIRE(vals && off && ends && out && world >= 1 && world <= kMaxRanks && n >= 1 &&
                     (n + kPChunk - 1) / kPChunk <= kMaxGroupChunks,
                 "grace_sparse_aggregate_sorted: bad arguments (1 <= world <= 1024, n <= 2^28)");
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
   chunk_accumulate_kernel<<<(unsigned)nchunks, kPBlock, 0, as_stream(stream)>>>(
-      vals, idx, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
+      vals, off, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
   GRACE_CHECK_LAUNCH("grace_sparse_aggregate_sorted");
   return GRACE_OK;
 }

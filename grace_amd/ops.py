@@ -372,18 +372,23 @@ def sparse_aggregate_capped(recs, cap, world, n, divisor, stat):
 SORT_PAYLOAD_MAX_N = 1 << 28   # payload.hip kMaxGroupChunks * chunk: largest bucket sort_payload groups
 
 
+def _off_words(k):
+    return (int(k) + 1) // 2     # u16 chunk offsets of k entries, in 4-B words
+
+
 def sorted_payload_len(k, n):
-    """f32 words of a chunk-grouped payload: [vals f32[k] | idx i32[k] | chunk ends u32[ceil(n/8192)]]."""
-    return 2 * int(k) + (int(n) + 8191) // 8192
+    """4-B words of a chunk-grouped payload: [vals f32[k] | offsets u16[k] (padded to a word) |
+    chunk ends u32[ceil(n/8192)]] -- 6 B per entry on the wire instead of the packed payload's 8."""
+    return int(k) + _off_words(k) + (int(n) + 8191) // 8192
 
 
 def sort_payload(buf, k, n):
     """Packed payload [vals f32[k] | idx i32[k]] -> a new chunk-grouped payload
-    [vals | idx | chunk end offsets] (sorted_payload_len(k, n) words), ready for the exchange."""
+    [vals | u16 offsets inside the chunk | chunk end offsets] (sorted_payload_len(k, n) words)."""
     out = torch.empty(sorted_payload_len(k, n), dtype=F32, device=buf.device)
     ws = workspace("sortpay", _lib.query("grace_sort_payload_workspace_bytes", k, n), buf.device)
     _lib.call("grace_sort_payload", _p(buf), _p(buf[k:]), int(k), int(n), _p(out), _p(out[k:]),
-              _p(out[2 * k:]), _p(ws), ws.numel(), _stream())
+              _p(out[k + _off_words(k):]), _p(ws), ws.numel(), _stream())
     return out
 
 
@@ -391,8 +396,8 @@ def sparse_aggregate_sorted(gathered, k, world, n, divisor):
     """Rank-ordered aggregate of W chunk-grouped payloads (rank-major, stride sorted_payload_len)."""
     out = torch.empty(n, dtype=F32, device=gathered.device)
     stride = sorted_payload_len(k, n)
-    _lib.call("grace_sparse_aggregate_sorted", _p(gathered), _p(gathered[k:]), _p(gathered[2 * k:]), stride,
-              int(world), float(divisor), _p(out), int(n), _stream())
+    _lib.call("grace_sparse_aggregate_sorted", _p(gathered), _p(gathered[k:]), _p(gathered[k + _off_words(k):]),
+              stride, int(world), float(divisor), _p(out), int(n), _stream())
     return out
 
 

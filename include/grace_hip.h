@@ -161,12 +161,14 @@ grace_status_t grace_sparse_decode_i64(const float* vals, const int64_t* idx, in
  * by chunk, n <= 2^28; ws = grace_sort_payload_workspace_bytes; ends_out[ceil(n / 8192)] receives
  * the end offset of every chunk's entries and is sent with the payload), then
  * grace_sparse_aggregate_sorted writes out = (((0 + d_0) + d_1) + ...) / divisor densely in one
- * pass over the output (no zero-fill, no per-rank scatter).  vals / idx / ends of rank w start at
- * w * stride elements.  Indices must be unique within each payload. */
+ * pass over the output (no zero-fill, no per-rank scatter).  The grouped payload carries each
+ * entry's offset inside its 8192-element chunk (u16, off_out) instead of its index: 6 B per entry
+ * on the wire.  vals and ends of rank w start at w * stride 4-B words, its offsets at 2 w stride u16.
+ * Indices must be unique within each payload. */
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n);
 grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t k, int64_t n, float* vals_out,
-                                  int32_t* idx_out, uint32_t* ends_out, void* ws, size_t ws_bytes, void* stream);
-grace_status_t grace_sparse_aggregate_sorted(const float* vals, const int32_t* idx, const uint32_t* ends,
+                                  uint16_t* off_out, uint32_t* ends_out, void* ws, size_t ws_bytes, void* stream);
+grace_status_t grace_sparse_aggregate_sorted(const float* vals, const uint16_t* off, const uint32_t* ends,
                                              int64_t stride, int32_t world, float divisor, float* out, int64_t n,
                                              void* stream);
 /* as grace_sparse_aggregate with `out` already zero-filled by the caller (lets the fill overlap

@@ -266,12 +266,16 @@ def test_sparse_aggregate_rank_ordered(world, n, k):
     # chunk-grouped payloads (grace_sort_payload) for the one-pass aggregate
     sorted_buf = torch.cat([G.sort_payload(buf[w * 2 * k:(w + 1) * 2 * k], k, n) for w in range(world)])
     L = ops.sorted_payload_len(k, n)
+    nch, ow = (n + 8191) // 8192, (k + 1) // 2
+    assert L == k + ow + nch                                          # 6 B per entry + the chunk ends
     for w in range(world):
-        idx_s = _np(sorted_buf[w * L + k:w * L + 2 * k].view(torch.int32))
-        vals_s = _np(sorted_buf[w * L:w * L + k])
-        ends = _np(sorted_buf[w * L + 2 * k:(w + 1) * L].view(torch.int32))
-        assert np.all(np.diff(idx_s >> 13) >= 0)                       # grouped by 8192-chunk
-        assert np.array_equal(ends, np.searchsorted(idx_s >> 13, np.arange(L - 2 * k), side="right"))
+        base = w * L
+        vals_s = _np(sorted_buf[base:base + k])
+        offs = _np(sorted_buf[base + k:base + k + ow].view(torch.int16)).view(np.uint16)[:k].astype(np.int64)
+        ends = _np(sorted_buf[base + k + ow:base + L].view(torch.int32))
+        assert ends.size == nch and ends[-1] == k and np.all(np.diff(ends) >= 0)
+        assert np.all(offs < 8192)
+        idx_s = np.searchsorted(ends, np.arange(k), side="right") * 8192 + offs   # grouped by 8192-chunk
         order = np.argsort(idx_s)
         assert np.array_equal(idx_s[order], np.sort(idx_l[w]))        # same entries
         assert same_bits(vals_s[order], vals_l[w][np.argsort(idx_l[w])])
@@ -295,8 +299,12 @@ def test_sort_payload_workspace_reuse_across_sizes():
         vals = rng.standard_normal(k).astype(np.float32)
         buf = torch.cat([torch.from_numpy(vals), torch.from_numpy(idx.view(np.float32))]).to(dev)
         out = ops.sort_payload(buf, k, n).cpu().numpy()
-        ov, oi = out[:k], out[k:2 * k].view(np.int32)
-        assert np.all(np.diff(oi // 8192) >= 0), (n, k)
+        ow = (k + 1) // 2
+        ov = out[:k]
+        offs = out[k:k + ow].view(np.uint16)[:k].astype(np.int64)
+        ends = out[k + ow:].view(np.int32)
+        assert ends[-1] == k and np.all(np.diff(ends) >= 0), (n, k)
+        oi = np.searchsorted(ends, np.arange(k), side="right") * 8192 + offs
         order = np.argsort(idx)
         o2 = np.argsort(oi)
         assert np.array_equal(idx[order], oi[o2]) and np.array_equal(vals[order], ov[o2]), (n, k)
