@@ -38,6 +38,7 @@ constexpr int kSegQ = kSegChunk / (4 * kSegBlock);    // quads per thread
 static_assert(kSegQ * 4 <= 32, "one mask bit per element of a thread");
 constexpr int kSegBins = 2048;                        // histogram of key >> 20
 constexpr int kSegSelBlock = 1024;
+constexpr int kSelR = 16;                             // candidates per thread held in registers
 
 struct SegCtl {
   int32_t B;        // boundary bin (-1: every element selected)
@@ -71,14 +72,24 @@ struct SegChunk {
   int s;
   int64_t c0, c1;
 };
-__device__ __forceinline__ SegChunk seg_chunk(const SegArgs& a) {
+__device__ __forceinline__ SegChunk seg_chunk(const SegArgs& a, int64_t chunk) {
   SegChunk c;
-  c.s = a.chunk_seg[blockIdx.x];
+  c.s = a.chunk_seg[chunk];
   const int64_t s0 = a.seg_off[c.s], s1 = a.seg_off[c.s + 1];
-  c.c0 = s0 + ((int64_t)blockIdx.x - a.chk_off[c.s]) * kSegChunk;
+  c.c0 = s0 + (chunk - a.chk_off[c.s]) * kSegChunk;
   c.c1 = min(c.c0 + (int64_t)kSegChunk, s1);
   return c;
 }
+__device__ __forceinline__ SegChunk seg_chunk(const SegArgs& a) { return seg_chunk(a, blockIdx.x); }
+
+#ifndef GRACE_SEG_P1_CHUNKS
+#define GRACE_SEG_P1_CHUNKS 4
+#endif
+// p1 chunks per workgroup: the per-segment histogram leaves with one global atomic per non-zero
+// bin per flush, and a workgroup flushes once per segment it covers instead of once per chunk
+// (the atomics of one flush per 8192-element chunk kept the memory-side atomic unit busy ~20 us
+// past p1's end: the find kernel's first loads waited for them)
+constexpr int kSegP1Chunks = GRACE_SEG_P1_CHUNKS;
 
 __device__ __forceinline__ void seg_quad(const float* p, int64_t e, int64_t end, bool vec, float (&v)[4]) {
   if (vec && e + 3 < end) {
@@ -100,38 +111,44 @@ __device__ __forceinline__ void seg_store(float* p, int64_t e, int64_t end, bool
 }
 
 // ---- p1: compensate, residual = t, per-segment histogram
-__global__ __launch_bounds__(kSegBlock) void seg_p1_kernel(SegArgs a, int vec_base) {
+__global__ __launch_bounds__(kSegBlock) void seg_p1_kernel(SegArgs a, int vec_base, int64_t nchunks) {
   __shared__ uint32_t lh[kSegBlock / kWave][kSegBins];   // one histogram per wave: fewer same-bin conflicts
-  const SegChunk c = seg_chunk(a);
   const int tid = threadIdx.x, w = tid >> 6;
   for (int b = tid; b < (kSegBlock / kWave) * kSegBins; b += kSegBlock) (&lh[0][0])[b] = 0u;
-  const bool vec = vec_base && (c.c0 & 3) == 0;
-  float gv[kSegQ][4], rv[kSegQ][4] = {};
+  const int64_t ch0 = (int64_t)blockIdx.x * kSegP1Chunks, ch1 = min(ch0 + (int64_t)kSegP1Chunks, nchunks);
+  for (int64_t ch = ch0; ch < ch1; ++ch) {
+    const SegChunk c = seg_chunk(a, ch);
+    const bool vec = vec_base && (c.c0 & 3) == 0;
+    float gv[kSegQ][4], rv[kSegQ][4] = {};
 #pragma unroll
-  for (int u = 0; u < kSegQ; ++u) {
-    const int64_t e = c.c0 + 4 * ((int64_t)u * kSegBlock + tid);
-    seg_quad(a.g, e, c.c1, vec, gv[u]);
-    if (a.has_res) seg_quad(a.r, e, c.c1, vec, rv[u]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kSegQ; ++u) {
-    const int64_t e = c.c0 + 4 * ((int64_t)u * kSegBlock + tid);
-    float t[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t[j] = a.has_res ? a.beta * rv[u][j] + a.gamma * gv[u][j] : gv[u][j];
-      if (e + j < c.c1) atomicAdd(&lh[w][abs_key(t[j]) >> 20], 1u);
+    for (int u = 0; u < kSegQ; ++u) {
+      const int64_t e = c.c0 + 4 * ((int64_t)u * kSegBlock + tid);
+      seg_quad(a.g, e, c.c1, vec, gv[u]);
+      if (a.has_res) seg_quad(a.r, e, c.c1, vec, rv[u]);
     }
-    seg_store(a.r, e, c.c1, vec, t);
-  }
-  __syncthreads();
-  uint32_t* gh = a.hist + (int64_t)c.s * kSegBins;
-  for (int b = tid; b < kSegBins; b += kSegBlock) {
-    uint32_t v = 0;
+    __syncthreads();   // (first chunk: the histogram clear)
 #pragma unroll
-    for (int ww = 0; ww < kSegBlock / kWave; ++ww) v += lh[ww][b];
-    if (v) atomicAdd(&gh[b], v);
+    for (int u = 0; u < kSegQ; ++u) {
+      const int64_t e = c.c0 + 4 * ((int64_t)u * kSegBlock + tid);
+      float t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[j] = a.has_res ? a.beta * rv[u][j] + a.gamma * gv[u][j] : gv[u][j];
+        if (e + j < c.c1) atomicAdd(&lh[w][abs_key(t[j]) >> 20], 1u);
+      }
+      seg_store(a.r, e, c.c1, vec, t);
+    }
+    // flush when the next chunk belongs to another segment (or this is the last one)
+    if (ch + 1 == ch1 || a.chunk_seg[ch + 1] != c.s) {
+      __syncthreads();
+      uint32_t* gh = a.hist + (int64_t)c.s * kSegBins;
+      for (int b = tid; b < kSegBins; b += kSegBlock) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int ww = 0; ww < kSegBlock / kWave; ++ww) { v += lh[ww][b]; lh[ww][b] = 0u; }
+        if (v) atomicAdd(&gh[b], v);
+      }
+    }
   }
 }
 
@@ -236,6 +253,55 @@ __global__ __launch_bounds__(kSegSelBlock) void seg_select_kernel(SegArgs a) {
   if (ct.need == 0) return;
   const int2* list = a.cand + a.seg_off[s];
   const uint32_t nc = ct.n_cand;
+  if (nc <= (uint32_t)(kSegSelBlock * kSelR)) {
+    // the list held in registers for every radix pass (the global-list select below re-reads it
+    // from memory once per pass, a dependent round trip per round of loads)
+    int2 e[kSelR];
+#pragma unroll
+    for (int u = 0; u < kSelR; ++u) {
+      const uint32_t j = threadIdx.x + (uint32_t)u * kSegSelBlock;
+      e[u] = j < nc ? list[j] : make_int2(0, 0);
+    }
+    auto comp = [&](int u) { return comp_key(abs_key(u2f((uint32_t)e[u].y)), (uint32_t)e[u].x); };
+    uint64_t prefix = (uint64_t)((uint32_t)ct.B >> 1) << 53, pmask = (uint64_t)2047u << 53;
+    uint32_t rem = ct.need;
+    for (int pass = 1; pass < 6; ++pass) {   // block_select_comp's passes, from the second digit
+      const int shift = pass < 5 ? 53 - 11 * pass : 0;
+      const uint32_t dmask = pass < 5 ? 2047u : 511u;
+      for (int b = threadIdx.x; b < 2048; b += kSegSelBlock) hist[b] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSelR; ++u) {
+        const uint64_t c = comp(u);
+        if (threadIdx.x + (uint32_t)u * kSegSelBlock < nc && (c & pmask) == prefix)
+          atomicAdd(&hist[(c >> shift) & dmask], 1u);
+      }
+      __syncthreads();
+      uint32_t above;
+      const int d = find_bin_desc<kSegSelBlock, 2048>(hist, rem, s_w, s_res, &above);
+      rem -= above;
+      prefix |= (uint64_t)d << shift;
+      pmask |= (uint64_t)dmask << shift;
+      const bool whole = hist[d] == rem;
+      __syncthreads();
+      if (whole) break;
+    }
+    if (threadIdx.x == 0) s_pos = 0;
+    __syncthreads();
+    const int64_t kb = a.k_off[s] + ct.above;
+#pragma unroll
+    for (int u = 0; u < kSelR; ++u) {
+      if (threadIdx.x + (uint32_t)u * kSegSelBlock < nc && comp(u) >= prefix) {
+        const float v = u2f((uint32_t)e[u].y);
+        const uint32_t p = atomicAdd(&s_pos, 1u);
+        a.vals[kb + p] = v;
+        a.idx[kb + p] = e[u].x;
+        a.r[e[u].x] = v - v;
+        if (a.out) a.out[e[u].x] = 0.f + v;
+      }
+    }
+    return;
+  }
   auto src = [list](int64_t j) {
     const int2 e = list[j];
     return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
@@ -307,7 +373,7 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
   const int vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual) |
                     reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   hipStream_t st = as_stream(stream);
-  seg_p1_kernel<<<(unsigned)nchunks, kSegBlock, 0, st>>>(a, vec);
+  seg_p1_kernel<<<(unsigned)((nchunks + kSegP1Chunks - 1) / kSegP1Chunks), kSegBlock, 0, st>>>(a, vec, nchunks);
   GRACE_CHECK_LAUNCH("grace_topk_segmented_step");
   seg_find_kernel<<<(unsigned)nseg, kSegBlock, 0, st>>>(a);
   GRACE_CHECK_LAUNCH("grace_topk_segmented_step");

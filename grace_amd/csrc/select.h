@@ -46,23 +46,28 @@ __device__ void find_bins_desc(const uint32_t* hist, const uint32_t (&rank)[NR],
   constexpr int PER = NBINS / BLOCK;
   const int t = threadIdx.x;
   const int top = NBINS - 1 - t * PER;  // this thread covers bins top, top-1, ..., top-PER+1
-  uint32_t s = 0;
+  // the thread's bins stay in registers: with a global histogram, re-reading them in the search
+  // below was a chain of dependent global loads (the segmented find kernel's 22 us)
+  uint32_t h[PER], s = 0;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) s += hist[top - j];
+  for (int j = 0; j < PER; ++j) h[j] = hist[top - j];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) s += h[j];
   if (t < 2 * NR) s_res[t] = 0;
   const uint32_t ex = block_excl_scan<BLOCK>(s, s_w, nullptr);
 #pragma unroll
   for (int q = 0; q < NR; ++q) {
     if (ex < rank[q] && rank[q] <= ex + s) {
       uint32_t acc = ex;
+      bool found = false;
+#pragma unroll
       for (int j = 0; j < PER; ++j) {
-        const uint32_t h = hist[top - j];
-        if (acc + h >= rank[q]) {
+        if (!found && acc + h[j] >= rank[q]) {
           s_res[2 * q] = (uint32_t)(top - j);
           s_res[2 * q + 1] = acc;
-          break;
+          found = true;
         }
-        acc += h;
+        acc += h[j];
       }
     }
   }
