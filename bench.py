@@ -485,7 +485,61 @@ def bench_topk_e2e(args, world, rank, dev):
     line["config"] = {"workload": "pinned host bucket -> H2D -> Allgather(TopK 1%, ResidualMemory).step -> D2H",
                       "numel": n, "h2d_plus_d2h_ms": round(t_copy / args.steps * 1e3, 4)}
     line["roofline"] = None
+    line["pipelined"] = bench_topk_e2e_pipelined(args, world, dev)
     return line
+
+
+def bench_topk_e2e_pipelined(args, world, dev):
+    """The same per-bucket work as a DDP loop sees it: bucket i's H2D on a copy-in stream, its step on
+    the compute stream, its D2H on a copy-out stream, so bucket i + 1 arrives while bucket i computes
+    and bucket i - 1 leaves (PCIe is full duplex).  Three buckets with their own residuals rotate;
+    events order each bucket's three stages and the reuse of its device buffer."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = args.numel
+    comm = Allgather(TopKCompressor(args.ratio), ResidualMemory(), world)
+    nb = 3
+    hosts = [torch.randn(n).pin_memory() for _ in range(nb)]
+    backs = [torch.empty(n).pin_memory() for _ in range(nb)]
+    dbufs = [torch.empty(n, device=dev) for _ in range(nb)]
+    s_in, s_cmp, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+    done = [None] * nb          # event: bucket b's step has finished reading dbufs[b]
+    left = [None] * nb          # event: bucket b's last D2H out of backs[b] has finished
+
+    def step(i):
+        b = i % nb
+        with torch.cuda.stream(s_in):
+            if done[b] is not None:
+                s_in.wait_event(done[b])
+            dbufs[b].copy_(hosts[b], non_blocking=True)
+            arrived = torch.cuda.Event()
+            arrived.record(s_in)
+        with torch.cuda.stream(s_cmp):
+            s_cmp.wait_event(arrived)
+            out = comm.step(dbufs[b], f"bucket{b}")
+            computed = torch.cuda.Event()
+            computed.record(s_cmp)
+            done[b] = computed
+        with torch.cuda.stream(s_out):
+            s_out.wait_event(computed)
+            if left[b] is not None:
+                s_out.wait_event(left[b])
+            backs[b].copy_(out, non_blocking=True)
+            out.record_stream(s_out)
+            ev = torch.cuda.Event()
+            ev.record(s_out)
+            left[b] = ev
+
+    for i in range(nb):
+        step(i)
+    torch.cuda.synchronize(dev)
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
+    t = elapsed / args.steps
+    return {"ms_per_step": round(t * 1e3, 4), "value": round(4.0 * n / t / 1e9, 2), "unit": "GB/s",
+            "streams": 3, "buckets": nb,
+            "note": "H2D of bucket i+1, the step of bucket i and the D2H of bucket i-1 overlap (copy-in, compute, "
+                    "copy-out streams); the serial line above runs the three one after the other"}
 
 
 def bench_topk_sharded(args, world, rank, dev):
