@@ -39,7 +39,8 @@ constexpr int kMaxGroupChunks = 32768;                 // LDS histogram bins (12
 // last workgroup to finish (ticket; agent-scope atomics, no L2 fences) scans the counts in place
 __device__ void scan_counts_block(uint32_t* counts, int64_t nchunks);
 
-__global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const int32_t* __restrict__ idx, int64_t k,
+template <typename IdxT>
+__global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const IdxT* __restrict__ idx, int64_t k,
                                                                 int64_t nchunks, uint32_t* __restrict__ counts,
                                                                 uint32_t* __restrict__ ticket) {
   extern __shared__ uint32_t h[];
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const int32_t* 
 #pragma unroll 4
   for (int e = 0; e < kGroupPer; ++e) {
     const int64_t j = base + (int64_t)e * kGroupBlock + threadIdx.x;
-    if (j < k) atomicAdd(&h[idx[j] >> kPChunkLog], 1u);
+    if (j < k) atomicAdd(&h[(int64_t)idx[j] >> kPChunkLog], 1u);
   }
   __syncthreads();
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock)
@@ -108,8 +109,9 @@ __device__ void scan_counts_block(uint32_t* counts, int64_t nchunks) {
 
 // pass 2: each workgroup reserves its range of every chunk it touches (one atomic per non-zero
 // bin), ranks its entries within a bin with LDS atomics, and writes them grouped by chunk
+template <typename IdxT>
 __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float* __restrict__ vals,
-                                                                   const int32_t* __restrict__ idx, int64_t k,
+                                                                   const IdxT* __restrict__ idx, int64_t k,
                                                                    int64_t nchunks, uint32_t* __restrict__ cursor,
                                                                    float* __restrict__ vals_out,
                                                                    uint16_t* __restrict__ off_out) {
@@ -122,8 +124,8 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
 #pragma unroll
   for (int e = 0; e < kGroupPer; ++e) {
     const int64_t j = base + (int64_t)e * kGroupBlock + threadIdx.x;
-    ii[e] = j < k ? idx[j] : -1;
-    vv[e] = j < k ? vals[j] : 0.f;
+    ii[e] = j < k ? (int32_t)idx[j] : -1;
+    vv[e] = j < k && vals ? vals[j] : 0.f;
   }
 #pragma unroll
   for (int e = 0; e < kGroupPer; ++e)
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
   for (int e = 0; e < kGroupPer; ++e) {
     if (ii[e] < 0) continue;
     const uint32_t pos = atomicAdd(&h[ii[e] >> kPChunkLog], 1u);
-    vals_out[pos] = vv[e];
+    if (vals_out) vals_out[pos] = vv[e];
     off_out[pos] = (uint16_t)(ii[e] & (kPChunk - 1));   // the offset inside its chunk (13 bits)
   }
 }
@@ -207,6 +209,25 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
   }
 }
 
+// group entries by 8192-element chunk (u16 offsets, chunk end offsets); vals optional.  Shared by
+// grace_sort_payload and the world-1 random-k step (sparse.hip).
+template <typename IdxT>
+hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t nchunks, float* vals_out,
+                          uint16_t* off_out, uint32_t* ends_out, uint32_t* ticket, hipStream_t s) {
+  uint32_t* counts = ends_out;   // counts -> exclusive offsets (hist) -> chunk ends (scatter cursors)
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
+  if (e != hipSuccess || k == 0) return e;
+  const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
+  const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
+  group_hist_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  group_scatter_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out);
+  return hipGetLastError();
+}
+template hipError_t group_by_chunk<int64_t>(const float*, const int64_t*, int64_t, int64_t, float*, uint16_t*,
+                                            uint32_t*, uint32_t*, hipStream_t);
+
 }  // namespace grace
 
 using namespace grace;
@@ -227,18 +248,9 @@ grace_status_t grace_sort_payload(const float* vals, const int32_t* idx, int64_t
   GRACE_REQUIRE(vals && idx && vals_out && off_out && ends_out && ws && k >= 0 && k < ((int64_t)1 << 31) &&
                     n >= 1 && nchunks <= kMaxGroupChunks && ws_bytes >= grace_sort_payload_workspace_bytes(k, n),
                 "grace_sort_payload: bad arguments (n <= 2^28)");
-  hipStream_t s = as_stream(stream);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(ws);
-  uint32_t* counts = ends_out;   // counts -> exclusive offsets (hist) -> chunk ends (scatter cursors)
-  hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
+  const hipError_t e = group_by_chunk<int32_t>(vals, idx, k, nchunks, vals_out, off_out, ends_out,
+                                               reinterpret_cast<uint32_t*>(ws), as_stream(stream));
   if (e != hipSuccess) { set_error("grace_sort_payload", e); return GRACE_ERR_HIP; }
-  if (k == 0) return GRACE_OK;
-  const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
-  const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
-  group_hist_kernel<<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
-  GRACE_CHECK_LAUNCH("grace_sort_payload");
-  group_scatter_kernel<<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out);
-  GRACE_CHECK_LAUNCH("grace_sort_payload");
   return GRACE_OK;
 }
 

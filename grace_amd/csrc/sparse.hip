@@ -74,6 +74,84 @@ __global__ __launch_bounds__(kSBlock) void randomk_pass_kernel(const float* __re
   }
 }
 
+// World-1 Allgather(RandomK, ResidualMemory).step in ONE streaming pass (the dense variant; no
+// payload is materialised: at world 1 the step's result is out alone).  The drawn indices are
+// grouped by 8192-element chunk first (payload.hip's counting sort: u16 offsets + chunk ends);
+// workgroup c marks its chunk's selected offsets in an LDS bitmap (duplicates set the same bit,
+// as zeros.scatter_ writes the same value twice), then streams the chunk once:
+// selected -> out = 0 + t, r' = t - t; else out = 0, r' = t.  16 B per element and no random
+// gathers / scatters (which move whole lines for 4-B values).
+template <typename IdxT>
+hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t nchunks, float* vals_out,
+                          uint16_t* off_out, uint32_t* ends_out, uint32_t* ticket, hipStream_t s);
+constexpr int kRkChunkLog = 13;                  // = payload.hip kPChunkLog
+constexpr int kRkChunk = 1 << kRkChunkLog;
+constexpr int kRkQ = kRkChunk / (4 * kSBlock);   // quads per thread per array
+template <bool HAS_RES>
+__global__ __launch_bounds__(kSBlock) void randomk_dense_pass_kernel(const float* __restrict__ g, float* __restrict__ r,
+                                                                    float beta, float gamma, int64_t n,
+                                                                    const uint16_t* __restrict__ offs,
+                                                                    const uint32_t* __restrict__ ends,
+                                                                    float* __restrict__ out) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t bm[kRkChunk / 32];
+  const int64_t c = blockIdx.x;
+  const int64_t c0 = c << kRkChunkLog, c1 = min(c0 + (int64_t)kRkChunk, n);
+  const int t = threadIdx.x;
+  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r) |
+                     reinterpret_cast<uintptr_t>(out)) & 15u) == 0 && c1 - c0 == kRkChunk;
+  f4 gv[kRkQ], rv[kRkQ];
+  if (vec) {
+#pragma unroll
+    for (int u = 0; u < kRkQ; ++u) {
+      const int64_t e = c0 + 4 * ((int64_t)u * kSBlock + t);
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g + e));
+      if (HAS_RES) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(r + e));
+    }
+  }
+  for (int w = t; w < kRkChunk / 32; w += kSBlock) bm[w] = 0u;
+  __syncthreads();
+  const uint32_t e0 = c > 0 ? ends[c - 1] : 0u, e1 = ends[c];
+  for (uint32_t j = e0 + t; j < e1; j += kSBlock) {
+    const uint32_t o = offs[j];
+    atomicOr(&bm[o >> 5], 1u << (o & 31));
+  }
+  __syncthreads();
+  auto one = [&](float tv, int64_t i, float& o, float& rr) {
+    const int64_t l = i - c0;
+    const bool sel = (bm[l >> 5] >> (l & 31)) & 1u;
+    o = sel ? 0.f + tv : 0.f;
+    rr = sel ? tv - tv : tv;
+  };
+  if (vec) {
+#pragma unroll
+    for (int u = 0; u < kRkQ; ++u) {
+      const int64_t e = c0 + 4 * ((int64_t)u * kSBlock + t);
+      f4 tt = gv[u];
+      if (HAS_RES) tt = f4{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
+                           beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
+      f4 o, rr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a, b;
+        one(tt[j], e + j, a, b);
+        o[j] = a;
+        rr[j] = b;
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<f4*>(out + e));
+      __builtin_nontemporal_store(rr, reinterpret_cast<f4*>(r + e));
+    }
+  } else {
+    for (int64_t i = c0 + t; i < c1; i += kSBlock) {
+      const float tv = HAS_RES ? beta * r[i] + gamma * g[i] : g[i];
+      float a, b;
+      one(tv, i, a, b);
+      out[i] = a;
+      r[i] = b;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kSBlock) void randomk_scatter_kernel(const int64_t* __restrict__ idx,
                                                                  const float* __restrict__ vals, int64_t k,
                                                                  float* __restrict__ r, float* __restrict__ out) {
@@ -528,6 +606,34 @@ grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t ha
   GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
   randomk_scatter_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(idx, vals, k, residual, out);
   GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
+  return GRACE_OK;
+}
+
+size_t grace_randomk_step_w1_dense_workspace_bytes(int64_t n, int64_t k) {
+  const int64_t nch = (n + kRkChunk - 1) / kRkChunk;
+  return 256 + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255) + sizeof(uint16_t) * (size_t)(k < 1 ? 1 : k);
+}
+
+grace_status_t grace_randomk_step_w1_dense(const float* g, float* residual, int32_t has_residual, float beta,
+                                           float gamma, int64_t n, const int64_t* idx, int64_t k, float* out,
+                                           void* ws, size_t ws_bytes, void* stream) {
+  GRACE_REQUIRE(g && residual && out && ws && n >= 1 && n < ((int64_t)1 << 31) && k >= 0 && (k == 0 || idx) &&
+                    ws_bytes >= grace_randomk_step_w1_dense_workspace_bytes(n, k),
+                "grace_randomk_step_w1_dense: bad arguments (n < 2^31, workspace)");
+  const int64_t nch = (n + kRkChunk - 1) / kRkChunk;
+  GRACE_REQUIRE(nch <= 32768, "grace_randomk_step_w1_dense: n <= 2^28");
+  hipStream_t s = as_stream(stream);
+  char* p = reinterpret_cast<char*>(ws);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(p);
+  uint32_t* ends = reinterpret_cast<uint32_t*>(p + 256);
+  uint16_t* offs = reinterpret_cast<uint16_t*>(p + 256 + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255));
+  const hipError_t e = group_by_chunk<int64_t>(nullptr, idx, k, nch, nullptr, offs, ends, ticket, s);
+  if (e != hipSuccess) { set_error("grace_randomk_step_w1_dense", e); return GRACE_ERR_HIP; }
+  if (has_residual)
+    randomk_dense_pass_kernel<true><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out);
+  else
+    randomk_dense_pass_kernel<false><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_step_w1_dense");
   return GRACE_OK;
 }
 

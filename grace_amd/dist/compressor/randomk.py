@@ -34,8 +34,9 @@ class RandomKCompressor(Compressor):
         return ops.randomk_indices(h, numel, k, flat.device)
 
     def fused_step(self, communicator, tensor, name):
-        """World-1 Allgather(RandomK, ResidualMemory).step in three launches (grace_randomk_step_w1):
-        the same values as compensate + compress + update + send_receive."""
+        """World-1 Allgather(RandomK, ResidualMemory).step: the indices grouped by chunk, then one
+        streaming pass for r' and out (grace_randomk_step_w1_dense; no payload at world 1) -- the
+        same values as compensate + compress + update + send_receive."""
         from grace_amd.dist.communicator.allgather import Allgather
         from grace_amd.dist.memory.residual import ResidualMemory
         mem = communicator.memory
@@ -48,7 +49,10 @@ class RandomKCompressor(Compressor):
         if not has:
             res = torch.empty_like(g)
         indices = self._indices(g, name)
-        _, out = ops.randomk_step_w1(g, res, has, mem.beta, mem.gamma, indices)
+        if g.numel() <= ops.SORT_PAYLOAD_MAX_N:
+            out = ops.randomk_step_w1_dense(g, res, has, mem.beta, mem.gamma, indices)
+        else:
+            _, out = ops.randomk_step_w1(g, res, has, mem.beta, mem.gamma, indices)
         mem.residuals[name] = res
         return out.view(tensor.shape)
 

@@ -660,6 +660,21 @@ def randomk_step_w1(g, residual, has_residual, beta, gamma, idx):
     return vals, out
 
 
+def randomk_step_w1_dense(g, residual, has_residual, beta, gamma, idx, out=None):
+    """The world-1 step's out (and r' in `residual`) in one streaming pass after grouping the indices
+    by chunk (grace_randomk_step_w1_dense); no payload."""
+    g = dev_f32(g)
+    idx = require_dev(idx, "indices")
+    if idx.dtype != torch.int64:
+        raise ValueError("grace_amd: random-k indices are int64")
+    out = torch.empty_like(g) if out is None else out
+    n, k = g.numel(), idx.numel()
+    ws = workspace("randomk_w1", _lib.query("grace_randomk_step_w1_dense_workspace_bytes", n, k), g.device)
+    _lib.call("grace_randomk_step_w1_dense", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
+              float(gamma), n, _p(idx), k, _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
 def gather(x, idx):
     x = dev_f32(x)
     idx = require_dev(idx)

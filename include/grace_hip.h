@@ -297,6 +297,14 @@ grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float
 grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
                                      int64_t n, const int64_t* idx, int64_t k, float* vals, float* out,
                                      void* stream);
+/* The same world-1 step without materialising the payload (only `out` is the step's result at
+ * world 1): the indices are grouped by 8192-element chunk, then ONE streaming pass writes r' and
+ * out (16 B per element, no random gathers / scatters); bit-identical out and r'.  n < 2^31 and
+ * n <= 2^28; ws: grace_randomk_step_w1_dense_workspace_bytes, zeroed once at allocation. */
+size_t grace_randomk_step_w1_dense_workspace_bytes(int64_t n, int64_t k);
+grace_status_t grace_randomk_step_w1_dense(const float* g, float* residual, int32_t has_residual, float beta,
+                                           float gamma, int64_t n, const int64_t* idx, int64_t k, float* out,
+                                           void* ws, size_t ws_bytes, void* stream);
 /* Threshold (threshold.py:16-19): idx = where(|x| >= min(thr, max(x))) in ascending order.
  * count -> (host reads meta = ws[0..2]: bound bits, count, recount flag) -> [recount] -> write.
  * The caller synchronises once to size the variable-length payload. */

@@ -340,3 +340,26 @@ def test_randomk_world1_fused_step_equals_unfused(n, rng):
         assert same_bits(fo[s], uo[s]), s
     assert same_bits(fr, ur)
     assert np.count_nonzero(fo[-1]) > 0
+
+
+@pytest.mark.parametrize("n,ratio", [((1 << 24) + 5, 0.01), (100003, 0.7), (8192, 0.3)])
+def test_randomk_dense_step_equals_three_launch_step(n, ratio):
+    """grace_randomk_step_w1_dense (indices grouped by chunk, one streaming pass) against
+    grace_randomk_step_w1 (pass + gather + scatter): out and r' bit-identical, with many duplicate
+    indices (ratio 0.7), special values and a partial last chunk."""
+    from grace_amd import ops as G
+    rng = np.random.default_rng(n)
+    g0 = rng.standard_normal(n).astype(np.float32)
+    g0[rng.choice(n, 3, replace=False)] = np.nan
+    g0[rng.choice(n, 3, replace=False)] = -np.inf
+    g0[rng.choice(n, 20, replace=False)] = -0.0
+    r0 = (0.3 * rng.standard_normal(n)).astype(np.float32)
+    k = G.ratio_k(n, ratio)
+    idx = torch.from_numpy(rng.integers(0, n, k).astype(np.int64)).to("cuda")
+    g = _t(g0)
+    for has in (False, True):
+        ra, rb = _t(r0), _t(r0)
+        _, out_a = G.randomk_step_w1(g, ra, has, 1.0, 1.0, idx)
+        out_b = G.randomk_step_w1_dense(g, rb, has, 1.0, 1.0, idx)
+        assert same_bits(_np(out_b), _np(out_a)), has
+        assert same_bits(_np(rb), _np(ra)), has
