@@ -248,6 +248,7 @@ def bench_topk(args, world, rank, dev):
                                       "arrays, 3 rotated sets, the fastest launch of the fastest of 6 layouts "
                                       f"(variant {variant}), HIP events")
     roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
+    roofline["frac_of_measured_copy_median"] = round(achieved / copy_med, 4) if copy_med else None
     line["roofline"] = roofline
     if world == 1 and not args.no_overlap:
         line["two_streams"] = bench_topk_two_streams(args, grads, names)
