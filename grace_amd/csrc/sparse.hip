@@ -288,32 +288,67 @@ __global__ __launch_bounds__(kSBlock) void thr_spec_kernel(const float* __restri
   float mx = -INFINITY;
   uint32_t nan = 0;
   auto acc = [&](float v) { if (v != v) nan = 1; else mx = fmaxf(mx, v); };
-  for (int64_t e0 = base + 4 * (int64_t)threadIdx.x; e0 < qe; e0 += 4 * (int64_t)kSBlock * kThrU) {
+  auto process = [&](int64_t e, const f4s& gq, const f4s& rq) {
+    f4s t = gq;
+    if (MODE == 2) t = f4s{beta * rq.x + gamma * gq.x, beta * rq.y + gamma * gq.y, beta * rq.z + gamma * gq.z,
+                           beta * rq.w + gamma * gq.w};
+    f4s o, rr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc(t[j]);
+      float oj, rj;
+      thr_sel(t[j], thr, oj, rj);
+      o[j] = oj;
+      rr[j] = rj;
+    }
+    __builtin_nontemporal_store(o, reinterpret_cast<f4s*>(out + e));
+    if (MODE != 0) __builtin_nontemporal_store(rr, reinterpret_cast<f4s*>(r + e));
+  };
+  if (qe - base == kThrChunk) {
+    // a whole chunk: a compile-time number of rounds, the next round's loads issued before the
+    // current round is processed (8 or 16 x 16 B in flight per lane, no guarded loads)
+    constexpr int NR = kThrChunk / (4 * kSBlock * kThrU);
+    const int64_t b0 = base + 4 * (int64_t)threadIdx.x;
     f4s gv[kThrU], rv[kThrU];
 #pragma unroll
     for (int u = 0; u < kThrU; ++u) {
-      const int64_t e = e0 + 4 * (int64_t)u * kSBlock < qe ? e0 + 4 * (int64_t)u * kSBlock : e0;
-      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + e));
-      if (MODE == 2) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(r + e));
+      gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + b0 + 4 * (int64_t)u * kSBlock));
+      if (MODE == 2) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(r + b0 + 4 * (int64_t)u * kSBlock));
     }
 #pragma unroll
-    for (int u = 0; u < kThrU; ++u) {
-      const int64_t e = e0 + 4 * (int64_t)u * kSBlock;
-      if (e >= qe) break;
-      f4s t = gv[u];
-      if (MODE == 2) t = f4s{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
-                             beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
-      f4s o, rr;
+    for (int q = 0; q < NR; ++q) {
+      const int64_t e0 = b0 + (int64_t)q * 4 * kSBlock * kThrU;
+      f4s gn[kThrU], rn[kThrU];
+      if (q + 1 < NR) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc(t[j]);
-        float oj, rj;
-        thr_sel(t[j], thr, oj, rj);
-        o[j] = oj;
-        rr[j] = rj;
+        for (int u = 0; u < kThrU; ++u) {
+          const int64_t e = e0 + 4 * (int64_t)kSBlock * kThrU + 4 * (int64_t)u * kSBlock;
+          gn[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + e));
+          if (MODE == 2) rn[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(r + e));
+        }
       }
-      __builtin_nontemporal_store(o, reinterpret_cast<f4s*>(out + e));
-      if (MODE != 0) __builtin_nontemporal_store(rr, reinterpret_cast<f4s*>(r + e));
+#pragma unroll
+      for (int u = 0; u < kThrU; ++u) process(e0 + 4 * (int64_t)u * kSBlock, gv[u], rv[u]);
+      if (q + 1 < NR) {
+#pragma unroll
+        for (int u = 0; u < kThrU; ++u) { gv[u] = gn[u]; rv[u] = rn[u]; }
+      }
+    }
+  } else {
+    for (int64_t e0 = base + 4 * (int64_t)threadIdx.x; e0 < qe; e0 += 4 * (int64_t)kSBlock * kThrU) {
+      f4s gv[kThrU], rv[kThrU];
+#pragma unroll
+      for (int u = 0; u < kThrU; ++u) {
+        const int64_t e = e0 + 4 * (int64_t)u * kSBlock < qe ? e0 + 4 * (int64_t)u * kSBlock : e0;
+        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(g + e));
+        if (MODE == 2) rv[u] = __builtin_nontemporal_load(reinterpret_cast<const f4s*>(r + e));
+      }
+#pragma unroll
+      for (int u = 0; u < kThrU; ++u) {
+        const int64_t e = e0 + 4 * (int64_t)u * kSBlock;
+        if (e >= qe) break;
+        process(e, gv[u], rv[u]);
+      }
     }
   }
   for (int64_t i = qe + threadIdx.x; i < end; i += kSBlock) {
