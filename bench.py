@@ -35,6 +35,7 @@ Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -123,10 +124,13 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         backend = os.environ.get("GRACE_BENCH_BACKEND", "nccl")
+        # a bounded collective timeout: a rank that never arrives ends the job instead of holding
+        # the node until the driver's limit
+        tmo = datetime.timedelta(seconds=int(os.environ.get("GRACE_BENCH_PG_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     run = {"topk": bench_topk, "topk_nomem": bench_topk_nomem, "topk_e2e": bench_topk_e2e, "topk_sharded": bench_topk_sharded,
            "ddp_params": bench_ddp, "ddp_bucket": bench_ddp, "ddp_segmented": bench_ddp, "sign": bench_sign, "sign256": bench_sign, "qsgd": bench_quant, "qsgd_step": bench_quant, "terngrad_step": bench_quant,
            "terngrad": bench_quant, "powersgd": bench_powersgd, "dgc": bench_dgc, "sign_bits": bench_sign_bits,
@@ -140,13 +144,45 @@ def main():
     if args.workload == "topk" and world > 1 and not args.no_sharded:
         # BASELINE configs[4] (one 256 MiB bucket sharded over the ranks, top-k 0.1 %) rides in the
         # same JSON line, so the driver's 1 -> 8 GPU record covers it next to the DP replicas
-        sh = bench_topk_sharded(args, world, rank, dev)
-        line["sharded"] = {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config",
-                                                    "roofline")}
+        line["sharded"] = nested_sharded(line, args, world, rank, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def nested_sharded(line, args, world, rank, dev):
+    """The configs[4] record inside the DP-replica line, guarded so that it can never cost the DP
+    record: an exception on a rank is agreed through one all_reduce and recorded as {"error": ...};
+    a rank that hangs (a collective some rank never reaches) is bounded by a watchdog that prints
+    the DP line with {"error": "timeout"} on rank 0 and ends every rank's process."""
+    import threading
+    limit = float(os.environ.get("GRACE_BENCH_SHARDED_LIMIT", "120"))
+
+    def expire():
+        if rank == 0:
+            line["sharded"] = {"error": f"timeout: the sharded leg did not finish within {limit:.0f} s"}
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    dog = threading.Timer(limit, expire)
+    dog.daemon = True
+    dog.start()
+    err = None
+    try:
+        if os.environ.get("GRACE_BENCH_INJECT_SHARDED_FAILURE", "") in ("all", str(rank)):
+            raise RuntimeError(f"injected failure on rank {rank}")
+        sh = bench_topk_sharded(args, world, rank, dev)
+    except Exception as e:          # recorded, not raised: the DP-replica record stays
+        err = f"{type(e).__name__}: {e}"[:400]
+    flag = torch.tensor([1.0 if err else 0.0], device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    dog.cancel()
+    if float(flag.item()) > 0:
+        return {"error": err or "failed on another rank"}
+    return {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config", "roofline")}
 
 
 # GRACE_BENCH_NO_PROBE=1: skip the in-bench HBM probes (profiling passes, whose per-dispatch

@@ -23,6 +23,7 @@ SIGNATURES = {
     "grace_version": (ctypes.c_int, []),
     "grace_last_error": (ctypes.c_char_p, []),
     "grace_read_status": (ST, [P, P, P]),
+    "grace_status_take": (ctypes.c_int32, [P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
     "grace_timer_collect": (ST, [P, P]),
     "grace_event_create": (ST, [P]),
@@ -54,15 +55,9 @@ SIGNATURES = {
     "grace_topk_segmented_workspace_bytes": (SZ, [I64, I32]),
     "grace_topk_segmented_chunk": (I32, []),
     "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]),
-    "grace_topk_shard_xs_words": (SZ, []),
-    "grace_topk_shard_xh_words": (SZ, []),
-    "grace_topk_shard_sample": (ST, [P, P, I32, F32, F32, I64, I64, P, P]),
-    "grace_topk_shard_main": (ST, [P, P, I32, F32, F32, I64, I64, I64, I64, I64, P, P, P, SZ, P, P, P]),
-    "grace_topk_shard_route": (ST, [P, I64, I64, I64, I32, P, P, P, SZ, P, P]),
-    "grace_topk_shard_boundary": (ST, [P, I64, I64, I64, P, I32, I64, ctypes.c_uint32, P, P, I64, P, SZ, P]),
-    "grace_topk_shard_take": (ST, [P, P, I64, P, I64, I64, P, P, I64, P]),
-    "grace_topk_shard_read": (ST, [P, P, P]),
-    "grace_sparse_scatter_range": (ST, [P, P, I64, I64, I32, I64, I64, P, P]),
+    "grace_shard_record_words": (SZ, [I64]),
+    "grace_shard_select_workspace_bytes": (SZ, [I32, I64]),
+    "grace_shard_select": (ST, [P, I32, I32, I64, P, I64, P, P, I64, I64, P, P, SZ, P, P]),
     "grace_dgc_workspace_bytes": (SZ, [I64]),
     "grace_dgc_sample": (ST, [P, I64, P, U64, I64, P, P]),
     "grace_dgc_threshold": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),

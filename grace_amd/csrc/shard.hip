@@ -1,0 +1,316 @@
+// Sharded top-k with residual error feedback (BASELINE configs[4]): ONE gradient
+// bucket of n elements split into contiguous shards, one per rank; the ranks together select
+// exactly the single-GPU top-k of the whole bucket (TopKCompressor, grace_dl/dist/compressor/
+// topk.py:32-42, with the single-GPU engine's tie rule: larger |t| first, lower global index
+// first), keep the residual of their own shard (ResidualMemory, memory/residual.py:10-20) and
+// decode the dense result (replicated, or only their own slice).
+//
+// One exchange per step, no host synchronisation, exact by construction.  The global top-k is
+// contained in the union of the ranks' LOCAL top-k (a rank contributes at most k entries, and
+// those are its own best k by the same composite order), so:
+//   1. local: the single-GPU engine (grace_topk_residual_step, 12 B/element) selects this
+//      shard's top-k_loc, k_loc = min(k, m), straight into this rank's record
+//      [header | vals f32[cap] | local idx i32[cap]] (cap = k; idx -1 pads a short shard); it
+//      leaves r' = t - t at its picks and r' = t elsewhere;
+//   2. ONE all_gather_into_tensor of the fixed-size records (8 k bytes per rank);
+//   3. shard_hist (every rank, identically): a 32768-bin histogram of key >> 16 over the W * cap
+//      gathered entries; the last workgroup to arrive finds the bin B holding the k-th key;
+//   4. shard_apply: entries above B are selected, below B rejected; the bin-B entries go to a short
+//      boundary list that the last workgroup ranks exactly by the composite (key, global index).
+//      A selected entry is written to the dense output (0 + v); an own entry the global cut rejects
+//      gets its t back in the residual (r' = v: the engine had zeroed it), and pay_idx marks this
+//      rank's record entries with their global index (selected) or -1.
+// No sample exchange, no capacity guess and no bracket-miss protocol: the record capacity is k
+// (a rank can hold at most k of the global top-k), and a degenerate local bucket is handled inside
+// the local engine's own exact fallback.  The partition (shard lengths) is agreed on a name's first
+// step; each record header carries its shard length and shard_hist checks it against the agreed
+// table, setting bit 1 of the caller's pinned status word on a mismatch (sharded.py raises at the
+// next step, or redoes the step exactly with check_sizes=True).
+#include "common.h"
+#include "select.h"
+
+namespace grace {
+
+constexpr int kShHdr = 8;            // record header words: [0] = this rank's shard length
+constexpr int kShBlock = 1024;
+constexpr int kShPer = 4;            // entries per thread per round (all loads before any use)
+constexpr int kShBins = 32768;       // key >> 16: 1/128-octave bins
+constexpr int kShMaxWorld = 1024;
+constexpr int kShMaxGrid = 512;
+
+struct ShCtl {
+  int32_t b1;        // boundary bin; -1 = every valid entry is selected
+  uint32_t above;    // valid entries in bins above b1
+  uint32_t need;     // entries still to take from bin b1
+  uint32_t ticket1;  // shard_hist arrivals (reset by the last)
+  uint32_t ticket2;  // shard_apply arrivals (reset by the last)
+  uint32_t nb;       // boundary-list fill counter (reset by the last shard_apply)
+  uint32_t pad[10];
+};
+static_assert(sizeof(ShCtl) == 64, "ShCtl layout");
+
+struct ShArgs {
+  const int32_t* recs;  // W gathered records, `stride` words each
+  int64_t stride, cap;
+  int32_t world, rank;
+  const int64_t* tab;   // device [m_0 .. m_{W-1}, base_0 .. base_{W-1}]: the agreed partition
+  int64_t k;
+  float* r;             // this rank's residual shard
+  float* out;           // dense output, zero-filled, global range [out_base, out_base + out_len)
+  int64_t out_base, out_len;
+  int32_t* pay_idx;     // this rank's record entries: global index if selected, -1 otherwise
+  ShCtl* ctl;
+  uint32_t* hist;       // [kShBins], left zeroed
+  uint32_t* bnd;        // boundary list of entry numbers [world * cap]
+  int32_t* status;      // pinned host word (system-scope fetch_or), may be null
+};
+
+__device__ __forceinline__ const float* rec_vals(const ShArgs& a, uint32_t w) {
+  return reinterpret_cast<const float*>(a.recs + (int64_t)w * a.stride + kShHdr);
+}
+__device__ __forceinline__ const int32_t* rec_idx(const ShArgs& a, uint32_t w) {
+  return a.recs + (int64_t)w * a.stride + kShHdr + a.cap;
+}
+
+// entry number e -> (rank w, slot j); N = world * cap < 2^31 (checked on the host)
+__device__ __forceinline__ void split_entry(uint32_t e, uint32_t cap, uint32_t& w, uint32_t& j) {
+  w = e / cap;
+  j = e - w * cap;
+}
+
+// 3. the histogram of key >> 16 over the gathered entries; the last arriver finds bin B
+__global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
+  __shared__ uint32_t h[kShBins];
+  __shared__ uint32_t s_w[kShBlock / kWave + 1];
+  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_last;
+  const int t = threadIdx.x;
+  for (int b = t; b < kShBins; b += kShBlock) h[b] = 0u;
+  __syncthreads();
+  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
+  const uint32_t step = gridDim.x * kShBlock * kShPer;
+  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += step) {
+    int32_t li[kShPer];
+    float v[kShPer];
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u) {
+      const uint32_t e = e0 + u * kShBlock;
+      uint32_t w, j;
+      split_entry(e < N ? e : e0, cap, w, j);
+      li[u] = rec_idx(a, w)[j];
+      v[u] = rec_vals(a, w)[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u)
+      if (e0 + u * kShBlock < N && li[u] >= 0) atomicAdd(&h[abs_key(v[u]) >> 16], 1u);
+  }
+  __syncthreads();
+  for (int b = t; b < kShBins; b += kShBlock) {
+    const uint32_t c = h[b];
+    if (c) atomicAdd(&a.hist[b], c);
+  }
+  // arrival (DESIGN §4 memory-model table, row 1: device atomics, vmcnt(0), barrier, one ticket)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(&a.ctl->ticket1, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  // last workgroup: the merged histogram into LDS (agent-scope loads), the global one re-zeroed
+  uint32_t tot = 0;
+  for (int b = t; b < kShBins; b += kShBlock) {
+    const uint32_t c = __hip_atomic_load(&a.hist[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h[b] = c;
+    tot += c;
+    a.hist[b] = 0u;
+  }
+  uint32_t total;
+  block_excl_scan<kShBlock>(tot, s_w, &total);   // also a barrier: h complete
+  const uint32_t k = (uint32_t)a.k;
+  int b1 = -1;
+  uint32_t above = total;
+  if (total > k) {
+    const uint32_t rank[1] = {k};
+    int d[1];
+    uint32_t ab[1];
+    find_bins_desc<kShBlock, kShBins, 1>(h, rank, s_w, s_res, d, ab);
+    b1 = d[0];
+    above = ab[0];
+  }
+  if (t == 0) {
+    a.ctl->b1 = b1;
+    a.ctl->above = above;
+    a.ctl->need = b1 < 0 ? 0u : k - above;
+    a.ctl->ticket1 = 0u;
+  }
+  // the partition every rank planned with vs the shard lengths the records carry
+  uint32_t bad = 0;
+  for (int w = t; w < a.world; w += kShBlock)
+    if ((int64_t)(uint32_t)a.recs[(int64_t)w * a.stride] != a.tab[w]) bad = 1u;
+  if (total < k) bad |= 2u;   // fewer valid entries than k (only after a repartition)
+  bad = __ballot(bad & 1u) ? 1u : 0u;
+  if (a.status && (t & 63) == 0 && bad) __hip_atomic_fetch_or(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.status && t == 0 && total < k) __hip_atomic_fetch_or(a.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the decision for one entry: dense output, and for this rank's entries pay_idx and the residual
+__device__ __forceinline__ void shard_take(const ShArgs& a, bool sel, uint32_t w, uint32_t j, int32_t li, float v,
+                                           int64_t gbase) {
+  const int64_t gi = gbase + li;
+  if (sel) {
+    const int64_t o = gi - a.out_base;
+    if (o >= 0 && o < a.out_len) a.out[o] = 0.f + v;
+  }
+  if ((int32_t)w == a.rank) {
+    a.pay_idx[j] = sel ? (int32_t)gi : -1;
+    if (!sel) a.r[li] = v;   // the local engine zeroed it (r' = t - t); the global cut rejects it: r' = t
+  }
+}
+
+struct BndComp {   // composite key of boundary entry j (agent-scope load of the list)
+  const ShArgs* a;
+  const int64_t* base;
+  __device__ uint64_t operator()(int64_t jj) const {
+    const uint32_t e = __hip_atomic_load(&a->bnd[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t w, j;
+    split_entry(e, (uint32_t)a->cap, w, j);
+    const int64_t gi = base[w] + rec_idx(*a, w)[j];
+    return comp_key(abs_key(rec_vals(*a, w)[j]), (uint32_t)gi);
+  }
+};
+
+// 4. apply the cut: above B selected, below rejected, bin B listed and ranked by the last arriver
+__global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
+  __shared__ int64_t s_base[kShMaxWorld];
+  __shared__ uint32_t hsel[2048];
+  __shared__ uint32_t s_w[kShBlock / kWave + 1];
+  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_last;
+  const int t = threadIdx.x;
+  for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
+  const int32_t b1 = a.ctl->b1;         // written by shard_hist (kernel boundary)
+  const uint32_t need = a.ctl->need;
+  __syncthreads();
+  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
+  const uint32_t step = gridDim.x * kShBlock * kShPer;
+  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += step) {
+    int32_t li[kShPer];
+    float v[kShPer];
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u) {
+      const uint32_t e = e0 + u * kShBlock;
+      uint32_t w, j;
+      split_entry(e < N ? e : e0, cap, w, j);
+      li[u] = rec_idx(a, w)[j];
+      v[u] = rec_vals(a, w)[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u) {
+      const uint32_t e = e0 + u * kShBlock;
+      bool inb = false;
+      if (e < N) {
+        uint32_t w, j;
+        split_entry(e, cap, w, j);
+        if (li[u] < 0) {
+          if ((int32_t)w == a.rank) a.pay_idx[j] = -1;
+        } else {
+          const int kb = (int)(abs_key(v[u]) >> 16);
+          inb = kb == b1;
+          if (!inb) shard_take(a, kb > b1, w, j, li[u], v[u], s_base[w]);
+        }
+      }
+      // boundary entries: one atomic per wave, write-through (sc1) stores for the last arriver
+      const uint64_t m = __ballot(inb);
+      if (m) {
+        uint32_t base0 = 0;
+        if (lane_rank(m) == 0 && inb) base0 = atomicAdd(&a.ctl->nb, (uint32_t)__popcll(m));
+        const int leader = __builtin_ctzll(m);
+        base0 = __shfl(base0, leader, 64);
+        if (inb) __hip_atomic_store(&a.bnd[base0 + lane_rank(m)], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(&a.ctl->ticket2, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  const uint32_t nb = __hip_atomic_load(&a.ctl->nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // T: exactly `need` of the nb boundary entries have composite >= T (unique composites)
+  uint64_t T;
+  if (need == 0u) {
+    T = ~0ull;
+  } else if (need >= nb) {
+    T = 0ull;
+  } else {
+    const BndComp src{&a, s_base};
+    // every boundary entry shares key >> 16 = b1, i.e. composite bits 63..48: start at pass 1
+    const uint64_t p0 = ((uint64_t)(uint32_t)b1 << 48) & (0x7FFull << 53);
+    T = block_select_comp<kShBlock>(src, (int64_t)nb, need, hsel, s_w, s_res, 1, p0, 0x7FFull << 53);
+  }
+  for (uint32_t jj = t; jj < nb; jj += kShBlock) {
+    const uint32_t e = __hip_atomic_load(&a.bnd[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t w, j;
+    split_entry(e, cap, w, j);
+    const int32_t li = rec_idx(a, w)[j];
+    const float v = rec_vals(a, w)[j];
+    const int64_t gi = s_base[w] + li;
+    shard_take(a, comp_key(abs_key(v), (uint32_t)gi) >= T, w, j, li, v, s_base[w]);
+  }
+  if (t == 0) {
+    a.ctl->nb = 0u;
+    a.ctl->ticket2 = 0u;
+  }
+}
+
+static size_t sh_ws_bytes(int64_t world, int64_t cap) {
+  return 256 + sizeof(uint32_t) * kShBins + ((sizeof(uint32_t) * world * cap + 255) & ~(size_t)255);
+}
+
+}  // namespace grace
+
+using namespace grace;
+
+extern "C" {
+
+size_t grace_shard_record_words(int64_t cap) { return (size_t)(kShHdr + 2 * cap); }
+
+size_t grace_shard_select_workspace_bytes(int32_t world, int64_t cap) { return sh_ws_bytes(world, cap); }
+
+grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t rank, int64_t cap, const int64_t* tab,
+                                  int64_t k, float* residual, float* out, int64_t out_base, int64_t out_len,
+                                  int32_t* pay_idx, void* ws, size_t ws_bytes, int32_t* status_host, void* stream) {
+  GRACE_REQUIRE(recs && tab && residual && out && pay_idx && ws && world >= 1 && world <= kShMaxWorld &&
+                    rank >= 0 && rank < world && cap >= 1 && k >= 1 && out_base >= 0 && out_len >= 0 &&
+                    (int64_t)world * cap < ((int64_t)1 << 31),
+                "grace_shard_select: bad arguments");
+  GRACE_REQUIRE(ws_bytes >= sh_ws_bytes(world, cap), "grace_shard_select: workspace too small");
+  char* p = reinterpret_cast<char*>(ws);
+  ShArgs a;
+  a.recs = recs;
+  a.stride = kShHdr + 2 * cap;
+  a.cap = cap;
+  a.world = world;
+  a.rank = rank;
+  a.tab = tab;
+  a.k = k;
+  a.r = residual;
+  a.out = out;
+  a.out_base = out_base;
+  a.out_len = out_len;
+  a.pay_idx = pay_idx;
+  a.ctl = reinterpret_cast<ShCtl*>(p);
+  a.hist = reinterpret_cast<uint32_t*>(p + 256);
+  a.bnd = reinterpret_cast<uint32_t*>(p + 256 + sizeof(uint32_t) * kShBins);
+  a.status = status_host;
+  const int64_t N = (int64_t)world * cap;
+  int64_t g = (N + kShBlock * kShPer - 1) / (kShBlock * kShPer);
+  const unsigned grid = (unsigned)(g < 1 ? 1 : (g > kShMaxGrid ? kShMaxGrid : g));
+  hipStream_t s = as_stream(stream);
+  shard_hist_kernel<<<grid, kShBlock, 0, s>>>(a);
+  GRACE_CHECK_LAUNCH("grace_shard_select");
+  shard_apply_kernel<<<grid, kShBlock, 0, s>>>(a);
+  GRACE_CHECK_LAUNCH("grace_shard_select");
+  return GRACE_OK;
+}
+
+}  // extern "C"

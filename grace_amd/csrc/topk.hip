@@ -125,7 +125,6 @@ static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 #endif
 #define STAMP(ctlp, slot) STAMP_IF(blockIdx.x == 0, ctlp, slot)
 
-constexpr int kXcnt = 8;                                   // sharded exchange counters
 #ifndef GRACE_SAMPLE_MAX
 #define GRACE_SAMPLE_MAX 131072
 #endif
@@ -156,7 +155,6 @@ struct TopkWs {
   int2* cand;
   int2* bnd;
   int64_t cap;
-  uint32_t* xcnt;      // sharded mode: [n_sure, n_cand, shard length] of this rank, exchanged after the main pass
 };
 
 static inline int64_t topk_cap(int64_t n, int64_t k) {
@@ -181,7 +179,6 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   w.cand = reinterpret_cast<int2*>(p);
   p += align256(sizeof(int2) * w.cap);
   w.bnd = reinterpret_cast<int2*>(p);
-  w.xcnt = nullptr;
   return w;
 }
 
@@ -271,7 +268,6 @@ struct StepArgs {
   float* out;          // dense output (kDenseFused, kDenseOut)
   int64_t sample_n;    // stratified sample size (<= kSampleMax)
   int64_t stratum;     // n / sample_n
-  int64_t idx_base;    // sharded mode: global index of this shard's element 0 (payload indices)
   // residual-sample carry (grace_topk_residual_step_carry), f32[sample_n + 2]: the bracket writes
   // the step's t[pos(s)] to rs_out[s] (it computes them anyway), the finalize writes the step's
   // composite selection threshold (selected <=> comp_key >= T) as a u64 at rs_out + sample_n;
@@ -327,130 +323,6 @@ constexpr double kSampleSigma = GRACE_SAMPLE_SIGMA;        // bracket half-width
 constexpr int kSamplePer = GRACE_SAMPLE_PER;               // samples per thread: 1 is fastest --
                                                            // the strided samples are latency-bound
                                                            // random loads that want many waves
-
-template <bool HAS_RES>
-__global__ __launch_bounds__(kSampleBlock) void topk_sample(StepArgs a, TopkWs w) {
-  __shared__ uint32_t lh[kBracketBins];
-  const int tid = threadIdx.x;
-  STAMP(w.ctl, 0);
-  // issue every sample load first: their latency hides the LDS clear
-  const uint32_t st = (uint32_t)a.stratum;
-  float t[kSamplePer];
-  bool valid[kSamplePer];
-#pragma unroll
-  for (int p = 0; p < kSamplePer; ++p) {
-    const int64_t sidx = ((int64_t)blockIdx.x * kSamplePer + p) * kSampleBlock + tid;
-    valid[p] = sidx < a.sample_n;
-    t[p] = 0.f;
-    if (valid[p]) {
-      const uint32_t off = (uint32_t)(((uint64_t)hash32((uint32_t)sidx * 0x9E3779B9u + 0x5EEDu) * st) >> 32);
-      t[p] = compensate<HAS_RES>(a, sidx * (int64_t)st + off);
-    }
-  }
-  for (int b = tid; b < kBracketBins; b += kSampleBlock) lh[b] = 0;
-  __syncthreads();
-  STAMP(w.ctl, 1);
-#pragma unroll
-  for (int p = 0; p < kSamplePer; ++p)
-    if (valid[p]) atomicAdd(&lh[abs_key(t[p]) >> 16], 1u);
-  __syncthreads();
-  for (int b = tid; b < kBracketBins; b += kSampleBlock)
-    if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
-  STAMP(w.ctl, 2);
-}
-
-// Conflict-free chunk sums of an LDS histogram: thread t owns bins [PER*t, PER*t+PER) but reads
-// them in a lane-rotated order so the 32 lanes of a half-wave hit 32 different banks.
-template <int BLOCK, int NBINS>
-__device__ __forceinline__ uint32_t chunk_sum_rot(const uint32_t* h, int t) {
-  constexpr int PER = NBINS / BLOCK;
-  uint32_t s = 0;
-#pragma unroll 8
-  for (int j = 0; j < PER; ++j) s += h[t * PER + ((j + t) & (PER - 1))];
-  return s;
-}
-
-// select body: lh = the whole sample histogram in LDS (kSelBlock threads)
-__device__ void bracket_select(const StepArgs& a, const TopkWs& w, uint32_t* lh) {
-  constexpr int PER = kBracketBins / kSelBlock;   // 32
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_res[4];
-  const int tid = threadIdx.x;
-  const int64_t S = a.sample_n;
-  // sample ranks (descending, 0-based) bracketing the k-th largest with ~6 sigma
-  const double p = (double)a.k / (double)a.n;
-  const double mu = p * (double)S;
-  const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
-  const int64_t rank_hi = (int64_t)floor(mu - kSampleSigma * sd - 2.0);   // < 0: nothing is "sure"
-  const int64_t rank_lo = (int64_t)ceil(mu + kSampleSigma * sd + 2.0);    // >= S: everything a candidate
-  const uint32_t r1[2] = {(uint32_t)((rank_hi < 0 ? 0 : (rank_hi >= S ? S - 1 : rank_hi)) + 1),
-                          (uint32_t)((rank_lo < 0 ? 0 : (rank_lo >= S ? S - 1 : rank_lo)) + 1)};
-  // descending scan: thread t owns the chunk of bins [PER*(NT-1-t), PER*(NT-1-t)+PER)
-  const int chunk = kSelBlock - 1 - tid;
-  const uint32_t sum = chunk_sum_rot<kSelBlock, kBracketBins>(lh, chunk);
-  __shared__ uint32_t s_fc[4];   // owning chunk and the count above it, per target rank
-  if (tid < 4) { s_res[tid] = 0; s_fc[tid] = 0; }
-  const uint32_t ex = block_excl_scan<kSelBlock>(sum, s_w, nullptr);
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-    if (ex < r1[q] && r1[q] <= ex + sum) { s_fc[2 * q] = (uint32_t)chunk; s_fc[2 * q + 1] = ex; }
-  __syncthreads();
-  // the bin inside the owning chunk: one half-wave per target, inclusive scan of its 32 bins
-  // (descending) and the first lane whose running count reaches the rank
-  static_assert(PER == 32, "one half-wave per chunk");
-  if (tid < 64) {
-    const int q = tid >> 5, j = tid & 31;
-    const uint32_t bin = s_fc[2 * q] * PER + (PER - 1 - j);
-    uint32_t v = lh[bin];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      const uint32_t t = __shfl_up(v, o, 32);
-      if (j >= o) v += t;
-    }
-    const uint32_t hm = (uint32_t)(__ballot(s_fc[2 * q + 1] + v >= r1[q]) >> (32 * q));
-    if (j == __ffs(hm) - 1) s_res[q] = bin;
-  }
-  __syncthreads();
-  const uint32_t d0 = s_res[0], d1 = s_res[1];
-  // re-zero the state the next kernels accumulate into
-  for (int b = tid; b < kHistBins; b += kSelBlock) w.hist[b * kHistStride] = 0;
-  if (tid < (int)(sizeof(TopkCtl) / 4)) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
-  if (w.xcnt && tid < kXcnt) w.xcnt[tid] = 0u;
-  __syncthreads();
-  if (tid == 0) {
-    // sure = key > hi: round up to the top of the bin (fewer sure); candidates start at the bottom
-    // of the low bin (more candidates)
-    uint32_t hi = (d0 << 16) | 0xFFFFu;
-    uint32_t lo = d1 << 16;
-    if (rank_hi < 0) hi = 0x7FFFFFFFu;
-    if (rank_lo >= S) lo = 0u;
-    if (lo > hi) lo = hi;
-    uint32_t sh = 0;
-    const uint64_t span = (uint64_t)hi - (uint64_t)lo;   // keys lo..hi -> bins 0..span>>sh
-    while ((span >> sh) >= (uint64_t)kHistBins) ++sh;
-    w.ctl->thr_lo = lo;
-    w.ctl->thr_hi = hi;
-    w.ctl->shift = sh;
-  }
-}
-
-__global__ __launch_bounds__(kSelBlock) void topk_select(StepArgs a, TopkWs w) {
-  __shared__ uint32_t lh[kBracketBins];
-  const int tid = threadIdx.x;
-  STAMP(w.ctl, 3);
-  // coalesced copy of the global sample histogram into LDS, re-zeroing it behind us
-  const uint4* gh = reinterpret_cast<const uint4*>(w.shist);
-  uint4* lh4 = reinterpret_cast<uint4*>(lh);
-#pragma unroll
-  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) lh4[tid + j * kSelBlock] = gh[tid + j * kSelBlock];
-  __syncthreads();
-  uint4* gz = reinterpret_cast<uint4*>(w.shist);
-#pragma unroll
-  for (int j = 0; j < kBracketBins / 4 / kSelBlock; ++j) gz[tid + j * kSelBlock] = make_uint4(0, 0, 0, 0);
-  STAMP(w.ctl, 4);
-  bracket_select(a, w, lh);
-  STAMP(w.ctl, 5);
-}
 
 // Single-GPU bracket: sample + select in ONE launch.  The sample workgroups count their keys into
 // a fine (key >> 16, 32768 bins) and a coarse (key >> 20, 2048 bins) LDS histogram and flush both
@@ -745,7 +617,7 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
         if ((msel >> b) & 1u) {
           const int64_t i = gbase + (int64_t)u * (kMainBlock * 4) + j;
           const float tv = comp4(t[u], j);
-          const int2 e = make_int2((int)(i + a.idx_base), (int)f2u(tv));
+          const int2 e = make_int2((int)i, (int)f2u(tv));
           if ((msure >> b) & 1u) {
             if (ps < (uint32_t)kStage) {
               sm.sure[ps] = e;
@@ -818,11 +690,6 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
     sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
     sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
   }
-  if (w.xcnt && tid == 1) {   // sharded mode: totals incl. the overflowed (spilled) entries
-    const uint32_t all = sm.cnt[0];
-    if (all & 0xFFFFu) atomicAdd(&w.xcnt[0], all & 0xFFFFu);
-    if (all >> 16) atomicAdd(&w.xcnt[1], all >> 16);
-  }
   __syncthreads();
   for (uint32_t j = tid; j < ns; j += kMainBlock) {
     const uint32_t gp = sm.cnt[1] + j;
@@ -850,9 +717,6 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   const int64_t nchunks = (a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>;
-  // sharded mode: this rank's shard length rides in the exchanged counters, so every rank can
-  // check the shard sizes it planned with (grace_amd/dist/sharded.py)
-  if (w.xcnt && blockIdx.x == 0 && tid == 0) w.xcnt[2] = (uint32_t)a.n;
   __syncthreads();
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
@@ -1528,211 +1392,6 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
 }
 
 // ------------------------------------------------------------------------------------------------
-// Sharded top-k (BASELINE configs[4]): one bucket split into W contiguous shards,
-// one per rank; the union of the ranks' payloads is exactly the single-GPU top-k of the whole
-// bucket (same (|t| desc, global index asc) rule).  Per step, driven by grace_amd/dist/sharded.py:
-//   sample (local, into the exchange histogram xs) -> all_reduce(xs) -> select (global bracket)
-//   -> main (local RES pass, global indices, local histogram + counts into xh) -> all_gather(xh)
-//   -> host: boundary bin B, need, list capacities -> route (above-B to the payload, bin-B to a
-//   list) -> all_gather(lists) -> boundary (exact global selection of `need` in bin B; this
-//   rank's winners join its payload, payload padded with idx -1) -> all_gather(payloads) ->
-//   scatter-range decode.
-// The residual buffer holds t for every element after the main pass (RES mode), which is what
-// the exact fallback (bracket miss: all_gather t, single-GPU select) starts from.
-
-// route: local candidates above bin B -> payload (after the local sure entries), bin B -> bsend
-// list [count, pad, entries...]; the residual of every payload entry (sure + above) is zeroed.
-__global__ __launch_bounds__(kSelBlock) void topk_shard_route(StepArgs a, TopkWs w, int B, int64_t* bsend) {
-  const TopkCtl c = *w.ctl;
-  const int t = threadIdx.x;
-  const int64_t base = a.idx_base;
-  const uint32_t stride = gridDim.x * kSelBlock;
-  for (uint32_t j0 = blockIdx.x * kSelBlock + t; j0 < c.n_sure; j0 += stride * kFinPer) {
-    float v[kFinPer];
-    int32_t ix[kFinPer];
-#pragma unroll
-    for (int u = 0; u < kFinPer; ++u) {   // every load before any store (no dependent chains)
-      const uint32_t j = j0 + u * stride < c.n_sure ? j0 + u * stride : j0;
-      v[u] = a.vals[j];
-      ix[u] = a.idx[j];
-    }
-#pragma unroll
-    for (int u = 0; u < kFinPer; ++u)
-      if (j0 + u * stride < c.n_sure) a.r[ix[u] - base] = v[u] - v[u];
-  }
-  int2* blist = reinterpret_cast<int2*>(bsend + 1);
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_base[2];
-  // contiguous slice per workgroup; one block scan places the round, one atomic per list reserves
-  const uint32_t per = (c.n_cand + gridDim.x - 1) / gridDim.x;
-  const uint32_t b0 = blockIdx.x * per, b1 = min(c.n_cand, b0 + per);
-  for (uint32_t j0 = b0; j0 < b1; j0 += kSelBlock) {
-    const uint32_t j = j0 + t;
-    int2 e = make_int2(0, 0);
-    int bin = -1;
-    if (j < b1) {
-      e = w.cand[j];
-      bin = (int)((abs_key(u2f((uint32_t)e.y)) - c.thr_lo) >> c.shift);
-    }
-    const uint32_t packed = (bin > B ? 1u : 0u) | ((bin == B ? 1u : 0u) << 16);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kSelBlock>(packed, s_w, &tot);
-    if (t == 0) {
-      s_base[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
-      s_base[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
-    }
-    __syncthreads();
-    if (bin > B) {
-      const uint32_t pos = c.n_sure + s_base[0] + (ex & 0xFFFFu);
-      const float v = u2f((uint32_t)e.y);
-      a.vals[pos] = v;
-      a.idx[pos] = e.x;
-      a.r[e.x - base] = v - v;
-    } else if (bin == B) {
-      blist[s_base[1] + (ex >> 16)] = e;
-    }
-    __syncthreads();
-  }
-  // the list count: written by the last workgroup to finish (ticket), after every entry
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ uint32_t s_last;
-  if (t == 0) s_last = atomicAdd(&w.ctl->ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (s_last && t == 0) bsend[0] = (int64_t)__hip_atomic_load(&w.ctl->n_bacc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// boundary: the W gathered bin-B lists (segment w at brecv + w * (cap_b + 1) int64 words: count,
-// then entries) hold every element of bin B; the `need` best by (|t| desc, index asc) are
-// selected exactly; this rank's winners are appended to its payload (residual zeroed), and the
-// payload [count, cap_p) is padded with idx -1.
-struct ShardList {
-  const int64_t* recv;
-  int64_t seg;          // words per rank segment
-  int world;
-  const uint32_t* off;  // LDS prefix offsets [world + 1]
-  __device__ int2 at(int64_t j) const {
-    int w = 0;
-    while (w + 1 < world && (int64_t)off[w + 1] <= j) ++w;
-    const int2* l = reinterpret_cast<const int2*>(recv + w * seg + 1);
-    return l[j - off[w]];
-  }
-};
-
-__global__ __launch_bounds__(kSelBlock) void topk_shard_boundary(StepArgs a, TopkWs w, const int64_t* brecv,
-                                                                int world, int64_t cap_b, uint32_t need,
-                                                                int64_t cap_p) {
-  __shared__ uint32_t s_off[65];
-  __shared__ uint64_t s_comp[kSelBlock];
-  __shared__ uint32_t hist[2048];
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_pos;
-  const int t = threadIdx.x;
-  const int64_t seg = cap_b + 1;
-  if (t == 0) {
-    uint32_t acc = 0;
-    for (int q = 0; q < world; ++q) { s_off[q] = acc; acc += (uint32_t)brecv[q * seg]; }
-    s_off[world] = acc;
-    s_pos = w.ctl->n_sure + w.ctl->n_sel;
-  }
-  __syncthreads();
-  const uint32_t nb = s_off[world];
-  const ShardList L{brecv, seg, world, s_off};
-  const int64_t base = a.idx_base, m = a.n;
-  auto take = [&](int2 e) {
-    const int64_t gi = e.x;
-    if (gi >= base && gi < base + m) {
-      const uint32_t p = atomicAdd(&s_pos, 1u);
-      const float v = u2f((uint32_t)e.y);
-      a.vals[p] = v;
-      a.idx[p] = e.x;
-      a.r[gi - base] = v - v;
-    }
-  };
-  if (need > 0) {
-    if (nb <= (uint32_t)kSelBlock) {
-      int2 e = make_int2(0, 0);
-      uint64_t me = 0;
-      if (t < (int)nb) {
-        e = L.at(t);
-        me = comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
-        s_comp[t] = me;
-      }
-      __syncthreads();
-      if (t < (int)nb) {
-        uint32_t rank = 0;
-        for (uint32_t q = 0; q < nb; ++q) rank += s_comp[q] > me;
-        if (rank < need) take(e);
-      }
-    } else {
-      auto src = [L](int64_t j) {
-        const int2 e = L.at(j);
-        return comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x);
-      };
-      const uint64_t T = block_select_comp(src, nb, need, hist, s_w, s_res);
-      for (uint32_t j = t; j < nb; j += kSelBlock) {
-        const int2 e = L.at(j);
-        if (comp_key(abs_key(u2f((uint32_t)e.y)), (uint32_t)e.x) >= T) take(e);
-      }
-    }
-  }
-  __syncthreads();
-  const uint32_t cnt = s_pos;
-  for (int64_t j = cnt + t; j < cap_p; j += kSelBlock) {
-    a.vals[j] = 0.f;
-    a.idx[j] = -1;
-  }
-  if (t == 0) w.ctl->n_bnd = cnt;   // this rank's payload count (diagnostics)
-}
-
-// exact fallback: from the whole bucket's exact selection (vals_all / idx_all, k entries), take
-// this rank's entries in order into its payload, zero their residual, pad to cap_p with idx -1
-__global__ __launch_bounds__(kSelBlock) void topk_shard_take(const float* vals_all, const int32_t* idx_all,
-                                                            int64_t k, StepArgs a, int64_t cap_p) {
-  __shared__ uint32_t s_w[kSelBlock / kWave + 1];
-  const int64_t base = a.idx_base, m = a.n;
-  uint32_t run = 0;
-  for (int64_t j0 = 0; j0 < k; j0 += kSelBlock) {
-    const int64_t j = j0 + threadIdx.x;
-    bool mine = false;
-    int32_t gi = 0;
-    float v = 0.f;
-    if (j < k) {
-      gi = idx_all[j];
-      v = vals_all[j];
-      mine = gi >= base && gi < base + m;
-    }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kSelBlock>(mine ? 1u : 0u, s_w, &tot);
-    if (mine && run + ex < (uint64_t)cap_p) {
-      a.vals[run + ex] = v;
-      a.idx[run + ex] = gi;
-      a.r[gi - base] = v - v;
-    }
-    run += tot;
-  }
-  for (int64_t j = run + threadIdx.x; j < cap_p; j += kSelBlock) {
-    a.vals[j] = 0.f;
-    a.idx[j] = -1;
-  }
-}
-
-// dense decode of gathered padded payloads (rank w's entries at vals/idx + w * stride, `per` of
-// them): out[idx - base] = 0 + v for base <= idx < base + len (idx -1 = padding); out must be
-// zero-filled first.  Indices are unique across ranks, so the order of the writes is irrelevant.
-__global__ void scatter_range_kernel(const float* __restrict__ vals, const int32_t* __restrict__ idx,
-                                     int64_t stride, int64_t per, int world, int64_t base, int64_t len,
-                                     float* __restrict__ out) {
-  const int64_t count = per * world;
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < count;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t w = j / per, q = j - w * per;
-    const int64_t gi = idx[w * stride + q];
-    if (gi >= base && gi < base + len) out[gi - base] = 0.f + vals[w * stride + q];
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // sparse decode / aggregate
 __global__ void scatter_kernel(const float* vals, const int32_t* idx, int64_t count, float* out) {
@@ -1789,6 +1448,12 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
     return GRACE_ERR_HIP;
   }
   return GRACE_OK;
+}
+
+int32_t grace_status_take(int32_t* host_word) {
+  // a host-side atomic exchange: a device fetch_or (system scope, over PCIe) that lands between
+  // a plain read and a plain clear would otherwise be lost
+  return host_word ? __atomic_exchange_n(host_word, 0, __ATOMIC_SEQ_CST) : 0;
 }
 
 grace_status_t grace_timer_enable(int enable) {
@@ -1999,132 +1664,5 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
 }
 
 
-size_t grace_topk_shard_xs_words(void) { return (size_t)kBracketBins; }
-size_t grace_topk_shard_xh_words(void) { return (size_t)(kHistBins + kXcnt); }
-
-static TopkWs shard_ws(void* ws, int64_t m, int64_t k, uint32_t* xs, uint32_t* xh) {
-  TopkWs w = carve(ws, m, k);
-  if (xs) w.shist = xs;
-  if (xh) {
-    w.hist = xh;
-    w.xcnt = xh + kHistBins;
-  }
-  return w;
-}
-
-grace_status_t grace_topk_shard_sample(const float* g, float* residual, int32_t has_residual, float beta,
-                                       float gamma, int64_t m, int64_t stratum, uint32_t* xs, void* stream) {
-  GRACE_REQUIRE(g && xs && m > 0 && stratum >= 1 && (!has_residual || residual),
-                "grace_topk_shard_sample: bad arguments");
-  StepArgs a{g, residual, beta, gamma, m, 1, nullptr, nullptr, nullptr};
-  a.stratum = stratum;
-  a.sample_n = m / stratum;
-  if (a.sample_n == 0) return GRACE_OK;
-  TopkWs w{};
-  w.shist = xs;
-  const unsigned grid = (unsigned)((a.sample_n + kSampleBlock * kSamplePer - 1) / (kSampleBlock * kSamplePer));
-  if (has_residual) topk_sample<true><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
-  else topk_sample<false><<<grid, kSampleBlock, 0, as_stream(stream)>>>(a, w);
-  GRACE_CHECK_LAUNCH("grace_topk_shard_sample");
-  return GRACE_OK;
-}
-
-grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t has_residual, float beta,
-                                     float gamma, int64_t m, int64_t idx_base, int64_t n_global, int64_t k,
-                                     int64_t sample_total, float* vals, int32_t* idx, void* ws, size_t ws_bytes_,
-                                     uint32_t* xs, uint32_t* xh, void* stream) {
-  GRACE_REQUIRE(g && residual && vals && idx && ws && xs && xh && m > 0 && k >= 1 && k <= n_global &&
-                    n_global < ((int64_t)1 << 31) && idx_base >= 0 && idx_base + m <= n_global &&
-                    sample_total >= 1,
-                "grace_topk_shard_main: bad arguments");
-  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_main: workspace too small");
-  hipStream_t s = as_stream(stream);
-  TopkWs w = shard_ws(ws, m, k, xs, xh);
-  StepArgs sel{g, residual, beta, gamma, n_global, k, vals, idx, nullptr};
-  sel.sample_n = sample_total;
-  topk_select<<<1, kSelBlock, 0, s>>>(sel, w);   // global bracket; re-zeroes xs, xh and the local state
-  GRACE_CHECK_LAUNCH("grace_topk_shard_main");
-  StepArgs a{g, residual, beta, gamma, m, k, vals, idx, nullptr};
-  a.idx_base = idx_base;
-  const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual)) & 15u) == 0;
-  unsigned nblk = (unsigned)((m + kChunkOf<true, kDenseRes> - 1) / kChunkOf<true, kDenseRes>);
-  if (!has_residual) nblk = (unsigned)((m + kChunkOf<false, kDenseRes> - 1) / kChunkOf<false, kDenseRes>);
-#ifdef GRACE_MAIN_PERSIST
-  if (nblk > (unsigned)GRACE_MAIN_PERSIST) nblk = GRACE_MAIN_PERSIST;
-#endif
-  if (has_residual) {
-    if (vec) launch_timed(topk_main<true, kDenseRes, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
-    else launch_timed(topk_main<true, kDenseRes, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
-  } else {
-    if (vec) launch_timed(topk_main<false, kDenseRes, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
-    else launch_timed(topk_main<false, kDenseRes, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
-  }
-  GRACE_CHECK_LAUNCH("grace_topk_shard_main");
-  return GRACE_OK;
-}
-
-grace_status_t grace_topk_shard_route(float* residual, int64_t m, int64_t idx_base, int64_t k,
-                                      int32_t boundary_bin, float* vals, int32_t* idx, void* ws,
-                                      size_t ws_bytes_, int64_t* bsend, void* stream) {
-  GRACE_REQUIRE(residual && vals && idx && ws && bsend && m > 0 && k >= 1,
-                "grace_topk_shard_route: bad arguments");
-  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_route: workspace too small");
-  TopkWs w = carve(ws, m, k);
-  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
-  a.idx_base = idx_base;
-  topk_shard_route<<<kFinBlocks, kSelBlock, 0, as_stream(stream)>>>(a, w, boundary_bin, bsend);
-  GRACE_CHECK_LAUNCH("grace_topk_shard_route");
-  return GRACE_OK;
-}
-
-grace_status_t grace_topk_shard_boundary(float* residual, int64_t m, int64_t idx_base, int64_t k,
-                                         const int64_t* brecv, int32_t world, int64_t cap_b, uint32_t need,
-                                         float* vals, int32_t* idx, int64_t cap_p, void* ws, size_t ws_bytes_,
-                                         void* stream) {
-  GRACE_REQUIRE(residual && vals && idx && ws && brecv && m > 0 && world >= 1 && world <= 64 && cap_b >= 0 &&
-                    cap_p >= 0,
-                "grace_topk_shard_boundary: bad arguments");
-  GRACE_REQUIRE(ws_bytes_ >= ws_bytes(m, k), "grace_topk_shard_boundary: workspace too small");
-  TopkWs w = carve(ws, m, k);
-  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
-  a.idx_base = idx_base;
-  topk_shard_boundary<<<1, kSelBlock, 0, as_stream(stream)>>>(a, w, brecv, world, cap_b, need, cap_p);
-  GRACE_CHECK_LAUNCH("grace_topk_shard_boundary");
-  return GRACE_OK;
-}
-
-grace_status_t grace_topk_shard_take(const float* vals_all, const int32_t* idx_all, int64_t k, float* residual,
-                                     int64_t m, int64_t idx_base, float* vals, int32_t* idx, int64_t cap_p,
-                                     void* stream) {
-  GRACE_REQUIRE(vals_all && idx_all && residual && vals && idx && k >= 1 && m > 0 && cap_p >= 0,
-                "grace_topk_shard_take: bad arguments");
-  StepArgs a{nullptr, residual, 1.f, 1.f, m, k, vals, idx, nullptr};
-  a.idx_base = idx_base;
-  topk_shard_take<<<1, kSelBlock, 0, as_stream(stream)>>>(vals_all, idx_all, k, a, cap_p);
-  GRACE_CHECK_LAUNCH("grace_topk_shard_take");
-  return GRACE_OK;
-}
-
-grace_status_t grace_topk_shard_read(const void* ws, uint32_t* ctl_host, void* stream) {
-  GRACE_REQUIRE(ws && ctl_host, "grace_topk_shard_read: bad arguments");
-  hipError_t e = hipMemcpyAsync(ctl_host, ws, sizeof(TopkCtl), hipMemcpyDeviceToHost, as_stream(stream));
-  if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
-  if (e != hipSuccess) {
-    set_error("grace_topk_shard_read", e);
-    return GRACE_ERR_HIP;
-  }
-  return GRACE_OK;
-}
-
-grace_status_t grace_sparse_scatter_range(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
-                                          int32_t world, int64_t base, int64_t len, float* out, void* stream) {
-  GRACE_REQUIRE(vals && idx && out && per >= 0 && world >= 1 && len >= 0,
-                "grace_sparse_scatter_range: bad arguments");
-  if (per == 0) return GRACE_OK;
-  scatter_range_kernel<<<stream_grid(per * world, 256, 2048), 256, 0, as_stream(stream)>>>(vals, idx, stride, per,
-                                                                                         world, base, len, out);
-  GRACE_CHECK_LAUNCH("grace_sparse_scatter_range");
-  return GRACE_OK;
-}
 
 }  // extern "C"

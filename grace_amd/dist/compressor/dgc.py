@@ -18,15 +18,18 @@ exchange, as for ThresholdCompressor:
     fixed-size record per rank (capacity = the largest count) moves in one all-gather;
   * ``exchange="capacity"``: the record capacity is the name's previous largest count x
     ``capacity_margin``, so the common step reads nothing on the host.  On overflow (a rank selected
-    more than the capacity) ``overflow="defer"`` (default) sends the first ``cap`` entries in index
+    more than the capacity) ``overflow="retry"`` (default) reads the stat once at the end of the step
+    and redoes an overflowing step through the counts exchange (bit-exact always, like Threshold);
+    ``overflow="defer"`` sends the first ``cap`` entries in index
     order and leaves the rest in the momentum memory -- DgcMemory.update zeroes r and a only where an
     entry travelled, so the unsent ones are selected again later (error feedback); the overflow stat
-    is copied asynchronously and grows the capacity at the name's next step.  ``overflow="retry"``
-    reads the stat once at the end of the step and redoes an overflowing step through the counts
-    exchange (bit-exact always).
+    is copied asynchronously and grows the capacity at the name's next step (a departure from the
+    reference step, so it is opt-in and warns once when it first defers).
 Without overflow every mode equals the reference's four calls bit for bit (the decode is the
 rank-ordered scatter-add of sparse.hip, divided once per element).
 """
+import warnings
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -36,8 +39,9 @@ from grace_amd.dist import Compressor
 
 
 class DgcCompressor(Compressor):
+    _warned_defer = False
 
-    def __init__(self, compress_ratio, rng="device", exchange="counts", capacity_margin=1.25, overflow="defer"):
+    def __init__(self, compress_ratio, rng="device", exchange="counts", capacity_margin=1.25, overflow="retry"):
         super().__init__(tensors_size_are_same=False)
         if exchange not in ("counts", "capacity") or overflow not in ("retry", "defer"):
             raise ValueError("exchange must be 'counts' or 'capacity', overflow 'retry' or 'defer'")
@@ -96,6 +100,8 @@ class DgcCompressor(Compressor):
                                                       mem.momentum, self.compress_ratio, sample_idx=sidx, seed=seed)
             mem.residuals[name], mem.gradients[name] = r_new, a_new
             return out.view(tensor.shape)
+        if W > 1 and tensor.numel() >= 2 ** 31:
+            return None        # grace_dgc_write_capped indexes with int32: the generic path handles it
         t = ops.dev_f32(mem.compensate(tensor, name))
         sidx, seed = self._sampling(t, name)
         if W == 1:
@@ -118,6 +124,11 @@ class DgcCompressor(Compressor):
         mx, over = (int(v) for v in pinned.tolist())
         if over:
             self.overflows += 1
+            if not DgcCompressor._warned_defer:
+                DgcCompressor._warned_defer = True
+                warnings.warn("grace_amd DgcCompressor(overflow='defer'): a step selected more entries than the "
+                              "record capacity; the unsent ones stay in the momentum memory (not the reference "
+                              "step; use overflow='retry' for bit-exact steps)", RuntimeWarning, stacklevel=3)
         cap = self.capacity.get(name)
         if cap is not None and (over or self._grow(mx, n) * 4 < cap):
             self.capacity[name] = self._grow(mx, n)

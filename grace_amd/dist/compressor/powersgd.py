@@ -21,9 +21,12 @@ def orthogonalize(matrix):
 
 class PowerSGDCompressor(Compressor):
 
-    def __init__(self, rank=1, use_memory=False, world_size=1, rng="device", one_pass=True):
+    def __init__(self, rank=1, use_memory=False, world_size=1, rng="device", one_pass=True, check_sync=False):
         super().__init__()
         self.one_pass = one_pass   # world size 1, rank 4: P and Q from one read of M (psgd_w1_pass)
+        # check_sync: wait for the one-pass kernels after every compress and raise PowerSGDWaitError
+        # on THIS call (default: the next call raises, so the step itself never blocks the host)
+        self.check_sync = check_sync
         self.world_size = world_size
         self.q_memory = {}
         self.rank = rank
@@ -56,6 +59,8 @@ class PowerSGDCompressor(Compressor):
             else:
                 self._step += 1
                 p, q = ops.powersgd_w1_compress(matrix, seed=ops.step_seed("powersgd-q", name, self._step))
+            if self.check_sync:
+                ops.powersgd_w1_check()
             ctx = p, q, shape
             if self.use_memory:
                 self.q_memory[name] = q

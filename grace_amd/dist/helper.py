@@ -27,7 +27,7 @@ def grace_from_params(params):
     comm = params.get('communicator', 'allreduce')
     if comp == 'dgc':
         from grace_amd.dist.compressor.dgc import DgcCompressor
-        compressor = DgcCompressor(params.get('compress_ratio', 0.3), **_exchange_kwargs(params, 'defer'))
+        compressor = DgcCompressor(params.get('compress_ratio', 0.3), **_exchange_kwargs(params, 'retry'))
     elif comp == 'efsignsgd':
         from grace_amd.dist.compressor.efsignsgd import EFSignSGDCompressor
         compressor = EFSignSGDCompressor(params.get('lr', 0.1))

@@ -2,252 +2,205 @@
 one per rank (BASELINE configs[4]: 256 MiB bucket, k = 0.1 %, 8 x MI355X).
 
 The reference has no sharded mode -- its Allgather (grace_dl/dist/communicator/allgather.py:8-45)
-runs every rank on its own full bucket.  Here each rank owns n/W elements and the ranks together
-select exactly the single-GPU top-k of the whole bucket (TopKCompressor, topk.py:32-42, with the
-same tie rule as the single-GPU engine: larger |t| first, lower global index first), keep the
+runs every rank on its own full bucket, and its variable-size gather reads the payload sizes back
+to the host every step (allgather.py:15-18).  Here each rank owns n/W elements and the ranks
+together select exactly the single-GPU top-k of the whole bucket (TopKCompressor, topk.py:32-42,
+with the single-GPU engine's tie rule: larger |t| first, lower global index first), keep the
 residual of their own shard (ResidualMemory, residual.py:10-20) and decode the replicated dense
 bucket (or only their own slice, ``dense="shard"``).
 
-Per step (kernels: grace_amd/csrc/topk.hip, "Sharded top-k"):
-  1. sample this shard's |t| into the shared bracket histogram xs      -> all_reduce(xs)
-  2. global bracket + one streaming pass over the shard (t, r' = t, local candidates)
-                                                                       -> all_gather(xh)
-  3. host: boundary bin B, how many of it are still needed, exact list capacities (one 8 KB/rank
-     read -- the step's only host synchronisation)
-  4. route: sure + above-B entries to the local payload, bin-B entries to a list
-                                                                       -> all_gather(lists)
-  5. boundary: exact global ranking of bin B; winners join their owner's payload
-                                                                       -> all_gather(payloads)
-  6. scatter-range decode into the dense output.
-If the sampled bracket misses (degenerate data: heavy ties, mostly-zero buckets) every rank
-gathers t and runs the exact single-GPU selection instead (same result, slower).
+One collective per step and no host synchronisation (grace_amd/csrc/shard.hip):
+  1. the single-GPU engine selects this shard's own top-k_loc (k_loc = min(k, m); 12 B per element:
+     g, r read, r' written) straight into this rank's fixed-size record -- the global top-k is
+     contained in the union of the local top-k's, so the record capacity is k and nothing about
+     the other ranks has to be known first;
+  2. ONE all_gather_into_tensor of the records (8k bytes per rank);
+  3. grace_shard_select on every rank: the exact global cut over the gathered entries, the dense
+     output (zero-filled on a side stream while 1-2 run), this rank's residual restored where the
+     cut rejects one of its local picks, and its payload marks.
+A degenerate shard (ties, zeros) is resolved inside the local engine's own exact fallback, so
+there is no bracket-miss protocol and no capacity overflow.
+
+The partition (every rank's shard length) is agreed on a name's first step -- one all_gather and
+one host read, that step only.  Every record carries its shard length, and the select kernel
+checks it against the agreed table: a rank whose shard changes size later is reported on every
+rank by ``ShardPartitionError`` at the next step (never a hang, never a silent mix of partitions).
+``check_sizes=True`` instead agrees the partition at every step (one small all_gather and one host
+read per step), so a resize is handled in the step where it happens: every rank re-plans with the
+new sizes, a rank whose shard kept its size keeps its error feedback, a resized rank starts from
+t = g, and the event is counted in ``resizes``.
 
 ``kernels`` defaults to the native HIP set; the CPU tests inject an oracle-backed emulator of the
-same six calls to run the protocol on gloo.
+same calls to run the protocol on gloo.
 """
-import numpy as np
 import torch
 import torch.distributed as dist
 
 from grace_amd import ops
 
-HIST_BINS = 2048
+
+class ShardPartitionError(RuntimeError):
+    """A rank's shard length differs from the partition agreed on the name's first step."""
 
 
 class NativeShardKernels:
     """The HIP kernels behind each protocol step (GPU tensors only)."""
 
-    def exchange_buffers(self, device):
-        return ops.shard_exchange_buffers(device)
+    HDR = ops.SHARD_HDR
 
-    def empty(self, n, dtype, device):
-        return torch.empty(n, dtype=dtype, device=device)
+    def record_words(self, cap):
+        return ops.shard_record_words(cap)
 
-    def cand_cap(self, m, k):
-        return min(m, 2 * k + 65536)   # topk.hip topk_cap
+    def local_step(self, g, res, has_res, k_loc, vals, idx):
+        ops.topk_residual_step(g, res, has_res, 1.0, 1.0, k_loc, out=None, payload=(None, vals, idx))
 
-    sample = staticmethod(ops.shard_sample)
-    main = staticmethod(ops.shard_main)
-    route = staticmethod(ops.shard_route)
-    boundary = staticmethod(ops.shard_boundary)
-    take = staticmethod(ops.shard_take)
-    scatter_range = staticmethod(ops.scatter_range)
+    select = staticmethod(ops.shard_select)
+
+    def status(self, device):
+        return ops.shard_status(device)
+
+    def take_status(self, st):
+        return ops.status_take(st)
 
     def fill_zero(self, x):
         return ops.fill(x, 0.0)
 
-    def select_all(self, t, k):
-        _, vals, idx = ops.topk_compress(t, k)
-        return vals, idx
 
+class _Plan:
+    """Per-name state: the agreed partition and the record buffers (one allocation each)."""
 
-def plan_boundary(xh_all, k, world, cand_cap):
-    """Host step 3 from the gathered [W, 2048 + 8] exchange rows (hist, n_sure, n_cand, ...).
+    def __init__(self, K, sizes, rank, ratio, device):
+        self.sizes = list(sizes)
+        self.world = len(sizes)
+        self.n = sum(sizes)
+        self.k = ops.ratio_k(self.n, ratio)
+        self.cap = self.k                       # a rank holds at most k of the global top-k
+        bases = [sum(sizes[:w]) for w in range(self.world)]
+        self.base = bases[rank]
+        self.tab = torch.tensor(list(sizes) + bases, dtype=torch.int64).to(device)
+        self.stride = K.record_words(self.cap)
+        self.recs = torch.empty(self.world * self.stride, dtype=torch.int32, device=device)
+        self.pay_idx = torch.full((self.cap,), -1, dtype=torch.int32, device=device)
+        self.rec = None
+        self.rec_m = None
 
-    Returns (ok, B, need, cap_b, cap_p): B the boundary bin (2048 when no candidate is needed),
-    need the count still to take from bin B, cap_b the largest per-rank bin-B list, cap_p an upper
-    bound of any rank's payload count.  ok False = the bracket missed or a list overflowed."""
-    xh_all = np.asarray(xh_all, dtype=np.int64).reshape(world, -1)
-    hist_r = xh_all[:, :HIST_BINS]
-    n_sure_r = xh_all[:, HIST_BINS]
-    n_cand_r = xh_all[:, HIST_BINS + 1]
-    s = int(n_sure_r.sum())
-    c = int(n_cand_r.sum())
-    if s > k or s + c < k or bool((n_cand_r > cand_cap).any()):
-        return False, -1, 0, 0, 0
-    target = k - s
-    if target == 0:
-        return True, HIST_BINS, 0, 0, int(n_sure_r.max())
-    hist = hist_r.sum(axis=0)
-    above_incl = np.cumsum(hist[::-1])[::-1]          # count in bins >= b
-    above = above_incl - hist                          # count in bins > b
-    cand = np.nonzero((above < target) & (target <= above_incl))[0]
-    B = int(cand.max())
-    need = int(target - above[B])
-    cap_b = int(hist_r[:, B].max())
-    cap_p = int(min(k, (n_sure_r + (hist_r[:, B:].sum(axis=1))).max()))
-    return True, B, need, cap_b, cap_p
+    def record(self, m, device, hdr):
+        """This rank's send buffer: header word 0 = m, idx -1 padding past k_loc (written once per m)."""
+        if self.rec is None or self.rec_m != m:
+            host = torch.full((self.stride,), -1, dtype=torch.int32)
+            host[:hdr] = 0
+            host[0] = m
+            self.rec = host.to(device)
+            self.rec_m = m
+        return self.rec
 
 
 class ShardedTopK:
     """Top-k (ratio) + residual memory over one bucket sharded across the ranks of `group`."""
 
-    def __init__(self, compress_ratio, group=None, dense="replicated", kernels=None):
+    def __init__(self, compress_ratio, group=None, dense="replicated", kernels=None, check_sizes=False):
         if dense not in ("replicated", "shard"):
             raise ValueError("dense must be 'replicated' or 'shard'")
         self.compress_ratio = compress_ratio
         self.group = group
         self.dense = dense
+        self.check_sizes = check_sizes
         self.k_ops = kernels or NativeShardKernels()
         self.residuals = {}
-        self._sizes = {}
-        self.last_payload = None      # (vals, idx) of this rank's entries of the last step
-        self.last_fallback = False
-        self.resizes = 0              # steps that found a rank's shard resized (and were redone)
+        self._plans = {}
+        self._side = {}
+        self.last_payload = None      # (vals, idx) of this rank's record: idx = global index, or -1
+        self.resizes = 0              # steps that found a rank's shard resized (check_sizes=True)
+        self.host_reads = 0           # host synchronisations (first step of a name; every step with check_sizes)
 
     def _world(self):
         if dist.is_available() and dist.is_initialized():
             return dist.get_world_size(self.group), dist.get_rank(self.group)
         return 1, 0
 
-    def _shard_sizes(self, name, m, device, world):
-        """Shard sizes of `name` on every rank.  Exchanged on a name's first step only; every later
-        step re-checks them for free through the shard length each rank's main pass writes into
-        its exchanged counters (step 3), so a resize on any rank is seen by ALL ranks in the same
-        step and they take the same branch (no rank-local collective)."""
-        sizes = self._sizes.get(name)
-        if sizes is None:
-            if world > 1:
-                mine = torch.tensor([m], dtype=torch.int64, device=device)
-                allm = self.k_ops.empty(world, torch.int64, device)
-                dist.all_gather_into_tensor(allm, mine, group=self.group)
-                sizes = [int(v) for v in allm.cpu().tolist()]
-            else:
-                sizes = [m]
-            self._sizes[name] = sizes
-        return sizes
+    def _gather_sizes(self, m, device, world):
+        if world == 1:
+            return [m]
+        mine = torch.tensor([m], dtype=torch.int64, device=device)
+        allm = torch.empty(world, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(allm, mine, group=self.group)
+        self.host_reads += 1
+        return [int(v) for v in allm.cpu().tolist()]
+
+    def _plan(self, name, m, device, world, rank):
+        plan = self._plans.get(name)
+        if plan is None or self.check_sizes:
+            sizes = self._gather_sizes(m, device, world)
+            if plan is None or sizes != plan.sizes:
+                if plan is not None:
+                    self.resizes += 1
+                plan = self._plans[name] = _Plan(self.k_ops, sizes, rank, self.compress_ratio, device)
+        return plan
+
+    def _check_status(self, device):
+        st = self.k_ops.status(device)
+        bits = self.k_ops.take_status(st)
+        if bits:
+            raise ShardPartitionError(
+                "grace_amd ShardedTopK: a rank's shard length changed after the name's first step (status "
+                f"{bits:#x}); the previous step mixed partitions.  Keep every rank's shard length fixed, or "
+                "construct ShardedTopK(check_sizes=True) to re-agree the partition at every step")
+        return st
+
+    def check(self, device=None):
+        """Wait for the device and raise ShardPartitionError if any finished step mixed partitions
+        (the step itself never blocks: its status is otherwise checked when the next step starts)."""
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        self._check_status(device)
+
+    def _zero_out(self, out_len, device):
+        """The dense output, zero-filled on a side stream so the fill overlaps the local step and
+        the exchange; the current stream waits for it only before the select."""
+        K = self.k_ops
+        if device.type != "cuda":
+            return K.fill_zero(torch.empty(out_len, dtype=torch.float32, device=device)), None
+        cur = torch.cuda.current_stream(device)
+        side = self._side.get(cur.cuda_stream)
+        if side is None:
+            side = self._side[cur.cuda_stream] = torch.cuda.Stream(device=device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            out = torch.empty(out_len, dtype=torch.float32, device=device)
+            K.fill_zero(out)
+        out.record_stream(cur)
+        return out, side
 
     def step(self, shard, name):
-        return self._step(shard.reshape(-1), name, compensated=False)
-
-    def _step(self, g, name, compensated):
-        """compensated=True: g already is t = beta r + gamma g (the redo after a resize)."""
         K = self.k_ops
         world, rank = self._world()
+        g = shard.reshape(-1)
         dev = g.device
         m = g.numel()
-        sizes = self._shard_sizes(name, m, dev, world)
-        base = sum(sizes[:rank])
-        n = sum(sizes)
-        k = ops.ratio_k(n, self.compress_ratio)
+        status = self._check_status(dev)
+        plan = self._plan(name, m, dev, world, rank)
         res = self.residuals.get(name)
-        has_res = res is not None and res.numel() == m and not compensated
-        if res is None or res.numel() != m:
-            res = K.empty(m, torch.float32, dev)
-        self.residuals[name] = res
-        stratum = max(1, n // ops.SAMPLE_MAX)
-        sample_total = sum(sz // stratum for sz in sizes)
-        xs, xh = K.exchange_buffers(dev)
-        vals = K.empty(k, torch.float32, dev)
-        idx = K.empty(k, torch.int32, dev)
-
-        K.sample(g, res, has_res, stratum, xs)
+        has_res = res is not None and res.numel() == m
+        if not has_res:
+            res = torch.empty(m, dtype=torch.float32, device=dev)
+            self.residuals[name] = res
+        out_len = m if self.dense == "shard" else plan.n
+        out_base = plan.base if self.dense == "shard" else 0
+        out, side = self._zero_out(out_len, dev)
+        rec = plan.record(m, dev, K.HDR)
+        cap = plan.cap
+        vals = rec[K.HDR:K.HDR + cap].view(torch.float32)
+        idx = rec[K.HDR + cap:K.HDR + 2 * cap]
+        K.local_step(g, res, has_res, min(cap, m), vals, idx)
         if world > 1:
-            dist.all_reduce(xs, group=self.group)
-        K.main(g, res, has_res, base, n, k, sample_total, vals, idx, xs, xh)
-        if world > 1:
-            xh_all = K.empty(world * xh.numel(), torch.int32, dev)
-            dist.all_gather_into_tensor(xh_all, xh, group=self.group)
+            dist.all_gather_into_tensor(plan.recs, rec, group=self.group)
+            recs = plan.recs
         else:
-            xh_all = xh
-        # the exchange rows go to the host asynchronously; the dense output's zero-fill is queued
-        # behind them, so it runs on the GPU while the host plans the boundary
-        host = self._host_rows(xh_all)
-        out_len = m if self.dense == "shard" else n
-        out = K.fill_zero(K.empty(out_len, torch.float32, dev))
-        self._wait_host()
-        rows = host.numpy().reshape(world, -1)
-        seen = [int(v) for v in rows[:, HIST_BINS + 2]]
-        if seen != list(sizes):
-            # some rank's shard changed size: this pass ran on stale offsets.  Every rank sees the
-            # same gathered lengths, so all of them redo the step with the new sizes.  The main
-            # pass left t = beta r + gamma g in the residual buffer, so the redo starts from a copy
-            # of t as an already-compensated gradient: a rank whose shard kept its size keeps its
-            # error feedback exactly (residual.py:10-14 applied once), a resized rank starts from
-            # t = g as on a first step.  Counted in ``resizes``.
-            self._sizes[name] = seen
-            self.resizes += 1
-            return self._step(res.clone(), name, compensated=True)
-        ok, B, need, cap_b, cap_p = plan_boundary(rows, k, world, K.cand_cap(m, k))
-        self.last_fallback = not ok
-        if not ok:
-            return self._fallback(res, base, n, k, sizes, world, vals, idx, dev, out)
-
-        bsend = K.empty(cap_b + 1, torch.int64, dev)
-        K.route(res, base, k, B, vals, idx, bsend)
-        if world > 1:
-            brecv = K.empty(world * (cap_b + 1), torch.int64, dev)
-            dist.all_gather_into_tensor(brecv, bsend, group=self.group)
-        else:
-            brecv = bsend
-        K.boundary(res, base, k, brecv, world, cap_b, need, vals, idx, cap_p)
-        self.last_payload = (vals[:cap_p], idx[:cap_p])
-        return self._decode(vals, idx, cap_p, base, n, m, world, dev, out)
-
-    def _host_rows(self, xh_all):
-        """Start the device->host copy of the exchange rows (pinned, non-blocking)."""
-        if not xh_all.is_cuda:
-            self._evt = None
-            return xh_all
-        buf = getattr(self, "_pinned", None)
-        if buf is None or buf.numel() != xh_all.numel():
-            buf = torch.empty(xh_all.numel(), dtype=xh_all.dtype, pin_memory=True)
-            self._pinned = buf
-        buf.copy_(xh_all, non_blocking=True)
-        self._evt = torch.cuda.Event()
-        self._evt.record()
-        return buf
-
-    def _wait_host(self):
-        if self._evt is not None:
-            self._evt.synchronize()
-
-    def _decode(self, vals, idx, cap_p, base, n, m, world, dev, out):
-        K = self.k_ops
-        if self.dense == "shard":
-            K.scatter_range(vals, idx, 0, cap_p, 1, base, out)
-            return out
-        if world == 1:
-            K.scatter_range(vals, idx, 0, cap_p, 1, 0, out)
-            return out
-        send = K.empty(2 * cap_p, torch.float32, dev)
-        send[:cap_p].copy_(vals[:cap_p])
-        send[cap_p:].copy_(idx[:cap_p].view(torch.float32))
-        recv = K.empty(world * 2 * cap_p, torch.float32, dev)
-        dist.all_gather_into_tensor(recv, send, group=self.group)
-        K.scatter_range(recv, recv[cap_p:].view(torch.int32), 2 * cap_p, cap_p, world, 0, out)
-        return out
-
-    def _fallback(self, res, base, n, k, sizes, world, vals, idx, dev, out):
-        """Exact path: the residual buffer holds t for every element after the main pass."""
-        K = self.k_ops
-        if world > 1:
-            if len(set(sizes)) != 1:
-                # unequal shards: RCCL / gloo gathers need one size, so pad every shard to the
-                # largest and cut the padding out of the gathered rows
-                mx = max(sizes)
-                send = K.empty(mx, torch.float32, dev)
-                send[:res.numel()].copy_(res)
-                recv = K.empty(world * mx, torch.float32, dev)
-                dist.all_gather_into_tensor(recv, send, group=self.group)
-                t_all = torch.cat([recv[r * mx:r * mx + sz] for r, sz in enumerate(sizes)])
-            else:
-                t_all = K.empty(n, torch.float32, dev)
-                dist.all_gather_into_tensor(t_all, res, group=self.group)
-        else:
-            t_all = res.clone()
-        vals_all, idx_all = K.select_all(t_all, k)
-        K.take(vals_all, idx_all, k, res, base, vals, idx, k)
-        self.last_payload = (vals, idx)
-        K.scatter_range(vals_all, idx_all, 0, k, 1, base if self.dense == "shard" else 0, out)
+            recs = rec
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side)
+        K.select(recs, world, rank, cap, plan.tab, plan.k, res, out, out_base, plan.pay_idx, status)
+        self.last_payload = (vals, plan.pay_idx)
         return out

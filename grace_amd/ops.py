@@ -808,9 +808,10 @@ def _w1_status(dev):
         st = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         hit = _w1_st[key] = (st, st.numpy())     # numpy view: a plain host read per call
     st, view = hit
-    v = int(view[0])
-    if v:
-        view[0] = 0
+    if view[0]:
+        # read-and-clear as one host atomic exchange: a bit a still-running kernel sets between a
+        # plain read and a plain clear would be lost
+        v = int(_lib.query("grace_status_take", st.data_ptr()))
         if v & 2:
             raise PowerSGDWaitError("grace_amd: a one-pass PowerSGD wait ran out in an earlier call; its P and Q "
                                     "were not valid (never expected: another kernel kept its workgroups from "
@@ -860,56 +861,40 @@ def normal(shape, seed, device):
 
 
 # ----------------------------------------------------------------------------- sharded top-k
-SAMPLE_MAX = 131072   # topk.hip kSampleMax: target size of the stratified bracket sample
+def shard_record_words(cap):
+    """int32 words of one rank's sharded top-k record: [header | vals f32[cap] | local idx i32[cap]]."""
+    return int(_lib.query("grace_shard_record_words", int(cap)))
 
 
-def shard_exchange_buffers(device):
-    """(xs, xh) int32 exchange buffers of the sharded top-k, zeroed once (re-zeroed by the kernels)."""
-    key = (str(device), "shard_x", torch.cuda.current_stream(device).cuda_stream)
-    hit = _ws.get(key)
-    if hit is None:
-        hit = (torch.zeros(_lib.query("grace_topk_shard_xs_words"), dtype=torch.int32, device=device),
-               torch.zeros(_lib.query("grace_topk_shard_xh_words"), dtype=torch.int32, device=device))
-        _ws[key] = hit
-    return hit
+SHARD_HDR = 8   # shard.hip kShHdr: header words (word 0 = the shard length)
 
 
-def shard_sample(g, residual, has_residual, stratum, xs):
-    _lib.call("grace_topk_shard_sample", _p(g), _p(residual), 1 if has_residual else 0, 1.0, 1.0, g.numel(),
-              int(stratum), _p(xs), _stream())
+def shard_select(recs, world, rank, cap, tab, k, residual, out, out_base, pay_idx, status):
+    """grace_shard_select over the W gathered records: the exact global top-k (dense output into the
+    zero-filled `out`, which covers global [out_base, out_base + out.numel())), this rank's residual
+    restored where the global cut rejects a local pick, pay_idx = global index or -1 per own entry.
+    `status`: pinned int32 word (bit 1: a record's shard length differs from the agreed `tab`)."""
+    dev = recs.device
+    ws = workspace("shardsel", _lib.query("grace_shard_select_workspace_bytes", int(world), int(cap)), dev)
+    _lib.call("grace_shard_select", _p(recs), int(world), int(rank), int(cap), _p(tab), int(k), _p(residual),
+              _p(out), int(out_base), out.numel(), _p(pay_idx), _p(ws), ws.numel(), status.data_ptr(), _stream())
 
 
-def shard_main(g, residual, has_residual, idx_base, n_global, k, sample_total, vals, idx, xs, xh):
-    m = g.numel()
-    ws = topk_workspace(m, k, g.device)
-    _lib.call("grace_topk_shard_main", _p(g), _p(residual), 1 if has_residual else 0, 1.0, 1.0, m, int(idx_base),
-              int(n_global), int(k), int(sample_total), _p(vals), _p(idx), _p(ws), ws.numel(), _p(xs), _p(xh),
-              _stream())
+_sh_st = {}
 
 
-def shard_route(residual, idx_base, k, boundary_bin, vals, idx, bsend):
-    m = residual.numel()
-    ws = topk_workspace(m, k, residual.device)
-    _lib.call("grace_topk_shard_route", _p(residual), m, int(idx_base), int(k), int(boundary_bin), _p(vals),
-              _p(idx), _p(ws), ws.numel(), _p(bsend), _stream())
+def shard_status(dev):
+    """The pinned status word the sharded select kernels set bits in (one per device)."""
+    key = str(dev)
+    st = _sh_st.get(key)
+    if st is None:
+        st = _sh_st[key] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    return st
 
 
-def shard_boundary(residual, idx_base, k, brecv, world, cap_b, need, vals, idx, cap_p):
-    m = residual.numel()
-    ws = topk_workspace(m, k, residual.device)
-    _lib.call("grace_topk_shard_boundary", _p(residual), m, int(idx_base), int(k), _p(brecv), int(world),
-              int(cap_b), int(need), _p(vals), _p(idx), int(cap_p), _p(ws), ws.numel(), _stream())
-
-
-def shard_take(vals_all, idx_all, k, residual, idx_base, vals, idx, cap_p):
-    _lib.call("grace_topk_shard_take", _p(vals_all), _p(idx_all), int(k), _p(residual), residual.numel(),
-              int(idx_base), _p(vals), _p(idx), int(cap_p), _stream())
-
-
-def scatter_range(vals, idx, stride, per, world, base, out):
-    """out[idx - base] = 0 + v over `world` padded payloads (idx -1 = padding); out pre-zeroed."""
-    _lib.call("grace_sparse_scatter_range", _p(vals), _p(idx), int(stride), int(per), int(world), int(base),
-              out.numel(), _p(out), _stream())
+def status_take(st):
+    """Bits set in a pinned status word since the last take (host atomic exchange; never blocks)."""
+    return int(_lib.query("grace_status_take", st.data_ptr())) if int(st[0]) else 0
 
 
 # ----------------------------------------------------------------------------- DGC

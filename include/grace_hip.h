@@ -45,6 +45,10 @@ const char* grace_last_error(void);
  * top-k launch on `workspace` (0 = sampled fast path, 1 = exact fallback). */
 grace_status_t grace_read_status(const void* workspace, int32_t* status_host, void* stream);
 
+/* Atomically read and clear a pinned host status word that kernels set bits in (system-scope
+ * fetch_or): returns the bits set since the last take.  Host only, never blocks. */
+int32_t grace_status_take(int32_t* host_word);
+
 /* Event timer on the kernel's own stream, used by bench.py to time the dominant kernel of a
  * fused step: when enabled, that kernel's launch is bracketed by hipEventRecord. */
 grace_status_t grace_timer_enable(int enable);
@@ -388,42 +392,27 @@ grace_status_t grace_powersgd_w1_compress(const float* M, int64_t n, int64_t m, 
 grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* stream);
 
 /* ---- sharded top-k (BASELINE configs[4]) ------------------------------------
- * One bucket of n_global elements split into contiguous shards, one per rank (this rank's shard:
- * m elements starting at idx_base).  The union of the ranks' payloads equals the single-GPU
- * grace_topk_residual_step selection on the whole bucket (same tie rule); the collectives between
- * the calls are the caller's (grace_amd/dist/sharded.py):
- *   shard_sample -> all_reduce(xs) -> shard_main -> all_gather(xh) -> [host: boundary bin, need]
- *   -> shard_route -> all_gather(bsend) -> shard_boundary -> all_gather(payload) -> scatter_range
- * xs: u32[grace_topk_shard_xs_words()] sample histogram, zero before the first step (shard_main
- * re-zeroes it); xh: u32[grace_topk_shard_xh_words()] = candidate histogram [2048] + counters
- * (n_sure, n_cand, ...).  vals/idx hold this rank's payload (capacity >= max(k, cap_p)); after
- * shard_boundary entries [count, cap_p) are padding with idx -1.  ws as grace_topk_workspace_bytes(m, k).
- * Replaces the single-process TopKCompressor.compress + ResidualMemory (topk.py:32-42,
- * residual.py:10-20) for one bucket sharded over ranks. */
-size_t grace_topk_shard_xs_words(void);
-size_t grace_topk_shard_xh_words(void);
-grace_status_t grace_topk_shard_sample(const float* g, float* residual, int32_t has_residual, float beta,
-                                       float gamma, int64_t m, int64_t stratum, uint32_t* xs, void* stream);
-grace_status_t grace_topk_shard_main(const float* g, float* residual, int32_t has_residual, float beta,
-                                     float gamma, int64_t m, int64_t idx_base, int64_t n_global, int64_t k,
-                                     int64_t sample_total, float* vals, int32_t* idx, void* ws, size_t ws_bytes,
-                                     uint32_t* xs, uint32_t* xh, void* stream);
-grace_status_t grace_topk_shard_route(float* residual, int64_t m, int64_t idx_base, int64_t k,
-                                      int32_t boundary_bin, float* vals, int32_t* idx, void* ws,
-                                      size_t ws_bytes, int64_t* bsend, void* stream);
-grace_status_t grace_topk_shard_boundary(float* residual, int64_t m, int64_t idx_base, int64_t k,
-                                         const int64_t* brecv, int32_t world, int64_t cap_b, uint32_t need,
-                                         float* vals, int32_t* idx, int64_t cap_p, void* ws, size_t ws_bytes,
-                                         void* stream);
-/* exact fallback (bracket miss): this rank's entries of the whole bucket's selection */
-grace_status_t grace_topk_shard_take(const float* vals_all, const int32_t* idx_all, int64_t k, float* residual,
-                                     int64_t m, int64_t idx_base, float* vals, int32_t* idx, int64_t cap_p,
-                                     void* stream);
-/* diagnostic: copy the 64-byte control block to the host (synchronises the stream) */
-grace_status_t grace_topk_shard_read(const void* ws, uint32_t* ctl_host, void* stream);
-/* out[idx - base] = 0 + v for gathered padded payloads (rank w at + w * stride, `per` entries) */
-grace_status_t grace_sparse_scatter_range(const float* vals, const int32_t* idx, int64_t stride, int64_t per,
-                                          int32_t world, int64_t base, int64_t len, float* out, void* stream);
+ * One bucket split into contiguous shards, one per rank; replaces the single-process
+ * TopKCompressor.compress + ResidualMemory (grace_dl/dist/compressor/topk.py:32-42,
+ * memory/residual.py:10-20) and the host-synced variable-size Allgather
+ * (grace_dl/dist/communicator/allgather.py:15-38) for one bucket sharded over ranks.  Per step
+ * (grace_amd/dist/sharded.py; csrc/shard.hip), no host synchronisation:
+ *   grace_topk_residual_step(shard, k_loc = min(k, m)) into this rank's record
+ *   [header (word 0 = m) | vals f32[cap] | local idx i32[cap], idx -1 = padding], cap = k
+ *   -> ONE all_gather of the W records -> grace_shard_select.
+ * grace_shard_select: the exact global top-k of the gathered entries (larger |t| first, lower
+ * global index first, as the single-GPU engine): out[gi - out_base] = 0 + v for every selected
+ * gi in [out_base, out_base + out_len) (out zero-filled by the caller); for this rank's record
+ * entries pay_idx[j] = global index if selected, else -1, and the residual gets t back
+ * (residual[idx] = v) where the local engine picked an entry the global cut rejects.
+ * tab: device int64 [m_0 .. m_{W-1}, base_0 .. base_{W-1}] (the agreed partition).  status_host
+ * (pinned, may be NULL): bit 1 = a record's shard length differs from tab, bit 2 = fewer valid
+ * entries than k (both set with system-scope atomics; read them with grace_status_take). */
+size_t grace_shard_record_words(int64_t cap);
+size_t grace_shard_select_workspace_bytes(int32_t world, int64_t cap);
+grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t rank, int64_t cap, const int64_t* tab,
+                                  int64_t k, float* residual, float* out, int64_t out_base, int64_t out_len,
+                                  int32_t* pay_idx, void* ws, size_t ws_bytes, int32_t* status_host, void* stream);
 
 /* ---- DGC (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39) -------------------------
  * compress: grace_dgc_sample (|t| at the sampled indices: sample_idx from the caller = torch's

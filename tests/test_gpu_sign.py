@@ -155,3 +155,43 @@ def test_w1_step_output_reuse_respects_views():
     assert np.array_equal(_np(b), np.where(-m.T >= 0, 1.0, -1.0).astype(np.float32))
     for h, e, cut in zip(held, exp, (0, 0, 1, 0)):                # still intact after more steps
         assert np.array_equal(_np(h).ravel(), e[cut:])
+
+
+def _planted(n, seed):
+    """f32[n] standard normal with +-0, NaN, +-inf and denormals planted at both ends and inside."""
+    x = np.random.default_rng(seed).standard_normal(n).astype(np.float32)
+    specials = np.array([0.0, -0.0, np.nan, -np.nan, np.inf, -np.inf, 1e-45, -1e-45], dtype=np.float32)
+    for base in (0, n // 3, n // 2 + 1, n - len(specials)):
+        x[base:base + len(specials)] = specials
+    return x
+
+
+@pytest.mark.parametrize("shape", [(1 << 20,), ((1 << 20) + 3,), (1024, 1024)],
+                         ids=["n=2^20", "n=2^20+3", "1024x1024"])
+def test_signsgd_configs0_at_size(shape):
+    """BASELINE configs[0] at its own size: Allgather(SignSGD, NoneMemory, 1).step on one 4 MiB f32
+    tensor (n = 1,048,576; plus a ragged n and a 2-D view), bit-exact against the oracle's
+    sign_aggregate([sign_decode(sign_encode(x))]) with +-0 / NaN / +-inf / denormals planted; the
+    unfused compress -> decompress -> aggregate at the same size gives the same bits
+    (grace_dl/dist/compressor/signsgd.py:6-30)."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.signsgd import SignSGDCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    n = int(np.prod(shape))
+    x = _planted(n, 40 + n % 7)
+    exp = O.sign_aggregate([O.sign_decode(O.sign_encode(x))]).reshape(shape)
+    comm = Allgather(SignSGDCompressor(), NoneMemory(), 1)
+    xt = _t(x).view(shape)
+    for _ in range(2):                        # the second step reuses the dropped output buffer
+        out = comm.step(xt, "w")
+        assert out.shape == torch.Size(shape)
+        assert same_bits(_np(out), exp)
+    comp = comm.compressor
+    (codes,), ctx = comp.compress(xt, "w")
+    assert np.array_equal(_np(codes), O.sign_encode(x))
+    dec = comp.decompress([codes], ctx)
+    assert same_bits(_np(dec), O.sign_decode(O.sign_encode(x)).reshape(shape))
+    assert same_bits(_np(comp.aggregate([dec])), exp)
+    assert same_bits(_np(comm.send_receive([codes], "w", ctx)), exp)
+    # x itself is never written
+    assert same_bits(_np(xt).ravel(), x)
