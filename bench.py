@@ -275,16 +275,18 @@ def bench_topk(args, world, rank, dev):
                 roofline["traffic"] = pmc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
-    # the fraction against a copy bandwidth measured on this box as well
-    copy_gbs, variant, copy_med = measured_copy_gbs(dev) if not NO_PROBE else (None, None, None)
-    roofline["measured_copy_gbs"] = copy_gbs
-    roofline["measured_copy_median_gbs"] = copy_med
-    roofline["measured_copy_kind"] = ("grace_hbm_probe: 2-read / 2-write non-temporal 16-B stream (the step's "
-                                      "dense traffic mix, in place like the main pass, no arithmetic) over 256 MiB "
-                                      "arrays, 3 rotated sets, the fastest launch of the fastest of 6 layouts "
-                                      f"(variant {variant}), HIP events")
-    roofline["frac_of_measured_copy"] = round(achieved / copy_gbs, 4) if copy_gbs else None
-    roofline["frac_of_measured_copy_median"] = round(achieved / copy_med, 4) if copy_med else None
+    # the fraction against a bandwidth measured on this box as well -- the main
+    # pass's own streaming skeleton (same kernel, chunking, loads and stores, no classification),
+    # each launch right after a real step, timed like the main pass
+    skel, skel_med = skeleton_ceiling(step, main_bytes, n, dev) if not NO_PROBE and world == 1 else (None, None)
+    roofline["measured_copy_gbs"] = skel
+    roofline["measured_copy_median_gbs"] = skel_med
+    roofline["measured_copy_kind"] = ("grace_topk_stream_probe: the topk_main kernel itself with the classification "
+                                      "compiled out (same grid, chunks, 16-B non-temporal loads / stores of g, r, r', "
+                                      "out) on 3 rotated 256 MiB buffer sets, each launch interleaved with a real "
+                                      "step, dispatch-packet events like the main pass; ceiling = fastest launch")
+    roofline["frac_of_measured_copy"] = round(achieved / skel, 4) if skel else None
+    roofline["frac_of_measured_copy_median"] = round(achieved / skel_med, 4) if skel_med else None
     line["roofline"] = roofline
     if world == 1 and not args.no_overlap:
         line["two_streams"] = bench_topk_two_streams(args, grads, names)
@@ -327,35 +329,30 @@ def bench_topk_two_streams(args, grads, names):
             "note": "bucket j on stream j % 2; not the headline value (that is one stream, in order)"}
 
 
-def measured_copy_gbs(dev, n=1 << 26, sets=3, reps=9):
-    """The box's HBM ceiling for the headline step's traffic mix (the fraction
-    against a measured bandwidth too): ``grace_hbm_probe``, read r, g and write r' = r + g, o = 0
-    with non-temporal 16-B loads / stores and no arithmetic, over 256 MiB arrays (the bucket size)
-    in `sets` rotated buffer sets (768 MiB each, so no launch finds its bytes in the 256 MB
-    Infinity Cache), HIP events on the probe's own stream.  Six streaming layouts (chunked like the
-    main pass, grid-stride); the fastest launch of the fastest layout is the ceiling (a ceiling is
-    the best rate the pure stream reached; the median is reported beside it).
-    Returns (GB/s, variant, median GB/s of that variant)."""
+def skeleton_ceiling(step, main_bytes, n, dev, sets=3, rounds=12):
+    """The main pass's streaming ceiling on this box: grace_topk_stream_probe (topk_main with the
+    classification compiled out: the same grid, loads and stores) on `sets` rotated buffer sets of
+    n floats (g, r, out: 768 MiB each, more than the Infinity Cache), each launch right after a real
+    step so it runs at the same clocks, timed with the library's dispatch-packet events exactly as
+    the main pass is.  Returns (GB/s of the fastest launch, GB/s of the median launch)."""
     from grace_amd import _lib, ops
     bufs = [tuple(torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(3)) for _ in range(sets)]
-    best, best_v, best_med = 0.0, None, None
-    for variant in range(6):
-        elems = int(_lib.query("grace_hbm_probe_elems", n, variant))
-        ts = []
-        for i in range(reps + sets):
-            r, g, o = bufs[i % sets]
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            _lib.call("grace_hbm_probe", r.data_ptr(), g.data_ptr(), o.data_ptr(), n, variant, ops._stream())
-            b.record()
-            b.synchronize()
-            if i >= sets:
-                ts.append(a.elapsed_time(b) * 1e-3)
-        gbs = 16.0 * elems / min(ts) / 1e9
-        if gbs > best:
-            best, best_v, best_med = gbs, variant, 16.0 * elems / sorted(ts)[len(ts) // 2] / 1e9
-    del bufs
-    return round(best, 1), best_v, round(best_med, 1)
+    ws = torch.zeros(int(_lib.query("grace_topk_stream_probe_workspace_bytes", n)), dtype=torch.uint8, device=dev)
+    ts = []
+    for i in range(rounds + sets):
+        step(i)
+        g, r, o = bufs[i % sets]
+        ops.timer_enable(True)
+        _lib.call("grace_topk_stream_probe", g.data_ptr(), r.data_ptr(), o.data_ptr(), n, ws.data_ptr(), ws.numel(),
+                  ops._stream())
+        ms, cnt = ops.timer_collect()
+        ops.timer_enable(False)
+        if i >= sets and cnt == 1:
+            ts.append(ms * 1e-3)
+    del bufs, ws
+    if not ts:
+        return None, None
+    return round(main_bytes / min(ts) / 1e9, 1), round(main_bytes / sorted(ts)[len(ts) // 2] / 1e9, 1)
 
 
 def measured_encode_gbs(dev, n, sets=4, reps=7):
@@ -640,7 +637,18 @@ def bench_ddp(args, world, rank, dev):
             "ddp_bucket": "one flat bucket, ONE global top-k (a different algorithm)"}[args.workload]
     line["config"] = {"workload": f"{kind}, Allgather(TopK 1 %, Residual), 161 ResNet-50 tensors", "numel": total,
                       "tensors": len(bucket.params)}
-    line["roofline"] = None
+    # algorithmic bytes: read g, r; write r' and (world 1) the dense output; the payload (8 B per
+    # selected entry: per-tensor k_i, or one global k for ddp_bucket)
+    if args.workload == "ddp_bucket":
+        k_sum = max(1, int(total * 0.01))
+    else:
+        k_sum = sum(min(p.numel(), max(1, int(p.numel() * 0.01))) for p in bucket.params)
+    alg = (16 if world == 1 else 12) * total + 8 * k_sum
+    t = elapsed / args.steps
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_step": alg, "selected_per_step": k_sum,
+                        "note": "16 B per element at world 1 (g, r read; r', dense out written) + 8 B per selected entry"}
     return line
 
 

@@ -24,6 +24,8 @@ SIGNATURES = {
     "grace_last_error": (ctypes.c_char_p, []),
     "grace_read_status": (ST, [P, P, P]),
     "grace_status_take": (ctypes.c_int32, [P]),
+    "grace_topk_stream_probe_workspace_bytes": (SZ, [I64]),
+    "grace_topk_stream_probe": (ST, [P, P, P, I64, P, SZ, P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
     "grace_timer_collect": (ST, [P, P]),
     "grace_event_create": (ST, [P]),
@@ -51,10 +53,13 @@ SIGNATURES = {
     "grace_topk_step_dense": (ST, [P, I64, I64, P, P, P, P, SZ, P]),
     "grace_topk_residual_step": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, SZ, P]),
     "grace_topk_carry_size": (I64, [I64, I64]),
-    "grace_topk_residual_step_carry": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, I64, I32, P, SZ, P]),
-    "grace_topk_segmented_workspace_bytes": (SZ, [I64, I32]),
-    "grace_topk_segmented_chunk": (I32, []),
-    "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, P, I32, I64, I64, P, P, P, P, SZ, P]),
+    "grace_topk_residual_step_carry": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, I64, I32, P, I64, P, SZ, P]),
+    "grace_topk_segmented_small_max": (I32, []),
+    "grace_topk_segmented_chunk": (I64, [I32, I32]),
+    "grace_topk_segmented_seg_ws_bytes": (I64, [I64, I64]),
+    "grace_topk_segmented_fin_blocks": (I32, [I64, I64]),
+    "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, I32, P, I32, P, P, I64, P, P, P, I64, I64, P, P, P, P,
+                                       SZ, P]),
     "grace_shard_record_words": (SZ, [I64]),
     "grace_shard_select_workspace_bytes": (SZ, [I32, I64]),
     "grace_shard_select": (ST, [P, I32, I32, I64, P, I64, P, P, I64, I64, P, P, SZ, P, P]),

@@ -18,10 +18,14 @@ from grace_amd.dist import Compressor
 
 class TopKCompressor(Compressor):
 
-    def __init__(self, compress_ratio, kernel='torch'):
+    def __init__(self, compress_ratio, kernel='torch', recycle_output=True):
         super().__init__()
         self.compress_ratio = compress_ratio
         self.kernel = kernel
+        # world-1 fused step: reuse a dropped, unmodified previous result of the same name and
+        # rewrite only its non-zeros (ops.OutputRecycler); False = a fresh dense output every step
+        self.recycle_output = recycle_output
+        self._recycler = ops.OutputRecycler()
 
     def compress(self, tensor, name):
         flat = ops.dev_f32(tensor)
@@ -68,11 +72,16 @@ class TopKCompressor(Compressor):
         world = int(communicator.world_size)
         carry, carry_valid = mem.carry_for(name, res, has, k)
         if world == 1:
-            out = torch.empty_like(g)
-            ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out, carry=carry,
-                                   carry_valid=carry_valid)
+            if self.recycle_output and n > ops.TOPK_SMALL_N:
+                out, prev_idx = self._recycler.take(name, g)
+            else:
+                out, prev_idx = torch.empty_like(g), None
+            _, _, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out, carry=carry,
+                                               carry_valid=carry_valid, prev_idx=prev_idx)
             mem.residuals[name] = res
             mem.carry_written(name, res, carry)
+            if self.recycle_output and n > ops.TOPK_SMALL_N:
+                self._recycler.keep(name, out, idx)
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
         buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None, carry=carry,
                                                 carry_valid=carry_valid)

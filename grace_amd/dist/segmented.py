@@ -5,7 +5,9 @@ The reference's DDP loop (examples/dist/CIFAR10-dawndist/core.py:203-206) calls
 tensor gets its own k_i = max(1, int(n_i * ratio)) (grace_dl/dist/compressor/topk.py:34) and its
 own residual (grace_dl/dist/memory/residual.py:10-20).  ``SegmentedTopK.step`` computes exactly
 that for all tensors at once -- they are segments of one flat gradient buffer (harness.GradBucket)
--- with four launches (grace_amd/csrc/segtopk.hip) instead of three per tensor.  At W > 1 the
+-- with three launches that stream every element once (grace_amd/csrc/topk.hip "Segmented": small
+tensors selected exactly in one workgroup each, large ones through the single-bucket engine's
+sampled bracket, main pass and finalize, per segment) instead of three launches per tensor.  At W > 1 the
 concatenated payloads (global indices) move in ONE all-gather and are decoded + aggregated in rank
 order into the flat output (allgather.py:40-45 per tensor = per element of the flat buffer).
 
@@ -29,35 +31,57 @@ class SegmentedTopK:
         self._tables = {}
         self.last_payload = None
 
-    def tables(self, sizes, device):
-        # per stream as well: the workspace's histograms and counters are re-zeroed by the next
-        # launch on the same stream, so two streams must never share one
-        key = (tuple(int(s) for s in sizes), str(device), ops._stream())
+    def tables(self, sizes, device, has_res, dense_out):
+        """Device tables of one segment list (cached): offsets, the small / large split, the main
+        pass's chunk map of the large segments (its chunk length follows the bytes per element, so
+        it depends on has_res and on the dense output) and their workspaces.  Per stream as well:
+        the workspaces' counters are re-zeroed by the next launch on the same stream, so two streams
+        must never share one."""
+        sizes = tuple(int(n) for n in sizes)
+        key = (sizes, str(device), ops._stream(), bool(has_res), bool(dense_out))
         hit = self._tables.get(key)
-        if hit is None:
-            chunk = _lib.query("grace_topk_segmented_chunk")
-            seg, kk, chk, cseg = [0], [0], [0], []
-            for i, n in enumerate(key[0]):
-                if n < 1:
-                    raise ValueError("empty tensor in the segment table")
-                seg.append(seg[-1] + n)
-                kk.append(kk[-1] + min(n, ops.ratio_k(n, self.compress_ratio)))   # torch.topk needs k <= n
-                c = (n + chunk - 1) // chunk
-                chk.append(chk[-1] + c)
-                cseg += [i] * c
-            t64 = lambda v: torch.tensor(v, dtype=torch.int64).to(device)   # noqa: E731
-            ws = torch.zeros(_lib.query("grace_topk_segmented_workspace_bytes", seg[-1], len(key[0])),
-                             dtype=torch.uint8, device=device)
-            hit = (t64(seg), t64(kk), t64(chk), torch.tensor(cseg, dtype=torch.int32).to(device), kk[-1], chk[-1], ws)
-            self._tables[key] = hit
+        if hit is not None:
+            return hit
+        small_max = int(_lib.query("grace_topk_segmented_small_max"))
+        chunk = int(_lib.query("grace_topk_segmented_chunk", 1 if has_res else 0, 1 if dense_out else 0))
+        seg, kk = [0], [0]
+        large, small, chk, chunk_li, ws_off, fin, fin_li = [], [], [0], [], [], [0], []
+        ws_total = 0
+        for i, n in enumerate(sizes):
+            if n < 1:
+                raise ValueError("empty tensor in the segment table")
+            k = min(n, ops.ratio_k(n, self.compress_ratio))        # torch.topk needs k <= n
+            seg.append(seg[-1] + n)
+            kk.append(kk[-1] + k)
+            if n <= small_max:
+                small.append(i)
+                continue
+            li = len(large)
+            large.append(i)
+            c = (n + chunk - 1) // chunk
+            chk.append(chk[-1] + c)
+            chunk_li += [li] * c
+            ws_off.append(ws_total)
+            f = int(_lib.query("grace_topk_segmented_fin_blocks", n, k))
+            fin.append(fin[-1] + f)
+            fin_li += [li] * f
+            ws_total += (int(_lib.query("grace_topk_segmented_seg_ws_bytes", n, k)) + 255) // 256 * 256
+        t64 = lambda v: torch.tensor(v, dtype=torch.int64).to(device)   # noqa: E731
+        t32 = lambda v: torch.tensor(v, dtype=torch.int32).to(device)   # noqa: E731
+        ws = torch.zeros(max(ws_total, 256), dtype=torch.uint8, device=device)
+        hit = {"seg_off": t64(seg), "k_off": t64(kk), "large": t32(large or [0]), "n_large": len(large),
+               "small": t32(small or [0]), "n_small": len(small), "chk_off": t64(chk), "chunk_li": t32(chunk_li or [0]),
+               "nchunks": chk[-1], "ws_off": t64(ws_off or [0]), "fin_off": t64(fin), "fin_li": t32(fin_li or [0]),
+               "nfin": fin[-1], "ws": ws, "k_total": kk[-1], "n": seg[-1]}
+        self._tables[key] = hit
         return hit
 
-    def step(self, flat, sizes, name="bucket", out=None):
-        """flat: f32[sum(sizes)] gradients; returns the flat aggregated result (``out`` if given,
-        which may be ``flat`` itself: every tensor's result lands in place)."""
+    def local_step(self, flat, sizes, name="bucket", dense=None):
+        """This rank's half of the step: every tensor's compensate + top-k + residual update, the
+        payload (vals, GLOBAL idx) in self.last_payload, and the dense result into `dense` when
+        given (world 1; may be ``flat`` itself).  Returns the packed payload [vals | idx]."""
         g = ops.dev_f32(flat)
         n = g.numel()
-        seg_off, k_off, chk_off, chunk_seg, k_total, nchunks, ws = self.tables(sizes, g.device)
         if sum(int(s) for s in sizes) != n:
             raise ValueError("segment sizes do not add up to the buffer")
         res = self.residuals.get(name)
@@ -65,18 +89,31 @@ class SegmentedTopK:
         if not has:
             res = torch.empty_like(g)
             self.residuals[name] = res
+        T = self.tables(sizes, g.device, has, dense is not None)
+        k_total = T["k_total"]
         pay = torch.empty(2 * k_total, dtype=torch.float32, device=g.device)
         vals, idx = pay[:k_total], pay[k_total:].view(torch.int32)
-        W = int(self.world_size)
-        dense = (out if out is not None else torch.empty_like(g)) if W == 1 else None
         _lib.call("grace_topk_segmented_step", g.data_ptr(), res.data_ptr(), 1 if has else 0, self.beta, self.gamma,
-                  seg_off.data_ptr(), k_off.data_ptr(), chk_off.data_ptr(), chunk_seg.data_ptr(), len(sizes), n,
-                  nchunks, vals.data_ptr(), idx.data_ptr(), dense.data_ptr() if dense is not None else None,
-                  ws.data_ptr(), ws.numel(), ops._stream())
+                  T["seg_off"].data_ptr(), T["k_off"].data_ptr(), T["large"].data_ptr(), T["n_large"],
+                  T["small"].data_ptr(), T["n_small"], T["chk_off"].data_ptr(), T["chunk_li"].data_ptr(),
+                  T["nchunks"], T["ws_off"].data_ptr(), T["fin_off"].data_ptr(), T["fin_li"].data_ptr(), T["nfin"], n,
+                  vals.data_ptr(), idx.data_ptr(),
+                  dense.data_ptr() if dense is not None else None, T["ws"].data_ptr(), T["ws"].numel(), ops._stream())
         self.last_payload = (vals, idx)
+        return pay
+
+    def step(self, flat, sizes, name="bucket", out=None):
+        """flat: f32[sum(sizes)] gradients; returns the flat aggregated result (``out`` if given,
+        which may be ``flat`` itself: every tensor's result lands in place)."""
+        W = int(self.world_size)
         if W == 1:
+            dense = out if out is not None else torch.empty_like(ops.dev_f32(flat))
+            self.local_step(flat, sizes, name, dense)
             return dense
-        gathered = torch.empty(W * 2 * k_total, dtype=torch.float32, device=g.device)
+        pay = self.local_step(flat, sizes, name, None)
+        k_total = pay.numel() // 2
+        n = flat.numel()
+        gathered = torch.empty(W * 2 * k_total, dtype=torch.float32, device=pay.device)
         dist.all_gather_into_tensor(gathered, pay)
         return ops.sparse_aggregate(gathered, gathered[k_total:].view(torch.int32), 2 * k_total, [k_total] * W, W, n,
                                     W if self.average else 1, out=None if out is None else ops.fill(out, 0.0))

@@ -109,6 +109,38 @@ def reusable_output(slot, shape, dtype, device):
     return buf
 
 
+class OutputRecycler:
+    """Per-name recycled dense outputs of the world-1 top-k step.  A step's result is zero except at
+    its payload positions; when the caller has dropped it (no tensor or view of its storage left
+    outside this cache: the reusable_output test) and never modified it (the tensor version counter
+    that views share is unchanged), the next step of the same name on the same stream gets it back
+    together with the payload indices, and the kernels zero those positions and write only their
+    own selection instead of rewriting all n elements (grace_topk_residual_step_carry, prev_idx).
+    A caller that keeps or edits its results gets a fresh tensor and the dense write, as before."""
+
+    def __init__(self):
+        self._hit = {}
+
+    def take(self, name, like):
+        """(out tensor, prev_idx or None) for the next step of `name` shaped like `like`."""
+        hit = self._hit.pop(name, None)
+        if hit is not None:
+            buf, cdata, storage, version, prev_idx, key = hit
+            # references to buf: the popped tuple, the local name, getrefcount's argument
+            if (key == (like.numel(), like.device, _stream()) and _getrefcount(buf) == 3
+                    and _storage_uses(cdata) == 2 and buf._version == version):
+                return buf, prev_idx
+        return torch.empty_like(like), None
+
+    def keep(self, name, out, idx):
+        """Remember this step's result and its payload indices (int32, length k)."""
+        st = out.untyped_storage()
+        self._hit[name] = (out, st._cdata, st, out._version, idx, (out.numel(), out.device, _stream()))
+
+    def clear(self):
+        self._hit.clear()
+
+
 # ----------------------------------------------------------------------------- elementwise
 def axpby(r, g, beta, gamma, out=None):
     r, g = dev_f32(r, "residual"), dev_f32(g, "gradient")
@@ -214,6 +246,9 @@ def onebit_decode(mask0, mean0, mean1, quirk=False):
 
 
 # ----------------------------------------------------------------------------- top-k
+TOPK_SMALL_N = 32768   # topk.hip kSmallN: buckets up to this size run in one workgroup (dense writes)
+
+
 def ratio_k(numel, ratio):
     """k = max(1, int(numel * ratio)) (grace_dl/dist/compressor/topk.py:34)."""
     return max(1, int(numel * ratio))
@@ -251,21 +286,26 @@ def topk_step_dense(x, k, out=None):
 
 
 def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payload=None, carry=None,
-                       carry_valid=False):
+                       carry_valid=False, prev_idx=None):
     """carry: f32[topk_carry_size(n, k)] kept with `residual` (grace_topk_residual_step_carry);
-    carry_valid: it holds the samples the previous step of this residual wrote."""
+    carry_valid: it holds the samples the previous step of this residual wrote.  prev_idx: int32
+    payload indices of the earlier step whose result `out` still holds unmodified (a recycled
+    output: the step zeroes those and writes only its own selection)."""
     g = dev_f32(g)
     n = g.numel()
     buf, vals, idx = new_payload(k, g.device) if payload is None else payload
     ws = topk_workspace(n, k, g.device)
     if carry is not None and (carry.dtype != F32 or not carry.is_contiguous()):
         raise ValueError("grace_amd: the top-k carry is a contiguous float32 device tensor")
-    if carry is None:
+    if prev_idx is not None and (out is None or prev_idx.dtype != torch.int32 or not prev_idx.is_contiguous()):
+        raise ValueError("grace_amd: prev_idx needs an output and contiguous int32 indices")
+    if carry is None and prev_idx is None:
         _lib.call("grace_topk_residual_step", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
                   float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
     else:
         _lib.call("grace_topk_residual_step_carry", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
-                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(carry), carry.numel(), 1 if carry_valid else 0,
+                  float(gamma), n, k, _p(vals), _p(idx), _p(out), _p(carry), carry.numel() if carry is not None else 0,
+                  1 if carry_valid else 0, _p(prev_idx), prev_idx.numel() if prev_idx is not None else 0,
                   _p(ws), ws.numel(), _stream())
     return buf, vals, idx
 

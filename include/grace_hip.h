@@ -45,6 +45,13 @@ const char* grace_last_error(void);
  * top-k launch on `workspace` (0 = sampled fast path, 1 = exact fallback). */
 grace_status_t grace_read_status(const void* workspace, int32_t* status_host, void* stream);
 
+/* The streaming skeleton of the headline main pass (bench.py's HBM ceiling): topk_main with the
+ * same chunking, loads, stores and grid, but no classification -- r' = r + g, out = 0 written
+ * in place.  Its rate is the ceiling of the real pass's exact memory layout. */
+size_t grace_topk_stream_probe_workspace_bytes(int64_t n);
+grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, void* ws, size_t ws_bytes,
+                                       void* stream);
+
 /* Atomically read and clear a pinned host status word that kernels set bits in (system-scope
  * fetch_or): returns the bits set since the last take.  Host only, never blocks. */
 int32_t grace_status_take(int32_t* host_word);
@@ -146,12 +153,17 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
  * residual, with carry_valid != 0, the bracket derives r' at those positions from it instead of
  * reading r (half its random DRAM reads; the same sample bit for bit).  A stale carry (the residual
  * changed in between) only misplaces the sampled bracket, whose exact fallback keeps the result
- * exact.  carry_size 0: no carry for this (n, k); carry NULL: the plain step. */
+ * exact.  carry_size 0: no carry for this (n, k); carry NULL: the plain step.
+ * Recycled output (prev_idx != NULL, out != NULL): `out` must hold exactly the result of an earlier
+ * step of this call whose payload indices are prev_idx[0 .. prev_count) -- zero everywhere else,
+ * unmodified since.  The step then zeroes those positions and writes only the elements it selects
+ * instead of all n (same result, bit for bit; 4 B per element less traffic).  NULL: dense write. */
 int64_t grace_topk_carry_size(int64_t n, int64_t k);
 grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, int32_t has_residual,
                                               float beta, float gamma, int64_t n, int64_t k, float* vals,
                                               int32_t* idx, float* out, float* carry, int64_t carry_len,
-                                              int32_t carry_valid, void* ws, size_t ws_bytes, void* stream);
+                                              int32_t carry_valid, const int32_t* prev_idx, int64_t prev_count,
+                                              void* ws, size_t ws_bytes, void* stream);
 /* zeros(n).scatter_(idx, vals)  (topk.py:45-49; threshold.py:25-26; randomk.py:39-40). */
 grace_status_t grace_sparse_decode(const float* vals, const int32_t* idx, int64_t count, float* out,
                                    int64_t n, void* stream);
@@ -265,21 +277,31 @@ grace_status_t grace_cast_step_w1(const float* x, int64_t n, int32_t mode, uint6
 grace_status_t grace_fp16_decompress_aggregate(const void* half_in, int64_t stride, int32_t world, int64_t n,
                                                float divisor, float* out, void* stream);
 
-/* Per-tensor top-k + residual over many tensors in one launch sequence (grace_amd/csrc/segtopk.hip):
+/* Per-tensor top-k + residual over many tensors in one launch sequence (csrc/topk.hip "Segmented"):
  * the reference's per-parameter DDP loop (examples/dist/CIFAR10-dawndist/core.py:203-206, one
  * TopKCompressor(ratio) + ResidualMemory step per tensor, k_i = max(1, int(n_i * ratio)),
- * grace_dl/dist/compressor/topk.py:34).  The tensors are segments of one flat buffer; device tables:
- * seg_off[nseg + 1] (elements), k_off[nseg + 1] (payload), chk_off[nseg + 1] (chunks of
- * grace_topk_segmented_chunk() elements, per segment), chunk_seg[nchunks].  Payload
- * (vals f32, idx i32 GLOBAL indices)[k_off[nseg]]; out (dense world-1 result, may alias g) or NULL.
- * The workspace is zeroed once; keep one per segment table (its layout depends on nseg). */
-size_t grace_topk_segmented_workspace_bytes(int64_t n_total, int32_t nseg);
-int32_t grace_topk_segmented_chunk(void);
+ * grace_dl/dist/compressor/topk.py:34).  The tensors are segments of one flat buffer; three launches
+ * stream every element once: small segments (n <= grace_topk_segmented_small_max()) are selected
+ * exactly in one workgroup each, large ones get a sampled bracket, one main pass over their chunks
+ * and one finalize workgroup each (the single-bucket engine per segment).  Device tables:
+ * seg_off[nseg + 1] (elements), k_off[nseg + 1] (payload), large[n_large] / small[n_small] (segment
+ * ids), chk_off[n_large + 1] (main-pass chunks of grace_topk_segmented_chunk(has_residual,
+ * out != NULL) elements per large segment), chunk_li[nchunks] (large slot of each chunk),
+ * ws_off[n_large] (byte offsets of each large segment's grace_topk_segmented_seg_ws_bytes(n, k)
+ * workspace, 256-B aligned, zeroed once), fin_off[n_large + 1] / fin_li[nfin] (the finalize
+ * workgroups: grace_topk_segmented_fin_blocks(n, k) per large segment).  Payload (vals f32, idx i32 GLOBAL indices)[k_off[nseg]];
+ * out (dense world-1 result, may alias g) or NULL (world > 1: residual and payload only). */
+int32_t grace_topk_segmented_small_max(void);
+int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out);
+int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k);
+int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k);
 grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_t has_residual, float beta,
                                          float gamma, const int64_t* seg_off, const int64_t* k_off,
-                                         const int64_t* chk_off, const int32_t* chunk_seg, int32_t nseg,
-                                         int64_t n_total, int64_t nchunks, float* vals, int32_t* idx, float* out,
-                                         void* ws, size_t ws_bytes, void* stream);
+                                         const int32_t* large, int32_t n_large, const int32_t* small,
+                                         int32_t n_small, const int64_t* chk_off, const int32_t* chunk_li,
+                                         int64_t nchunks, const int64_t* ws_off, const int64_t* fin_off,
+                                         const int32_t* fin_li, int64_t nfin, int64_t n_total, float* vals,
+                                         int32_t* idx, float* out, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------- random-k / threshold */
 /* Random-k indices (randomk.py:11: randint(numel, [k]), WITH replacement) from a counter-based

@@ -142,3 +142,75 @@ def test_harness_real_backward_resnet9():
                 gj = grads[which][offs[j]:offs[j + 1]]
                 _, _, _, res[which][j], out = O.topk_residual_step(gj, res[which][j], 0.01)
                 assert same_bits(p.grad.detach().cpu().numpy().ravel(), out), (("loop", "segmented")[which], s, j)
+
+
+def _hash32(x):
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def _sample_positions(n):
+    """The segment bracket's sample positions (csrc/topk.hip seg_sample_n + sample_pos)."""
+    S = min(max(n // 128, 1024), 8192)
+    S = min(S, n // 4)
+    st = n // S
+    pos = []
+    for sidx in range(S):
+        off = (_hash32(sidx * 0x9E3779B9 + 0x5EED) * st) >> 32
+        pos.append(sidx * st + off)
+    return np.array(pos, dtype=np.int64)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_segmented_edge_segments(world):
+    """Large segments the sampled bracket must survive, next to small ones, bit-exact per tensor
+    against the oracle over three steps: an all-tie (constant) large tensor, a large tensor with
+    NaN / +-inf / -0 planted, one whose 3k largest elements avoid every sampled position (the
+    bracket misses: the segment's exact fallback), a mostly-zero one (k-th key 0), and segments
+    starting at odd offsets.  world 2 runs the residual-only mode (no dense output) and checks the
+    payload (global indices) and residual; the exchange itself is covered in test_gpu_w8.py."""
+    from grace_amd.dist.segmented import SegmentedTopK
+    ratio = 0.01
+    sizes = [3, 40000, 5, 50001, 65536, 7, 60000, 33000, 1]
+    rng = np.random.default_rng(31)
+    eng = SegmentedTopK(ratio, world_size=world)
+    res = [None] * len(sizes)
+    miss_pos = _sample_positions(65536)
+    for s in range(3):
+        gs = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+        gs[1][:] = np.float32(0.5)                                 # all ties
+        gs[3][[0, 7, 77, 777, 50000]] = [np.nan, np.inf, -np.inf, -0.0, np.nan]
+        g2 = (rng.random(65536).astype(np.float32) - np.float32(0.5))
+        free = np.setdiff1d(np.arange(65536), miss_pos)
+        g2[free[rng.permutation(free.size)[:3 * 655]]] = np.float32(1000.0)
+        gs[4] = g2                                                 # sampled bracket misses
+        z = np.zeros(60000, np.float32)
+        z[rng.permutation(60000)[:60]] = rng.standard_normal(60).astype(np.float32)
+        gs[6] = z                                                  # mostly zeros: the k-th key is 0
+        flat = torch.from_numpy(np.concatenate(gs)).cuda()
+        if world == 1:
+            out = eng.step(flat, sizes).cpu().numpy()
+        else:                                                      # the local half of the W > 1 step
+            eng.local_step(flat, sizes)
+        vals, idx = (t.cpu().numpy() for t in eng.last_payload)
+        idx = idx.astype(np.int64)
+        rcat = eng.residuals["bucket"].cpu().numpy()
+        off = koff = 0
+        for j, g in enumerate(gs):
+            n = g.size
+            _, v_or, i_or, res[j], o = O.topk_residual_step(g, res[j], ratio)
+            if world == 1:
+                assert same_bits(out[off:off + n], o), (s, j)
+            k = i_or.size
+            mine = idx[koff:koff + k] - off
+            order = np.argsort(mine)
+            assert np.array_equal(mine[order], i_or.astype(np.int64)), (s, j)
+            assert same_bits(vals[koff:koff + k][order], v_or), (s, j)
+            assert same_bits(rcat[off:off + n], res[j]), (s, j)
+            off += n
+            koff += k

@@ -1,0 +1,43 @@
+"""Diagnostic: per-segment state of the segmented top-k after each step of the bench's ddp_segmented
+scenario (ResNet-50 shapes, gradients rewritten in place by the step), read from the large segments'
+workspaces: status (1 = exact fallback), n_sure, n_cand, need, boundary bin size, k, n."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from grace_amd.dist.segmented import SegmentedTopK  # noqa: E402
+from grace_amd.harness import GradBucket, ShapeModel, step_segmented  # noqa: E402
+
+dev = torch.device("cuda", 0)
+model = ShapeModel(bench.resnet50_shapes(), dev)
+bucket = GradBucket(model)
+bucket.flat.normal_()
+eng = SegmentedTopK(0.01)
+sizes = bucket.sizes
+for step in range(4):
+    step_segmented(bucket, eng)
+    torch.cuda.synchronize()
+    for key, T in eng._tables.items():
+        if key[3] != (step > 0):
+            continue
+        ws = T["ws"].cpu().numpy()
+        offs = T["ws_off"].cpu().numpy()
+        large = T["large"].cpu().numpy()[:T["n_large"]]
+        rows = []
+        for li, s in enumerate(large):
+            c = ws[offs[li]:offs[li] + 64].view(np.uint32)
+            n = sizes[s]
+            k = max(1, int(n * 0.01))
+            st = ws[offs[li] + 64:offs[li] + 256].view(np.uint64)
+            us = lambda a, b: (int(st[b]) - int(st[a])) / 100.0   # noqa: E731
+            rows.append((int(s), n, k, int(c[3]), int(c[4]), int(c[5]), int(c[9]), int(c[7]),
+                         us(8, 9), us(9, 10), us(10, 11), us(11, 12), us(8, 12)))
+        fb = [r for r in rows if r[3]]
+        print(f"step {step}: {len(rows)} large segments, fallbacks {len(fb)}")
+        for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8]:
+            print("  seg %d n %d k %d status %d n_sure %d n_cand %d need %d n_bnd %d | fin us: findB %.1f route %.1f "
+                  "to_last %.1f bnd %.1f total %.1f" % r)
