@@ -589,6 +589,10 @@ __global__ __launch_bounds__(kDBlock) void dgc_w1_spec_kernel(const float* __res
   }
   __syncthreads();
   if (!s_last) return;
+  // the grid runs several workgroups per CU, outside the guide's measured fence-free row (one per
+  // CU): the last arriver keeps the agent-scope acquire before it reads the others' partials
+  // (MI355X_MICROARCH.md, Consumer condition (4); one invalidate in one workgroup per launch)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint32_t tot = 0;
   for (int64_t j = threadIdx.x; j < (int64_t)gridDim.x; j += kDBlock)
     tot += __hip_atomic_load(&part[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

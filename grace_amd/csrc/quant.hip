@@ -1836,6 +1836,13 @@ static unsigned qenc_pipe_grid(int64_t nbuckets) {
   return (unsigned)std::max<int64_t>(stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncPipeGridCap), need);
 }
 
+#ifdef GRACE_TERN_FLUSH
+__global__ void tern_flush_kernel(float* p, int64_t n) {
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4)
+    *reinterpret_cast<float4*>(p + i) = make_float4(1.f, 2.f, 3.f, 4.f);
+}
+#endif
+
 extern "C" {
 
 grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg,
@@ -2004,6 +2011,16 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
   tern_stats_kernel<<<(unsigned)nunits, kQBlock, 0, as_stream(stream)>>>(x, seg_off, unit_off, nseg, clip_in, w,
                                                                        scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
+#ifdef GRACE_TERN_FLUSH
+  // diagnostic A/B build only: stream 512 MiB of writes between the statistics pass and the
+  // encoder, so the encoder's re-read of x cannot be served by the 256 MiB Infinity Cache
+  {
+    static float* junk = nullptr;
+    constexpr int64_t kJunk = (int64_t)1 << 27;
+    if (!junk && hipMalloc(&junk, kJunk * sizeof(float)) != hipSuccess) junk = nullptr;
+    if (junk) tern_flush_kernel<<<4096, 256, 0, as_stream(stream)>>>(junk, kJunk);
+  }
+#endif
   if (u)
     tern_encode_kernel<false, true><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
         x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, scalars);

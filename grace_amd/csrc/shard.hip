@@ -115,6 +115,7 @@ __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
   if (t == 0) s_last = atomicAdd(&a.ctl->ticket1, 1u) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // several workgroups per CU possible: keep the acquire
   // last workgroup: the merged histogram into LDS (agent-scope loads), the global one re-zeroed
   uint32_t tot = 0;
   for (int b = t; b < kShBins; b += kShBlock) {
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   if (t == 0) s_last = atomicAdd(&a.ctl->ticket2, 1u) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // several workgroups per CU possible: keep the acquire
   const uint32_t nb = __hip_atomic_load(&a.ctl->nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // T: exactly `need` of the nb boundary entries have composite >= T (unique composites)
   uint64_t T;

@@ -1860,11 +1860,14 @@ grace_status_t grace_topk_compress(const float* x, int64_t n, int64_t k, float* 
 }
 
 grace_status_t grace_topk_step_dense(const float* x, int64_t n, int64_t k, float* vals, int32_t* idx, float* out,
-                                     void* ws, size_t ws_bytes_, void* stream) {
+                                     const int32_t* prev_idx, int64_t prev_count, void* ws, size_t ws_bytes_,
+                                     void* stream) {
   GRACE_REQUIRE(x && vals && idx && out && n > 0 && k >= 1 && k <= n && n < (int64_t)1 << 31,
                 "grace_topk_step_dense: bad arguments");
   GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_step_dense: workspace required");
   StepArgs a{x, nullptr, 1.f, 1.f, n, k, vals, idx, out};
+  a.prev_idx = prev_idx;
+  a.prev_count = prev_idx ? prev_count : 0;
   return run_topk<false, kDenseOut>(a, ws, ws_bytes_, as_stream(stream));
 }
 

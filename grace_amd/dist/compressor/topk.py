@@ -57,7 +57,12 @@ class TopKCompressor(Compressor):
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):
             # no memory, world 1: payload and (0 + d) / 1 from one read of the tensor
             g = ops.dev_f32(tensor)
-            _, _, _, out = ops.topk_step_dense(g, ops.ratio_k(g.numel(), self.compress_ratio))
+            recycle = self.recycle_output and g.numel() > ops.TOPK_SMALL_N
+            out, prev_idx = self._recycler.take(name, g) if recycle else (None, None)
+            _, _, idx, out = ops.topk_step_dense(g, ops.ratio_k(g.numel(), self.compress_ratio), out=out,
+                                                 prev_idx=prev_idx)
+            if recycle:
+                self._recycler.keep(name, out, idx)
             return out.view(tensor.shape)
         if not (isinstance(communicator, Allgather) and type(mem) is ResidualMemory
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):

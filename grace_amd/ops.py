@@ -273,15 +273,17 @@ def topk_compress(x, k):
     return buf, vals, idx
 
 
-def topk_step_dense(x, k, out=None):
+def topk_step_dense(x, k, out=None, prev_idx=None):
     """World-1 Allgather(TopK, NoneMemory).step in one streaming pass (grace_topk_step_dense): the
-    payload of topk_compress plus the dense (0 + decode) / 1 result; x is only read."""
+    payload of topk_compress plus the dense (0 + decode) / 1 result; x is only read.  prev_idx: the
+    payload indices of the earlier step whose result `out` still holds unmodified (recycled)."""
     x = dev_f32(x)
     n = x.numel()
     buf, vals, idx = new_payload(k, x.device)
     out = torch.empty(n, dtype=F32, device=x.device) if out is None else out
     ws = topk_workspace(n, k, x.device)
-    _lib.call("grace_topk_step_dense", _p(x), n, k, _p(vals), _p(idx), _p(out), _p(ws), ws.numel(), _stream())
+    _lib.call("grace_topk_step_dense", _p(x), n, k, _p(vals), _p(idx), _p(out), _p(prev_idx),
+              prev_idx.numel() if prev_idx is not None else 0, _p(ws), ws.numel(), _stream())
     return buf, vals, idx, out
 
 

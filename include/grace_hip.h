@@ -136,9 +136,11 @@ grace_status_t grace_topk_compress(const float* x, int64_t n, int64_t k, float* 
                                    void* ws, size_t ws_bytes, void* stream);
 /* Fused world-1 Communicator.step for TopK + NoneMemory (grace_dl/dist/__init__.py:47-51,
  * memory/none.py, allgather.py:40-45): the payload of grace_topk_compress and, in the same
- * streaming pass, out = (0 + zeros(n).scatter_(idx, vals)) / 1.  x is only read. */
+ * streaming pass, out = (0 + zeros(n).scatter_(idx, vals)) / 1.  x is only read.  prev_idx
+ * (may be NULL): recycled output, as grace_topk_residual_step_carry. */
 grace_status_t grace_topk_step_dense(const float* x, int64_t n, int64_t k, float* vals, int32_t* idx,
-                                     float* out, void* ws, size_t ws_bytes, void* stream);
+                                     float* out, const int32_t* prev_idx, int64_t prev_count, void* ws,
+                                     size_t ws_bytes, void* stream);
 /* Fused Communicator.step for TopK + ResidualMemory (grace_dl/dist/__init__.py:47-51):
  *   t = beta*r + gamma*g (t = g when has_residual == 0), payload = topk(t), r <- t - decode(payload)
  *   out (may be NULL): the world-1 Allgather result, zeros with t scattered at the payload.

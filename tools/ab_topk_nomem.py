@@ -31,7 +31,7 @@ for rnd in range(6):
         e0.record()
         for s in range(10):
             L.grace_topk_step_dense(gs[s % 3].data_ptr(), n, k, pay.data_ptr(), pay[k:].data_ptr(), out.data_ptr(),
-                                    wss[i].data_ptr(), wss[i].numel(), stream)
+                                    None, ctypes.c_int64(0), wss[i].data_ptr(), wss[i].numel(), stream)
         e1.record()
         torch.cuda.synchronize()
         ms = ctypes.c_float(0)
