@@ -243,47 +243,67 @@ def bench_topk(args, world, rank, dev):
         step(i)
     for i in range(args.warmup):        # warm-up steps, untimed and outside the kernel timer
         step(i)
+    rec = comm.compressor._recycler
+    hits0 = rec.hits
     ops.timer_enable(True)
     elapsed = timed(step, args.steps, 0, world, dev)
     main_ms, launches = ops.timer_collect()
     ops.timer_enable(False)
+    # world 1: each step's result is consumed and dropped, so every timed step reuses its bucket's
+    # previous result (ops.OutputRecycler): the main pass writes only its selection into the output
+    recycled = world == 1 and rec.hits - hits0 == args.steps
 
     line = base_line(args, world, elapsed, 4.0 * n)
     line["config"] = {"workload": "Allgather(TopK 1%, ResidualMemory).step on a 256 MiB fp32 bucket "
                                   "(BASELINE configs[1])",
-                      "numel": n, "k": k, "parallelism": f"dp{world} replicas, RCCL allgather of payloads"}
+                      "numel": n, "k": k, "parallelism": f"dp{world} replicas, RCCL allgather of payloads",
+                      "output": ("recycled: each step's dropped result is handed back; its k previous non-zeros "
+                                 "are cleared and only the new selection is written (bit-identical)")
+                      if recycled else "fresh dense output every step"}
     # roofline of the dominant kernel (topk_main), HIP events on the stream it runs on; only the
     # timed steps are counted (warm-up launches ran with the timer off)
     main_avg_ms = main_ms / max(launches, 1)
-    bytes_per_elem = 16 if world == 1 else 12          # g, r read; r' (+ dense out at W=1) written
-    main_bytes = bytes_per_elem * n
+    # g, r read; r' written; the dense output at world 1 -- all n elements (16 B), or with the
+    # recycled output only the selected ones (12 B + 4 B per selected element, ~k)
+    if world > 1:
+        main_bytes = 12 * n
+    elif recycled:
+        main_bytes = 12 * n + 4 * k
+    else:
+        main_bytes = 16 * n
     achieved = main_bytes / (main_avg_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": "topk_main", "kernel_avg_us": round(main_avg_ms * 1e3, 2), "launches": launches,
                 "algorithmic_bytes_per_launch": main_bytes}
     if world == 1:
-        step_bytes = 16 * n + 16 * k
+        # SURVEY.md §8d config 2 counts 16n + 16k (dense output); recycled: 12n for g, r, r', the
+        # payload 8k, the previous payload's indices read 4k and its positions cleared 4k, the new
+        # selection written 4k
+        step_bytes = 12 * n + 20 * k if recycled else 16 * n + 16 * k
         roofline["step_algorithmic_bytes"] = step_bytes
         roofline["step_frac"] = round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+        roofline["step_frac_of_16n"] = round((16 * n + 16 * k) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
     prof = os.path.join(ROOT, "profiles", "pmc_topk_main.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:
                 pmc = json.load(f)
-            if pmc.get("numel") == n and pmc.get("world") == world:
+            if pmc.get("numel") == n and pmc.get("world") == world and pmc.get("recycled", False) == recycled:
                 roofline["traffic"] = pmc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
     # the fraction against a bandwidth measured on this box as well -- the main
     # pass's own streaming skeleton (same kernel, chunking, loads and stores, no classification),
     # each launch right after a real step, timed like the main pass
-    skel, skel_med = skeleton_ceiling(step, main_bytes, n, dev) if not NO_PROBE and world == 1 else (None, None)
+    skel, skel_med = (skeleton_ceiling(step, main_bytes, n, dev, sparse=recycled) if not NO_PROBE and world == 1
+                      else (None, None))
     roofline["measured_copy_gbs"] = skel
     roofline["measured_copy_median_gbs"] = skel_med
     roofline["measured_copy_kind"] = ("grace_topk_stream_probe: the topk_main kernel itself with the classification "
-                                      "compiled out (same grid, chunks, 16-B non-temporal loads / stores of g, r, r', "
-                                      "out) on 3 rotated 256 MiB buffer sets, each launch interleaved with a real "
+                                      "compiled out (same grid, chunks, 16-B non-temporal loads / stores of g, r, r'"
+                                      + (", out untouched as with the recycled output" if recycled else ", out") +
+                                      ") on 3 rotated 256 MiB buffer sets, each launch interleaved with a real "
                                       "step, dispatch-packet events like the main pass; ceiling = fastest launch")
     roofline["frac_of_measured_copy"] = round(achieved / skel, 4) if skel else None
     roofline["frac_of_measured_copy_median"] = round(achieved / skel_med, 4) if skel_med else None
@@ -329,7 +349,7 @@ def bench_topk_two_streams(args, grads, names):
             "note": "bucket j on stream j % 2; not the headline value (that is one stream, in order)"}
 
 
-def skeleton_ceiling(step, main_bytes, n, dev, sets=3, rounds=12):
+def skeleton_ceiling(step, main_bytes, n, dev, sets=3, rounds=12, sparse=False):
     """The main pass's streaming ceiling on this box: grace_topk_stream_probe (topk_main with the
     classification compiled out: the same grid, loads and stores) on `sets` rotated buffer sets of
     n floats (g, r, out: 768 MiB each, more than the Infinity Cache), each launch right after a real
@@ -343,8 +363,8 @@ def skeleton_ceiling(step, main_bytes, n, dev, sets=3, rounds=12):
         step(i)
         g, r, o = bufs[i % sets]
         ops.timer_enable(True)
-        _lib.call("grace_topk_stream_probe", g.data_ptr(), r.data_ptr(), o.data_ptr(), n, ws.data_ptr(), ws.numel(),
-                  ops._stream())
+        _lib.call("grace_topk_stream_probe", g.data_ptr(), r.data_ptr(), o.data_ptr(), n, 1 if sparse else 0,
+                  ws.data_ptr(), ws.numel(), ops._stream())
         ms, cnt = ops.timer_collect()
         ops.timer_enable(False)
         if i >= sets and cnt == 1:
@@ -471,18 +491,25 @@ def bench_topk_nomem(args, world, rank, dev):
 
     for i in range(args.warmup):
         step(i)
+    rec = comm.compressor._recycler
+    hits0 = rec.hits
     ops.timer_enable(True)
     elapsed = timed(step, args.steps, 0, world, dev)
     main_ms, launches = ops.timer_collect()
     ops.timer_enable(False)
+    recycled = world == 1 and rec.hits - hits0 == args.steps
     t_unfused = timed(step_unfused, args.steps, args.warmup, world, dev)
     line = base_line(args, world, elapsed, 4.0 * n,
                      metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket, top-k 1 %, no memory")
     line["config"] = {"workload": "Allgather(TopK 1%, NoneMemory).step on a 256 MiB fp32 bucket (BASELINE.md section 4)",
                       "numel": n, "k": k, "unfused_ms_per_step": round(t_unfused / args.steps * 1e3, 4)}
-    step_bytes = 8 * n + 16 * k                     # 8n + 16k
+    # 8n + 16k; with the recycled output (each dropped result handed back)
+    # the dense write shrinks to the selection: 4n + payload 8k + previous indices 4k + their clear
+    # 4k + the new selection 4k
+    step_bytes = 4 * n + 20 * k if recycled else 8 * n + 16 * k
+    line["config"]["output"] = "recycled" if recycled else "fresh dense output every step"
     main_avg_ms = main_ms / max(launches, 1)
-    main_bytes = (8 if world == 1 else 4) * n       # g read (+ dense out written at world 1)
+    main_bytes = (4 * n + 4 * k if recycled else 8 * n) if world == 1 else 4 * n
     t = elapsed / args.steps
     traffic, ratio = pmc_traffic("topk_nomem", step_bytes)
     line["roofline"] = {"bound": "hbm", "achieved": round(step_bytes / t / 1e9, 1), "peak": HBM_PEAK_GBS,

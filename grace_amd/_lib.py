@@ -25,7 +25,7 @@ SIGNATURES = {
     "grace_read_status": (ST, [P, P, P]),
     "grace_status_take": (ctypes.c_int32, [P]),
     "grace_topk_stream_probe_workspace_bytes": (SZ, [I64]),
-    "grace_topk_stream_probe": (ST, [P, P, P, I64, P, SZ, P]),
+    "grace_topk_stream_probe": (ST, [P, P, P, I64, I32, P, SZ, P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
     "grace_timer_collect": (ST, [P, P]),
     "grace_event_create": (ST, [P]),

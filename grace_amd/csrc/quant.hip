@@ -1211,7 +1211,11 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
 #pragma unroll
     for (int k = 0; k < kTernSub; ++k) {
       const int64_t j = t + (int64_t)(st * kTernSub + k) * kTernBlock;
+#ifdef GRACE_TERN_ENC_PLAIN   // A/B build only: the re-read of x with plain (cache-allocating) loads
+      if (nq > 0) dst[k] = xq[j < nq ? j : 0];
+#else
       if (nq > 0) dst[k] = __builtin_nontemporal_load(xq + (j < nq ? j : 0));
+#endif
     }
   };
   f4v cur[kTernSub], nxt[kTernSub];

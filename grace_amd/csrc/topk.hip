@@ -1754,8 +1754,8 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
 
 size_t grace_topk_stream_probe_workspace_bytes(int64_t n) { return ws_bytes(n, 1); }
 
-grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, void* ws, size_t ws_bytes_,
-                                       void* stream) {
+grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, int32_t sparse, void* ws,
+                                       size_t ws_bytes_, void* stream) {
   GRACE_REQUIRE(g && r && out && ws && n >= 1 && n < ((int64_t)1 << 31) &&
                     ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r) |
                       reinterpret_cast<uintptr_t>(out)) & 15u) == 0,
@@ -1765,7 +1765,10 @@ grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int
   StepArgs a{g, r, 1.f, 1.f, n, 1, nullptr, nullptr, out};
   const unsigned nblk = (unsigned)((n + kChunkOf<true, kDenseFused> - 1) / kChunkOf<true, kDenseFused>);
   // timed like the real pass (the event timer rides on the dispatch packet when it is enabled)
-  launch_timed(topk_main<true, kDenseFused, true, true>, dim3(nblk), dim3(kMainBlock), as_stream(stream), a, w);
+  if (sparse)   // the recycled-output layout: g, r read, r' written, out untouched
+    launch_timed(topk_main<true, kDenseFused, true, true, true>, dim3(nblk), dim3(kMainBlock), as_stream(stream), a, w);
+  else
+    launch_timed(topk_main<true, kDenseFused, true, true>, dim3(nblk), dim3(kMainBlock), as_stream(stream), a, w);
   GRACE_CHECK_LAUNCH("grace_topk_stream_probe");
   return GRACE_OK;
 }

@@ -120,6 +120,8 @@ class OutputRecycler:
 
     def __init__(self):
         self._hit = {}
+        self.hits = 0      # steps that got their previous result back (sparse write)
+        self.misses = 0    # steps that allocated (first step, result held / edited, other stream)
 
     def take(self, name, like):
         """(out tensor, prev_idx or None) for the next step of `name` shaped like `like`."""
@@ -129,7 +131,9 @@ class OutputRecycler:
             # references to buf: the popped tuple, the local name, getrefcount's argument
             if (key == (like.numel(), like.device, _stream()) and _getrefcount(buf) == 3
                     and _storage_uses(cdata) == 2 and buf._version == version):
+                self.hits += 1
                 return buf, prev_idx
+        self.misses += 1
         return torch.empty_like(like), None
 
     def keep(self, name, out, idx):

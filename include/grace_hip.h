@@ -46,11 +46,12 @@ const char* grace_last_error(void);
 grace_status_t grace_read_status(const void* workspace, int32_t* status_host, void* stream);
 
 /* The streaming skeleton of the headline main pass (bench.py's HBM ceiling): topk_main with the
- * same chunking, loads, stores and grid, but no classification -- r' = r + g, out = 0 written
- * in place.  Its rate is the ceiling of the real pass's exact memory layout. */
+ * same chunking, loads, stores and grid, but no classification -- r' = r + g and (sparse == 0)
+ * out = 0 written in place; sparse != 0 is the recycled-output layout (out untouched).  Its rate
+ * is the ceiling of the real pass's exact memory layout. */
 size_t grace_topk_stream_probe_workspace_bytes(int64_t n);
-grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, void* ws, size_t ws_bytes,
-                                       void* stream);
+grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, int32_t sparse, void* ws,
+                                       size_t ws_bytes, void* stream);
 
 /* Atomically read and clear a pinned host status word that kernels set bits in (system-scope
  * fetch_or): returns the bits set since the last take.  Host only, never blocks. */

@@ -32,7 +32,7 @@ for step in ${STEPS:-pytest smoke bench}; do
     exp) run exp 600 python3 ${EXP} ;;
     ternab) # TernGrad: does the encoder's re-read of x hit the Infinity Cache?  The same bench with a
             # 512 MiB write stream between the statistics pass and the encoder (ternflush build)
-            for lib in libgrace_hip libgrace_hip_ternflush; do
+            for lib in libgrace_hip libgrace_hip_ternflush libgrace_hip_ternplain; do
               GRACE_HIP_LIB=grace_amd/lib/$lib.so GRACE_BENCH_NO_PROBE=1 run prof_tern_$lib 300 rocprofv3 --kernel-trace \
                 --stats --output-format csv -d gpurun_out/prof_${TAG}_tern_$lib -o run \
                 -- python3 bench.py --workload terngrad --steps 50 --warmup 5 --no-cpu-baseline
