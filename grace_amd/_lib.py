@@ -128,7 +128,8 @@ SIGNATURES = {
     "grace_gather": (ST, [P, P, I64, P, P]),
     "grace_randomk_step_w1": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, P]),
     "grace_randomk_step_w1_dense_workspace_bytes": (SZ, [I64, I64]),
-    "grace_randomk_step_w1_dense": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, SZ, P]),
+    "grace_randomk_group_bytes": (SZ, [I64, I64]),
+    "grace_randomk_step_w1_dense": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, P, P, SZ, P]),
     "grace_threshold_workspace_bytes": (SZ, [I64]),
     "grace_threshold_count": (ST, [P, I64, F32, P, P]),
     "grace_threshold_recount": (ST, [P, I64, F32, P, P]),

@@ -87,12 +87,17 @@ hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t
 constexpr int kRkChunkLog = 13;                  // = payload.hip kPChunkLog
 constexpr int kRkChunk = 1 << kRkChunkLog;
 constexpr int kRkQ = kRkChunk / (4 * kSBlock);   // quads per thread per array
-template <bool HAS_RES>
+// SPARSE (recycled output): `out` holds the previous step's result of this name, non-zero only at
+// the previous grouping (poffs / pends): those positions not drawn again are cleared, and only the
+// drawn ones are written (out is not streamed; r' still is)
+template <bool HAS_RES, bool SPARSE>
 __global__ __launch_bounds__(kSBlock) void randomk_dense_pass_kernel(const float* __restrict__ g, float* __restrict__ r,
                                                                     float beta, float gamma, int64_t n,
                                                                     const uint16_t* __restrict__ offs,
                                                                     const uint32_t* __restrict__ ends,
-                                                                    float* __restrict__ out) {
+                                                                    float* __restrict__ out,
+                                                                    const uint16_t* __restrict__ poffs,
+                                                                    const uint32_t* __restrict__ pends) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ uint32_t bm[kRkChunk / 32];
   const int64_t c = blockIdx.x;
@@ -117,6 +122,13 @@ __global__ __launch_bounds__(kSBlock) void randomk_dense_pass_kernel(const float
     atomicOr(&bm[o >> 5], 1u << (o & 31));
   }
   __syncthreads();
+  if constexpr (SPARSE) {   // the previous result's non-zeros in this chunk, unless drawn again
+    const uint32_t p0 = c > 0 ? pends[c - 1] : 0u, p1 = pends[c];
+    for (uint32_t j = p0 + t; j < p1; j += kSBlock) {
+      const uint32_t o = poffs[j];
+      if (!((bm[o >> 5] >> (o & 31)) & 1u)) out[c0 + o] = 0.f;
+    }
+  }
   auto one = [&](float tv, int64_t i, float& o, float& rr) {
     const int64_t l = i - c0;
     const bool sel = (bm[l >> 5] >> (l & 31)) & 1u;
@@ -137,8 +149,12 @@ __global__ __launch_bounds__(kSBlock) void randomk_dense_pass_kernel(const float
         one(tt[j], e + j, a, b);
         o[j] = a;
         rr[j] = b;
+        if constexpr (SPARSE) {
+          const int64_t l = e + j - c0;
+          if ((bm[l >> 5] >> (l & 31)) & 1u) out[e + j] = a;
+        }
       }
-      __builtin_nontemporal_store(o, reinterpret_cast<f4*>(out + e));
+      if constexpr (!SPARSE) __builtin_nontemporal_store(o, reinterpret_cast<f4*>(out + e));
       __builtin_nontemporal_store(rr, reinterpret_cast<f4*>(r + e));
     }
   } else {
@@ -146,7 +162,8 @@ __global__ __launch_bounds__(kSBlock) void randomk_dense_pass_kernel(const float
       const float tv = HAS_RES ? beta * r[i] + gamma * g[i] : g[i];
       float a, b;
       one(tv, i, a, b);
-      out[i] = a;
+      const int64_t l = i - c0;
+      if (!SPARSE || ((bm[l >> 5] >> (l & 31)) & 1u)) out[i] = a;
       r[i] = b;
     }
   }
@@ -653,25 +670,48 @@ size_t grace_randomk_step_w1_dense_workspace_bytes(int64_t n, int64_t k) {
   return 256 + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255) + sizeof(uint16_t) * (size_t)(k < 1 ? 1 : k);
 }
 
+size_t grace_randomk_group_bytes(int64_t n, int64_t k) {
+  const int64_t nch = (n + kRkChunk - 1) / kRkChunk;
+  return ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255) + sizeof(uint16_t) * (size_t)(k < 1 ? 1 : k);
+}
+
 grace_status_t grace_randomk_step_w1_dense(const float* g, float* residual, int32_t has_residual, float beta,
                                            float gamma, int64_t n, const int64_t* idx, int64_t k, float* out,
-                                           void* ws, size_t ws_bytes, void* stream) {
+                                           void* grp, const void* prev_grp, void* ws, size_t ws_bytes,
+                                           void* stream) {
   GRACE_REQUIRE(g && residual && out && ws && n >= 1 && n < ((int64_t)1 << 31) && k >= 0 && (k == 0 || idx) &&
                     ws_bytes >= grace_randomk_step_w1_dense_workspace_bytes(n, k),
                 "grace_randomk_step_w1_dense: bad arguments (n < 2^31, workspace)");
   const int64_t nch = (n + kRkChunk - 1) / kRkChunk;
   GRACE_REQUIRE(nch <= 32768, "grace_randomk_step_w1_dense: n <= 2^28");
+  GRACE_REQUIRE(!prev_grp || grp, "grace_randomk_step_w1_dense: a recycled output needs this step's grouping buffer");
   hipStream_t s = as_stream(stream);
   char* p = reinterpret_cast<char*>(ws);
   uint32_t* ticket = reinterpret_cast<uint32_t*>(p);
-  uint32_t* ends = reinterpret_cast<uint32_t*>(p + 256);
-  uint16_t* offs = reinterpret_cast<uint16_t*>(p + 256 + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255));
+  // this step's grouping: into the caller's per-name buffer `grp` (it becomes the next step's
+  // prev_grp), or into the workspace
+  char* q = grp ? reinterpret_cast<char*>(grp) : p + 256;
+  const size_t eb = (sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255;
+  uint32_t* ends = reinterpret_cast<uint32_t*>(q);
+  uint16_t* offs = reinterpret_cast<uint16_t*>(q + eb);
+  const uint32_t* pends = prev_grp ? reinterpret_cast<const uint32_t*>(prev_grp) : nullptr;
+  const uint16_t* poffs = prev_grp ? reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(prev_grp) + eb) : nullptr;
   const hipError_t e = group_by_chunk<int64_t>(nullptr, idx, k, nch, nullptr, offs, ends, ticket, s);
   if (e != hipSuccess) { set_error("grace_randomk_step_w1_dense", e); return GRACE_ERR_HIP; }
-  if (has_residual)
-    randomk_dense_pass_kernel<true><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out);
-  else
-    randomk_dense_pass_kernel<false><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out);
+  if (prev_grp) {
+    if (has_residual)
+      randomk_dense_pass_kernel<true, true><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out,
+                                                                            poffs, pends);
+    else
+      randomk_dense_pass_kernel<false, true><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends,
+                                                                             out, poffs, pends);
+  } else if (has_residual) {
+    randomk_dense_pass_kernel<true, false><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out,
+                                                                           nullptr, nullptr);
+  } else {
+    randomk_dense_pass_kernel<false, false><<<(unsigned)nch, kSBlock, 0, s>>>(g, residual, beta, gamma, n, offs, ends, out,
+                                                                            nullptr, nullptr);
+  }
   GRACE_CHECK_LAUNCH("grace_randomk_step_w1_dense");
   return GRACE_OK;
 }

@@ -15,11 +15,14 @@ from grace_amd.dist import Compressor
 
 class RandomKCompressor(Compressor):
 
-    def __init__(self, compress_ratio, rng="device"):
+    def __init__(self, compress_ratio, rng="device", recycle_output=True):
         super().__init__()
         self.global_step = 0
         self.compress_ratio = compress_ratio
         self.rng = rng
+        self.recycle_output = recycle_output   # world-1 step: reuse a dropped, unmodified result
+        self._recycler = ops.OutputRecycler()
+        self._grp = {}
 
     def _indices(self, flat, name):
         """randomk.py:26-30: the seed h, the global generator reseeded with it, k indices drawn with
@@ -50,7 +53,23 @@ class RandomKCompressor(Compressor):
             res = torch.empty_like(g)
         indices = self._indices(g, name)
         if g.numel() <= ops.SORT_PAYLOAD_MAX_N:
-            out = ops.randomk_step_w1_dense(g, res, has, mem.beta, mem.gamma, indices)
+            if self.recycle_output:
+                # the dropped, unmodified previous result of this name comes back (ops.OutputRecycler)
+                # with the grouping of its indices: only those positions are cleared and only the
+                # drawn ones written; the two grouping buffers of a name alternate
+                out, prev = self._recycler.take(name, g)
+                key = (g.numel(), indices.numel(), g.device)
+                bufs = self._grp.get(name)
+                if bufs is None or bufs[0] != key:
+                    nb = ops.randomk_group_bytes(g.numel(), indices.numel())
+                    bufs = self._grp[name] = (key, [torch.empty(nb, dtype=torch.uint8, device=g.device) for _ in range(2)])
+                    prev = None
+                grp = bufs[1][1] if prev is bufs[1][0] else bufs[1][0]
+                out = ops.randomk_step_w1_dense(g, res, has, mem.beta, mem.gamma, indices, out=out, grp=grp,
+                                                prev_grp=prev)
+                self._recycler.keep(name, out, grp)
+            else:
+                out = ops.randomk_step_w1_dense(g, res, has, mem.beta, mem.gamma, indices)
         else:
             _, out = ops.randomk_step_w1(g, res, has, mem.beta, mem.gamma, indices)
         mem.residuals[name] = res

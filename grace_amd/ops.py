@@ -706,19 +706,28 @@ def randomk_step_w1(g, residual, has_residual, beta, gamma, idx):
     return vals, out
 
 
-def randomk_step_w1_dense(g, residual, has_residual, beta, gamma, idx, out=None):
+def randomk_step_w1_dense(g, residual, has_residual, beta, gamma, idx, out=None, grp=None, prev_grp=None):
     """The world-1 step's out (and r' in `residual`) in one streaming pass after grouping the indices
-    by chunk (grace_randomk_step_w1_dense); no payload."""
+    by chunk (grace_randomk_step_w1_dense); no payload.  grp: a per-name uint8 buffer of
+    randomk_group_bytes(n, k) receiving this step's grouping; prev_grp: the grouping of the earlier
+    step whose result `out` still holds unmodified (recycled output: only its non-zeros are
+    cleared and only the drawn positions written)."""
     g = dev_f32(g)
     idx = require_dev(idx, "indices")
     if idx.dtype != torch.int64:
         raise ValueError("grace_amd: random-k indices are int64")
+    if prev_grp is not None and (out is None or grp is None):
+        raise ValueError("grace_amd: a recycled random-k output needs `out` and this step's `grp`")
     out = torch.empty_like(g) if out is None else out
     n, k = g.numel(), idx.numel()
     ws = workspace("randomk_w1", _lib.query("grace_randomk_step_w1_dense_workspace_bytes", n, k), g.device)
     _lib.call("grace_randomk_step_w1_dense", _p(g), _p(residual), 1 if has_residual else 0, float(beta),
-              float(gamma), n, _p(idx), k, _p(out), _p(ws), ws.numel(), _stream())
+              float(gamma), n, _p(idx), k, _p(out), _p(grp), _p(prev_grp), _p(ws), ws.numel(), _stream())
     return out
+
+
+def randomk_group_bytes(n, k):
+    return int(_lib.query("grace_randomk_group_bytes", int(n), int(k)))
 
 
 def gather(x, idx):

@@ -329,11 +329,17 @@ grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t ha
 /* The same world-1 step without materialising the payload (only `out` is the step's result at
  * world 1): the indices are grouped by 8192-element chunk, then ONE streaming pass writes r' and
  * out (16 B per element, no random gathers / scatters); bit-identical out and r'.  n < 2^31 and
- * n <= 2^28; ws: grace_randomk_step_w1_dense_workspace_bytes, zeroed once at allocation. */
+ * n <= 2^28; ws: grace_randomk_step_w1_dense_workspace_bytes, zeroed once at allocation.
+ * grp (may be NULL): a caller-owned buffer of grace_randomk_group_bytes(n, k) that receives this
+ * step's grouping of the indices.  prev_grp (may be NULL, needs grp): recycled output -- `out`
+ * holds exactly the result of the earlier step whose grouping prev_grp is, unmodified since; its
+ * non-zeros that are not drawn again are cleared and only the drawn positions are written. */
 size_t grace_randomk_step_w1_dense_workspace_bytes(int64_t n, int64_t k);
+size_t grace_randomk_group_bytes(int64_t n, int64_t k);
 grace_status_t grace_randomk_step_w1_dense(const float* g, float* residual, int32_t has_residual, float beta,
                                            float gamma, int64_t n, const int64_t* idx, int64_t k, float* out,
-                                           void* ws, size_t ws_bytes, void* stream);
+                                           void* grp, const void* prev_grp, void* ws, size_t ws_bytes,
+                                           void* stream);
 /* Threshold (threshold.py:16-19): idx = where(|x| >= min(thr, max(x))) in ascending order.
  * count -> (host reads meta = ws[0..2]: bound bits, count, recount flag) -> [recount] -> write.
  * The caller synchronises once to size the variable-length payload. */

@@ -102,3 +102,31 @@ def test_recycled_output_two_names_and_streams():
             _, _, _, r_or[j], out_or = O.topk_residual_step(gs[j][s], r_or[j], 0.01)
             assert same_bits(_np(outs[j]), out_or), (s, j)
         del outs
+
+
+def test_randomk_recycled_output_equals_dense():
+    """World-1 Allgather(RandomK 1 %, Residual).step with the recycled output (the previous grouping
+    of the drawn indices clears the old non-zeros; duplicates and re-drawn positions included)
+    equals the dense-write step bit for bit, and held results are never touched."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.randomk import RandomKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = (1 << 20) + 5
+    rec = Allgather(RandomKCompressor(0.01, recycle_output=True), ResidualMemory(), 1)
+    ref = Allgather(RandomKCompressor(0.01, recycle_output=False), ResidualMemory(), 1)
+    gs = _grads(n, 7, 21)
+    held = []
+    hits = 0
+    for s, g in enumerate(gs):
+        gt = torch.from_numpy(g).to(DEV)
+        o1 = rec.step(gt, "b")
+        o2 = ref.step(gt, "b")
+        assert same_bits(_np(o1), _np(o2)), s
+        assert same_bits(_np(rec.memory.residuals["b"]), _np(ref.memory.residuals["b"])), s
+        if s == 2:
+            held.append((o1, _np(o2).copy()))
+        del o1, o2
+    hits = rec.compressor._recycler.hits
+    assert hits >= 4
+    for t, exp in held:
+        assert same_bits(_np(t), exp)
