@@ -94,7 +94,10 @@ struct AccOp {
 
 struct FillOp {
   float v; float* o;
-  __device__ void vec(int64_t i) const { reinterpret_cast<float4*>(o)[i] = make_float4(v, v, v, v); }
+  __device__ void vec(int64_t i) const {   // write-only stream: non-temporal 16-B stores
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{v, v, v, v}, reinterpret_cast<f4v*>(o) + i);
+  }
   __device__ void one(int64_t i) const { o[i] = v; }
 };
 

@@ -37,6 +37,7 @@ constexpr int kShPer = 4;            // entries per thread per round (all loads 
 constexpr int kShBins = 32768;       // key >> 16: 1/128-octave bins
 constexpr int kShMaxWorld = 1024;
 constexpr int kShMaxGrid = 512;
+constexpr unsigned kShHistGrid = 32;
 
 struct ShCtl {
   int32_t b1;        // boundary bin; -1 = every valid entry is selected
@@ -116,13 +117,20 @@ __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
   __syncthreads();
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // several workgroups per CU possible: keep the acquire
-  // last workgroup: the merged histogram into LDS (agent-scope loads), the global one re-zeroed
+  // last workgroup (after the acquire): the merged histogram into LDS with every 16-B load in
+  // flight at once (one agent-scope atomic load per bin was a chain of 32 round trips per thread),
+  // the global one re-zeroed
+  constexpr int kV = kShBins / 4 / kShBlock;
+  uint4* hg = reinterpret_cast<uint4*>(a.hist);
+  uint4 hv[kV];
+#pragma unroll
+  for (int u = 0; u < kV; ++u) hv[u] = hg[t + u * kShBlock];
   uint32_t tot = 0;
-  for (int b = t; b < kShBins; b += kShBlock) {
-    const uint32_t c = __hip_atomic_load(&a.hist[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h[b] = c;
-    tot += c;
-    a.hist[b] = 0u;
+#pragma unroll
+  for (int u = 0; u < kV; ++u) {
+    reinterpret_cast<uint4*>(h)[t + u * kShBlock] = hv[u];
+    tot += hv[u].x + hv[u].y + hv[u].z + hv[u].w;
+    hg[t + u * kShBlock] = make_uint4(0u, 0u, 0u, 0u);
   }
   uint32_t total;
   block_excl_scan<kShBlock>(tot, s_w, &total);   // also a barrier: h complete
@@ -167,11 +175,11 @@ __device__ __forceinline__ void shard_take(const ShArgs& a, bool sel, uint32_t w
   }
 }
 
-struct BndComp {   // composite key of boundary entry j (agent-scope load of the list)
+struct BndComp {   // composite key of boundary entry j (plain loads: read after the last arriver's acquire)
   const ShArgs* a;
   const int64_t* base;
   __device__ uint64_t operator()(int64_t jj) const {
-    const uint32_t e = __hip_atomic_load(&a->bnd[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t e = a->bnd[jj];
     uint32_t w, j;
     split_entry(e, (uint32_t)a->cap, w, j);
     const int64_t gi = base[w] + rec_idx(*a, w)[j];
@@ -183,6 +191,8 @@ struct BndComp {   // composite key of boundary entry j (agent-scope load of the
 __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   __shared__ int64_t s_base[kShMaxWorld];
   __shared__ uint32_t hsel[2048];
+  __shared__ uint32_t s_bnd[kShBlock * kShPer];   // this round's boundary entries, staged
+  __shared__ uint32_t s_cnt, s_gbase;
   __shared__ uint32_t s_w[kShBlock / kWave + 1];
   __shared__ uint32_t s_res[2];
   __shared__ uint32_t s_last;
@@ -190,17 +200,20 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
   const int32_t b1 = a.ctl->b1;         // written by shard_hist (kernel boundary)
   const uint32_t need = a.ctl->need;
+  if (t == 0) s_cnt = 0u;
   __syncthreads();
   const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
   const uint32_t step = gridDim.x * kShBlock * kShPer;
-  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += step) {
+  // uniform rounds (the workgroup barriers below): every thread runs every round
+  for (uint32_t r0 = blockIdx.x * kShBlock * kShPer; r0 < N; r0 += step) {
+    const uint32_t e0 = r0 + t;
     int32_t li[kShPer];
     float v[kShPer];
 #pragma unroll
     for (int u = 0; u < kShPer; ++u) {
       const uint32_t e = e0 + u * kShBlock;
       uint32_t w, j;
-      split_entry(e < N ? e : e0, cap, w, j);
+      split_entry(e < N ? e : N - 1, cap, w, j);
       li[u] = rec_idx(a, w)[j];
       v[u] = rec_vals(a, w)[j];
     }
@@ -219,16 +232,27 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
           if (!inb) shard_take(a, kb > b1, w, j, li[u], v[u], s_base[w]);
         }
       }
-      // boundary entries: one atomic per wave, write-through (sc1) stores for the last arriver
+      // boundary entries staged in LDS (one LDS atomic per wave); the round's list leaves with ONE
+      // global reservation per workgroup (a device atomic per wave on the one counter serialised
+      // thousands of round trips: the select took 157 us at W = 8)
       const uint64_t m = __ballot(inb);
       if (m) {
         uint32_t base0 = 0;
-        if (lane_rank(m) == 0 && inb) base0 = atomicAdd(&a.ctl->nb, (uint32_t)__popcll(m));
-        const int leader = __builtin_ctzll(m);
-        base0 = __shfl(base0, leader, 64);
-        if (inb) __hip_atomic_store(&a.bnd[base0 + lane_rank(m)], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane_rank(m) == 0 && inb) base0 = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+        base0 = __shfl(base0, __builtin_ctzll(m), 64);
+        if (inb) s_bnd[base0 + lane_rank(m)] = e;
       }
     }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    if (t == 0 && cnt) s_gbase = atomicAdd(&a.ctl->nb, cnt);
+    __syncthreads();
+    // write-through (sc1) stores for the last arriver
+    for (uint32_t q = t; q < cnt; q += kShBlock)
+      __hip_atomic_store(&a.bnd[s_gbase + q], s_bnd[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (t == 0) s_cnt = 0u;
+    __syncthreads();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -250,7 +274,7 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
     T = block_select_comp<kShBlock>(src, (int64_t)nb, need, hsel, s_w, s_res, 1, p0, 0x7FFull << 53);
   }
   for (uint32_t jj = t; jj < nb; jj += kShBlock) {
-    const uint32_t e = __hip_atomic_load(&a.bnd[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t e = a.bnd[jj];
     uint32_t w, j;
     split_entry(e, cap, w, j);
     const int32_t li = rec_idx(a, w)[j];
@@ -307,8 +331,11 @@ grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t ra
   const int64_t N = (int64_t)world * cap;
   int64_t g = (N + kShBlock * kShPer - 1) / (kShBlock * kShPer);
   const unsigned grid = (unsigned)(g < 1 ? 1 : (g > kShMaxGrid ? kShMaxGrid : g));
+  // the histogram flush's device atomics all land on the few bins around the k-th key: fewer
+  // workgroups, each looping over more entries, means fewer atomics per bin
+  const unsigned hgrid = grid < kShHistGrid ? grid : kShHistGrid;
   hipStream_t s = as_stream(stream);
-  shard_hist_kernel<<<grid, kShBlock, 0, s>>>(a);
+  shard_hist_kernel<<<hgrid, kShBlock, 0, s>>>(a);
   GRACE_CHECK_LAUNCH("grace_shard_select");
   shard_apply_kernel<<<grid, kShBlock, 0, s>>>(a);
   GRACE_CHECK_LAUNCH("grace_shard_select");

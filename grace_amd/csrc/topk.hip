@@ -1524,7 +1524,12 @@ __global__ void tag_divide_kernel(const int32_t* idx, int64_t stride, AggCum cum
 //            last arriver -- boundary bin, exact ranking by (|t| desc, index asc), or the
 //            segment's exact fallback when its bracket missed.
 // Payload indices are global (flat-buffer) indices (StepArgs::idx_base = the segment's offset).
-constexpr int kSegSampleMin = 1024, kSegSampleMax = 8192;
+// sample sizes: every sample is two random DRAM reads (g, r), and the bracket launch is bound by
+// their row activations: 8192 per large segment (45 ResNet-50 tensors, 737 K reads) took 47 us
+#ifndef GRACE_SEG_SAMPLE_MAX
+#define GRACE_SEG_SAMPLE_MAX 2048
+#endif
+constexpr int kSegSampleMin = 512, kSegSampleMax = GRACE_SEG_SAMPLE_MAX;
 
 struct SegPlan {
   const float* g;
@@ -1584,7 +1589,7 @@ __device__ __forceinline__ TopkWs seg_ws(const SegPlan& p, int li, int64_t n, in
   return w;
 }
 __device__ __forceinline__ int64_t seg_sample_n(int64_t n) {
-  int64_t S = n / 128;
+  int64_t S = n / 256;
   S = S < kSegSampleMin ? kSegSampleMin : (S > kSegSampleMax ? kSegSampleMax : S);
   return S < n / 4 ? S : n / 4;
 }

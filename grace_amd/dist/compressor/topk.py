@@ -22,8 +22,11 @@ class TopKCompressor(Compressor):
         super().__init__()
         self.compress_ratio = compress_ratio
         self.kernel = kernel
-        # world-1 fused step: reuse a dropped, unmodified previous result of the same name and
-        # rewrite only its non-zeros (ops.OutputRecycler); False = a fresh dense output every step
+        # world-1 step WITHOUT memory: reuse a dropped, unmodified previous result of the same name
+        # and rewrite only its non-zeros (ops.OutputRecycler; A/B r04: 0.1356 -> 0.1272 ms).  The
+        # residual step keeps the dense write: next to its g, r, r' streams the scattered writes
+        # cost more than the 4 B per element they save (0.2137 -> 0.2294 ms, tools/ab_recycle.py);
+        # recycle_output="always" turns it on there as well, False everywhere off.
         self.recycle_output = recycle_output
         self._recycler = ops.OutputRecycler()
 
@@ -77,7 +80,8 @@ class TopKCompressor(Compressor):
         world = int(communicator.world_size)
         carry, carry_valid = mem.carry_for(name, res, has, k)
         if world == 1:
-            if self.recycle_output and n > ops.TOPK_SMALL_N:
+            recycle = self.recycle_output == "always" and n > ops.TOPK_SMALL_N
+            if recycle:
                 out, prev_idx = self._recycler.take(name, g)
             else:
                 out, prev_idx = torch.empty_like(g), None
@@ -85,7 +89,7 @@ class TopKCompressor(Compressor):
                                                carry_valid=carry_valid, prev_idx=prev_idx)
             mem.residuals[name] = res
             mem.carry_written(name, res, carry)
-            if self.recycle_output and n > ops.TOPK_SMALL_N:
+            if recycle:
                 self._recycler.keep(name, out, idx)
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
         buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None, carry=carry,

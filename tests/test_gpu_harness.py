@@ -156,7 +156,7 @@ def _hash32(x):
 
 def _sample_positions(n):
     """The segment bracket's sample positions (csrc/topk.hip seg_sample_n + sample_pos)."""
-    S = min(max(n // 128, 1024), 8192)
+    S = min(max(n // 256, 512), 2048)
     S = min(S, n // 4)
     st = n // S
     pos = []

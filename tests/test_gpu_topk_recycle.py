@@ -23,7 +23,7 @@ def _comm(recycle):
     from grace_amd.dist.communicator.allgather import Allgather
     from grace_amd.dist.compressor.topk import TopKCompressor
     from grace_amd.dist.memory.residual import ResidualMemory
-    return Allgather(TopKCompressor(0.01, recycle_output=recycle), ResidualMemory(), 1)
+    return Allgather(TopKCompressor(0.01, recycle_output="always" if recycle else False), ResidualMemory(), 1)
 
 
 def _grads(n, steps, seed, ties_at=()):
@@ -130,3 +130,29 @@ def test_randomk_recycled_output_equals_dense():
     assert hits >= 4
     for t, exp in held:
         assert same_bits(_np(t), exp)
+
+
+def test_topk_nomem_recycled_output_equals_dense():
+    """The no-memory world-1 step (the default recycling path) against the dense-write step and the
+    oracle's compress + decompress over steps with dropped results, a held one and an exact-fallback
+    bucket (99.9 % zeros) in between."""
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.none import NoneMemory
+    n = (1 << 20) + 9
+    rec = Allgather(TopKCompressor(0.01), NoneMemory(), 1)
+    ref = Allgather(TopKCompressor(0.01, recycle_output=False), NoneMemory(), 1)
+    gs = _grads(n, 7, 33, ties_at=(4,))
+    held = None
+    for s, g in enumerate(gs):
+        gt = torch.from_numpy(g).to(DEV)
+        o1 = rec.step(gt, "b")
+        o2 = ref.step(gt, "b")
+        _, v_or, i_or, _, out_or = O.topk_residual_step(g, None, 0.01)
+        assert same_bits(_np(o1), _np(o2)), s
+        assert same_bits(_np(o1), out_or), s
+        if s == 2:
+            held = (o1, out_or)
+        del o1, o2
+    assert rec.compressor._recycler.hits >= 4
+    assert same_bits(_np(held[0]), held[1])

@@ -6,4 +6,4 @@ cd "$(dirname "$0")/.."
 python3 -c "import __graft_entry__ as g; g.build()"
 python3 -c "from grace_amd.build import build; build(variant='stamps')"
 GRACE_BUILD_DEFS=GRACE_TERN_FLUSH python3 -c "from grace_amd.build import build; build(variant='ternflush')"
-GRACE_BUILD_DEFS=GRACE_TERN_ENC_PLAIN python3 -c "from grace_amd.build import build; build(variant='ternplain')"
+GRACE_BUILD_DEFS=GRACE_TERN_ENC_NT python3 -c "from grace_amd.build import build; build(variant='ternnt')"

@@ -37,6 +37,16 @@ for step in range(4):
             rows.append((int(s), n, k, int(c[3]), int(c[4]), int(c[5]), int(c[9]), int(c[7]),
                          us(8, 9), us(9, 10), us(10, 11), us(11, 12), us(8, 12)))
         fb = [r for r in rows if r[3]]
+        # absolute stamps relative to the first large segment's finalize start (slot 8, block 0)
+        t0 = int(ws[offs[0] + 64:offs[0] + 256].view(np.uint64)[8])
+        rel = []
+        for li, s in enumerate(large):
+            st = ws[offs[li] + 64:offs[li] + 256].view(np.uint64)
+            rel.append((int(s), sizes[s], *[(int(st[q]) - t0) / 100.0 for q in (9, 10, 11, 12)]))
+        rel.sort(key=lambda r: -r[5])
+        print("  finalize stamps (us from the kernel start): seg n findB route last end; latest 6:")
+        for r in rel[:6]:
+            print("    seg %d n %d  %.1f %.1f %.1f %.1f" % r)
         print(f"step {step}: {len(rows)} large segments, fallbacks {len(fb)}")
         for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8]:
             print("  seg %d n %d k %d status %d n_sure %d n_cand %d need %d n_bnd %d | fin us: findB %.1f route %.1f "

@@ -30,9 +30,10 @@ for step in ${STEPS:-pytest smoke bench}; do
                 -- python3 bench.py --workload $wl --steps $st --warmup 5 --no-cpu-baseline
             done ;;
     exp) run exp 600 python3 ${EXP} ;;
+    exps) for e in ${EXPS}; do b=$(basename $e .py); run $b 300 python3 $e; grep -v amdgpu.ids gpurun_out/$b.log | tail -4; done ;;
     ternab) # TernGrad: does the encoder's re-read of x hit the Infinity Cache?  The same bench with a
             # 512 MiB write stream between the statistics pass and the encoder (ternflush build)
-            for lib in libgrace_hip libgrace_hip_ternflush libgrace_hip_ternplain; do
+            for lib in libgrace_hip libgrace_hip_ternflush libgrace_hip_ternnt; do
               GRACE_HIP_LIB=grace_amd/lib/$lib.so GRACE_BENCH_NO_PROBE=1 run prof_tern_$lib 300 rocprofv3 --kernel-trace \
                 --stats --output-format csv -d gpurun_out/prof_${TAG}_tern_$lib -o run \
                 -- python3 bench.py --workload terngrad --steps 50 --warmup 5 --no-cpu-baseline
