@@ -1131,6 +1131,9 @@ constexpr uint32_t kW1SpinMax = 1u << 22;     // bounded waits (never expected t
 #ifndef GRACE_W1_NT
 #define GRACE_W1_NT 1      // non-temporal loads of M (A/B, one process: compress 34.9 -> 33.7 us)
 #endif
+#ifndef GRACE_W1_XCD
+#define GRACE_W1_XCD 0     // A/B knob: the G column groups of a slab on one XCD
+#endif
 #ifndef GRACE_W1_QNT
 #define GRACE_W1_QNT 1     // non-temporal stores of the Qraw partials (A/B: compress 34.0 -> 32.9 us)
 #endif
@@ -1202,7 +1205,20 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cw = w & 3, rw = w >> 2;
-  const int G = gridDim.x, cg = blockIdx.x, SG = gridDim.y;
+  const int G = gridDim.x, SG = gridDim.y;
+  int cg = blockIdx.x, sy = blockIdx.y;
+#if GRACE_W1_XCD
+  {  // XCD-aware placement (A/B): workgroups are dealt to the 8 XCDs round-robin by linear id; the G
+     // column groups of one slab row get ids 8 apart, i.e. one XCD, so the slab's exchange waits on
+     // workgroups that share an L2 and a fabric port rather than on the slowest of G XCDs
+    const int NB = G * SG, L = blockIdx.y * G + blockIdx.x;
+    if (NB % (8 * G) == 0) {
+      const int x = L & 7, j = L >> 3;
+      cg = j % G;
+      sy = x * (NB / 8 / G) + j / G;
+    }
+  }
+#endif
   W1_STAMP(ws, 0);
   W1_SPAN(ws);
   const int64_t jc = (int64_t)cg * kW1Cols + 256 * cw + 4 * lane;
@@ -1214,7 +1230,7 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
   // rather than 4 S scattered 16-row runs)
   const int64_t L = 4 * (int64_t)S;
   bool qstaged = false;
-  for (int s = blockIdx.y; s < S; s += SG) {
+  for (int s = sy; s < S; s += SG) {
     const int64_t lrow = 4 * (int64_t)s + rw;
     f32x4v v[kW1Rows];
 #pragma unroll

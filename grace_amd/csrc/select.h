@@ -1,5 +1,5 @@
-// Shared selection building blocks of the top-k engines (topk.hip: single bucket and sharded;
-// segtopk.hip: per-tensor segments): block scans, descending histogram bin search, the unique
+// Shared selection building blocks of the top-k engines (topk.hip: single bucket and per-tensor
+// segments; shard.hip: the sharded global cut): block scans, descending histogram bin search, the unique
 // composite selection key and an exact single-workgroup radix select over composite keys.
 #pragma once
 
@@ -36,11 +36,17 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
   return r;
 }
 
-// Given a histogram hist[NBINS] (in LDS or global) find, scanning from the top, the bin d where
-// the running count reaches `rank` (1-based): sum_{b>d} < rank <= sum_{b>=d}, for NR ranks at
-// once (one block scan).  Returns d[q] and above[q] = sum_{b>d[q]}.  All BLOCK threads must call;
-// NBINS % BLOCK == 0; s_res needs 2*NR words.
-template <int BLOCK, int NBINS, int NR>
+// Padded LDS histogram layout: bin b at word b + b / 32.  find_bins_desc's thread t reads bins
+// 32 t .. 32 t + 31 of a 32768-bin histogram; unpadded, the 64 lanes of a wave hit the same two
+// banks (a 32-way conflict on every read: ~7 us of a segment bracket); padded, their stride is 33
+// words and every lane has a bank of its own.  NBINS + NBINS / 32 words.
+__device__ __forceinline__ int hist_pad(int b) { return b + (b >> 5); }
+
+// Given a histogram hist[NBINS] (in LDS or global; PAD: the hist_pad layout) find, scanning from
+// the top, the bin d where the running count reaches `rank` (1-based): sum_{b>d} < rank <=
+// sum_{b>=d}, for NR ranks at once (one block scan).  Returns d[q] and above[q] = sum_{b>d[q]}.
+// All BLOCK threads must call; NBINS % BLOCK == 0; s_res needs 2*NR words.
+template <int BLOCK, int NBINS, int NR, bool PAD = false>
 __device__ void find_bins_desc(const uint32_t* hist, const uint32_t (&rank)[NR], uint32_t* s_w,
                                uint32_t* s_res, int (&d)[NR], uint32_t (&above)[NR]) {
   constexpr int PER = NBINS / BLOCK;
@@ -50,7 +56,7 @@ __device__ void find_bins_desc(const uint32_t* hist, const uint32_t (&rank)[NR],
   // below was a chain of dependent global loads (the segmented find kernel's 22 us)
   uint32_t h[PER], s = 0;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) h[j] = hist[top - j];
+  for (int j = 0; j < PER; ++j) h[j] = hist[PAD ? hist_pad(top - j) : top - j];
 #pragma unroll
   for (int j = 0; j < PER; ++j) s += h[j];
   if (t < 2 * NR) s_res[t] = 0;

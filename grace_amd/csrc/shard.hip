@@ -15,8 +15,9 @@
 //   2. ONE all_gather_into_tensor of the fixed-size records (8 k bytes per rank);
 //   3. shard_hist (every rank, identically): a 32768-bin histogram of key >> 16 over the W * cap
 //      gathered entries; the last workgroup to arrive finds the bin B holding the k-th key;
-//   4. shard_apply: entries above B are selected, below B rejected; the bin-B entries go to a short
-//      boundary list that the last workgroup ranks exactly by the composite (key, global index).
+//   4. shard_apply: entries above B are selected, below B rejected; the bin-B entries go to a
+//      boundary list and a histogram of their next 11 key bits, and the last workgroup decides them
+//      by that sub-bin, ranking the few in the cut's sub-bin exactly by (key, global index).
 //      A selected entry is written to the dense output (0 + v); an own entry the global cut rejects
 //      gets its t back in the residual (r' = v: the engine had zeroed it), and pay_idx marks this
 //      rank's record entries with their global index (selected) or -1.
@@ -38,6 +39,10 @@ constexpr int kShBins = 32768;       // key >> 16: 1/128-octave bins
 constexpr int kShMaxWorld = 1024;
 constexpr int kShMaxGrid = 512;
 constexpr unsigned kShHistGrid = 32;
+constexpr int kShHistPer = 16;       // shard_hist: entries per thread per round (one round at W = 8)
+constexpr int kShSub = 2048;         // boundary sub-bins: key bits 15..5 of the bin-B entries
+constexpr int kShTakePer = 8;        // last arriver: boundary entries per thread per round
+constexpr int kShPairCap = 1024;     // sub-bin entries ranked pairwise
 
 struct ShCtl {
   int32_t b1;        // boundary bin; -1 = every valid entry is selected
@@ -62,6 +67,7 @@ struct ShArgs {
   int32_t* pay_idx;     // this rank's record entries: global index if selected, -1 otherwise
   ShCtl* ctl;
   uint32_t* hist;       // [kShBins], left zeroed
+  uint32_t* hist2;      // [kShSub] sub-bin histogram of the boundary entries, left zeroed
   uint32_t* bnd;        // boundary list of entry numbers [world * cap]
   int32_t* status;      // pinned host word (system-scope fetch_or), may be null
 };
@@ -81,20 +87,22 @@ __device__ __forceinline__ void split_entry(uint32_t e, uint32_t cap, uint32_t& 
 
 // 3. the histogram of key >> 16 over the gathered entries; the last arriver finds bin B
 __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
-  __shared__ uint32_t h[kShBins];
+  __shared__ uint32_t h[kShBins + kShBins / 32];   // hist_pad layout (select.h)
   __shared__ uint32_t s_w[kShBlock / kWave + 1];
   __shared__ uint32_t s_res[2];
   __shared__ uint32_t s_last;
   const int t = threadIdx.x;
-  for (int b = t; b < kShBins; b += kShBlock) h[b] = 0u;
+  for (int b = t; b < kShBins + kShBins / 32; b += kShBlock) h[b] = 0u;
   __syncthreads();
   const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
-  const uint32_t step = gridDim.x * kShBlock * kShPer;
-  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += step) {
-    int32_t li[kShPer];
-    float v[kShPer];
+  // kShHistPer entries per thread per round, every load issued before any is counted: at W = 8 the
+  // 32 workgroups finish in one round (4 entries per round took 4 serial load round trips)
+  const uint32_t step = gridDim.x * kShBlock * kShHistPer;
+  for (uint32_t e0 = blockIdx.x * kShBlock * kShHistPer + t; e0 < N; e0 += step) {
+    int32_t li[kShHistPer];
+    float v[kShHistPer];
 #pragma unroll
-    for (int u = 0; u < kShPer; ++u) {
+    for (int u = 0; u < kShHistPer; ++u) {
       const uint32_t e = e0 + u * kShBlock;
       uint32_t w, j;
       split_entry(e < N ? e : e0, cap, w, j);
@@ -102,12 +110,12 @@ __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
       v[u] = rec_vals(a, w)[j];
     }
 #pragma unroll
-    for (int u = 0; u < kShPer; ++u)
-      if (e0 + u * kShBlock < N && li[u] >= 0) atomicAdd(&h[abs_key(v[u]) >> 16], 1u);
+    for (int u = 0; u < kShHistPer; ++u)
+      if (e0 + u * kShBlock < N && li[u] >= 0) atomicAdd(&h[hist_pad(abs_key(v[u]) >> 16)], 1u);
   }
   __syncthreads();
   for (int b = t; b < kShBins; b += kShBlock) {
-    const uint32_t c = h[b];
+    const uint32_t c = h[hist_pad(b)];
     if (c) atomicAdd(&a.hist[b], c);
   }
   // arrival (DESIGN §4 memory-model table, row 1: device atomics, vmcnt(0), barrier, one ticket)
@@ -128,7 +136,11 @@ __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
   uint32_t tot = 0;
 #pragma unroll
   for (int u = 0; u < kV; ++u) {
-    reinterpret_cast<uint4*>(h)[t + u * kShBlock] = hv[u];
+    const int b0 = hist_pad(4 * (t + u * kShBlock));   // 4 bins never straddle a pad word
+    h[b0] = hv[u].x;
+    h[b0 + 1] = hv[u].y;
+    h[b0 + 2] = hv[u].z;
+    h[b0 + 3] = hv[u].w;
     tot += hv[u].x + hv[u].y + hv[u].z + hv[u].w;
     hg[t + u * kShBlock] = make_uint4(0u, 0u, 0u, 0u);
   }
@@ -141,7 +153,7 @@ __global__ __launch_bounds__(kShBlock) void shard_hist_kernel(ShArgs a) {
     const uint32_t rank[1] = {k};
     int d[1];
     uint32_t ab[1];
-    find_bins_desc<kShBlock, kShBins, 1>(h, rank, s_w, s_res, d, ab);
+    find_bins_desc<kShBlock, kShBins, 1, true>(h, rank, s_w, s_res, d, ab);
     b1 = d[0];
     above = ab[0];
   }
@@ -187,17 +199,30 @@ struct BndComp {   // composite key of boundary entry j (plain loads: read after
   }
 };
 
-// 4. apply the cut: above B selected, below rejected, bin B listed and ranked by the last arriver
+// boundary sub-bin of an entry of bin B: key bits 15..5 (composite bits 47..37)
+__device__ __forceinline__ int sub_bin(uint32_t key) { return (int)((key >> 5) & (kShSub - 1)); }
+
+// 4. apply the cut: above B selected, below rejected; the bin-B entries go to the boundary list and
+// into a 2048-bin histogram of their next 11 key bits (sub-bins).  The last workgroup to arrive finds
+// the sub-bin B2 holding the cut, decides every boundary entry above / below it in one pass, and
+// ranks the few B2 entries pairwise by the composite (key, global index).  One level of bins (key >>
+// 16, 1/128 octave) left thousands of entries in bin B at W = 8 -- the eight local top-k lists pile
+// up around the global cut, more so as the residual feedback accumulates -- and ranking them by a
+// single-workgroup radix select over indirect loads took 30-120 us.
 __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   __shared__ int64_t s_base[kShMaxWorld];
   __shared__ uint32_t hsel[2048];
+  __shared__ uint32_t s_h2[kShSub];
   __shared__ uint32_t s_bnd[kShBlock * kShPer];   // this round's boundary entries, staged
+  __shared__ uint64_t s_comp[kShPairCap];
+  __shared__ uint32_t s_ent[kShPairCap];
   __shared__ uint32_t s_cnt, s_gbase;
   __shared__ uint32_t s_w[kShBlock / kWave + 1];
   __shared__ uint32_t s_res[2];
   __shared__ uint32_t s_last;
   const int t = threadIdx.x;
   for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
+  for (int b = t; b < kShSub; b += kShBlock) s_h2[b] = 0u;
   const int32_t b1 = a.ctl->b1;         // written by shard_hist (kernel boundary)
   const uint32_t need = a.ctl->need;
   if (t == 0) s_cnt = 0u;
@@ -227,14 +252,16 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
         if (li[u] < 0) {
           if ((int32_t)w == a.rank) a.pay_idx[j] = -1;
         } else {
-          const int kb = (int)(abs_key(v[u]) >> 16);
+          const uint32_t key = abs_key(v[u]);
+          const int kb = (int)(key >> 16);
           inb = kb == b1;
-          if (!inb) shard_take(a, kb > b1, w, j, li[u], v[u], s_base[w]);
+          if (inb) atomicAdd(&s_h2[sub_bin(key)], 1u);
+          else shard_take(a, kb > b1, w, j, li[u], v[u], s_base[w]);
         }
       }
       // boundary entries staged in LDS (one LDS atomic per wave); the round's list leaves with ONE
       // global reservation per workgroup (a device atomic per wave on the one counter serialised
-      // thousands of round trips: the select took 157 us at W = 8)
+      // thousands of round trips)
       const uint64_t m = __ballot(inb);
       if (m) {
         uint32_t base0 = 0;
@@ -254,6 +281,10 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
     if (t == 0) s_cnt = 0u;
     __syncthreads();
   }
+  for (int b = t; b < kShSub; b += kShBlock) {   // the sub-bin counts (device atomics)
+    const uint32_t c = s_h2[b];
+    if (c) atomicAdd(&a.hist2[b], c);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) s_last = atomicAdd(&a.ctl->ticket2, 1u) == gridDim.x - 1 ? 1u : 0u;
@@ -261,26 +292,90 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // several workgroups per CU possible: keep the acquire
   const uint32_t nb = __hip_atomic_load(&a.ctl->nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // T: exactly `need` of the nb boundary entries have composite >= T (unique composites)
-  uint64_t T;
-  if (need == 0u) {
-    T = ~0ull;
-  } else if (need >= nb) {
-    T = 0ull;
-  } else {
-    const BndComp src{&a, s_base};
-    // every boundary entry shares key >> 16 = b1, i.e. composite bits 63..48: start at pass 1
-    const uint64_t p0 = ((uint64_t)(uint32_t)b1 << 48) & (0x7FFull << 53);
-    T = block_select_comp<kShBlock>(src, (int64_t)nb, need, hsel, s_w, s_res, 1, p0, 0x7FFull << 53);
+  // the sub-bin B2 holding the need-th boundary entry (descending), need2 = how many of B2 to take
+  for (int b = t; b < kShSub; b += kShBlock) {
+    s_h2[b] = a.hist2[b];
+    a.hist2[b] = 0u;
   }
-  for (uint32_t jj = t; jj < nb; jj += kShBlock) {
-    const uint32_t e = a.bnd[jj];
-    uint32_t w, j;
-    split_entry(e, cap, w, j);
-    const int32_t li = rec_idx(a, w)[j];
-    const float v = rec_vals(a, w)[j];
-    const int64_t gi = s_base[w] + li;
-    shard_take(a, comp_key(abs_key(v), (uint32_t)gi) >= T, w, j, li, v, s_base[w]);
+  __syncthreads();
+  int b2 = kShSub;        // need == 0: every boundary entry is rejected
+  uint32_t need2 = 0;
+  if (need >= nb) {
+    b2 = -1;              // every boundary entry is selected
+  } else if (need > 0) {
+    const uint32_t rank[1] = {need};
+    int d[1];
+    uint32_t ab[1];
+    find_bins_desc<kShBlock, kShSub, 1>(s_h2, rank, s_w, s_res, d, ab);
+    b2 = d[0];
+    need2 = need - ab[0];
+  }
+  if (t == 0) s_cnt = 0u;
+  __syncthreads();
+  // one pass over the boundary list: above / below B2 decided, B2 entries staged for ranking
+  // (kShTakePer entries per thread per round, the entry-number loads and then the record loads
+  // each issued together)
+  for (uint32_t j0 = t; j0 < nb; j0 += kShBlock * kShTakePer) {
+    uint32_t e[kShTakePer];
+#pragma unroll
+    for (int u = 0; u < kShTakePer; ++u) {
+      const uint32_t jj = j0 + u * kShBlock;
+      e[u] = a.bnd[jj < nb ? jj : j0];
+    }
+    int32_t li[kShTakePer];
+    float v[kShTakePer];
+#pragma unroll
+    for (int u = 0; u < kShTakePer; ++u) {
+      uint32_t w, j;
+      split_entry(e[u], cap, w, j);
+      li[u] = rec_idx(a, w)[j];
+      v[u] = rec_vals(a, w)[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kShTakePer; ++u) {
+      if (j0 + u * kShBlock >= nb) continue;
+      uint32_t w, j;
+      split_entry(e[u], cap, w, j);
+      const int sb = sub_bin(abs_key(v[u]));
+      if (sb != b2) {
+        shard_take(a, sb > b2, w, j, li[u], v[u], s_base[w]);
+      } else {
+        const uint32_t q = atomicAdd(&s_cnt, 1u);
+        if (q < (uint32_t)kShPairCap) {
+          s_ent[q] = e[u];
+          s_comp[q] = comp_key(abs_key(v[u]), (uint32_t)(s_base[w] + li[u]));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t n2 = s_cnt;
+  if (n2 <= (uint32_t)kShPairCap) {
+    // rank the B2 entries pairwise (unique composites): the need2 highest are selected
+    for (uint32_t q = t; q < n2; q += kShBlock) {
+      const uint64_t me = s_comp[q];
+      uint32_t rk = 0;
+      for (uint32_t o = 0; o < n2; ++o) rk += s_comp[o] > me;
+      uint32_t w, j;
+      split_entry(s_ent[q], cap, w, j);
+      shard_take(a, rk < need2, w, j, rec_idx(a, w)[j], rec_vals(a, w)[j], s_base[w]);
+    }
+  } else {
+    // massive ties (more than kShPairCap entries share key bits 31..5): exact radix select over
+    // the whole boundary list, then every boundary entry decided again by T (the decisions above
+    // stand: T agrees with them, so those writes repeat)
+    const BndComp src{&a, s_base};
+    const uint64_t p0 = ((uint64_t)(uint32_t)b1 << 48) & (0x7FFull << 53);
+    const uint64_t T = block_select_comp<kShBlock>(src, (int64_t)nb, need, hsel, s_w, s_res, 1, p0, 0x7FFull << 53);
+    for (uint32_t jj = t; jj < nb; jj += kShBlock) {
+      const uint32_t e = a.bnd[jj];
+      uint32_t w, j;
+      split_entry(e, cap, w, j);
+      const int32_t li = rec_idx(a, w)[j];
+      const float v = rec_vals(a, w)[j];
+      const int64_t gi = s_base[w] + li;
+      shard_take(a, comp_key(abs_key(v), (uint32_t)gi) >= T, w, j, li, v, s_base[w]);
+    }
   }
   if (t == 0) {
     a.ctl->nb = 0u;
@@ -289,7 +384,7 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
 }
 
 static size_t sh_ws_bytes(int64_t world, int64_t cap) {
-  return 256 + sizeof(uint32_t) * kShBins + ((sizeof(uint32_t) * world * cap + 255) & ~(size_t)255);
+  return 256 + sizeof(uint32_t) * (kShBins + kShSub) + ((sizeof(uint32_t) * world * cap + 255) & ~(size_t)255);
 }
 
 }  // namespace grace
@@ -326,7 +421,8 @@ grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t ra
   a.pay_idx = pay_idx;
   a.ctl = reinterpret_cast<ShCtl*>(p);
   a.hist = reinterpret_cast<uint32_t*>(p + 256);
-  a.bnd = reinterpret_cast<uint32_t*>(p + 256 + sizeof(uint32_t) * kShBins);
+  a.hist2 = reinterpret_cast<uint32_t*>(p + 256 + sizeof(uint32_t) * kShBins);
+  a.bnd = reinterpret_cast<uint32_t*>(p + 256 + sizeof(uint32_t) * (kShBins + kShSub));
   a.status = status_host;
   const int64_t N = (int64_t)world * cap;
   int64_t g = (N + kShBlock * kShPer - 1) / (kShBlock * kShPer);

@@ -328,6 +328,7 @@ constexpr double kSampleDeff = GRACE_SAMPLE_DEFF;
 #define GRACE_SAMPLE_SIGMA 6.0
 #endif
 constexpr double kSampleSigma = GRACE_SAMPLE_SIGMA;        // bracket half-width in binomial sigmas
+constexpr double kSurePoisson = 1e-6;                      // small-sample "sure" rank: miss probability
 constexpr int kSamplePer = GRACE_SAMPLE_PER;               // samples per thread: 1 is fastest --
                                                            // the strided samples are latency-bound
                                                            // random loads that want many waves
@@ -346,11 +347,29 @@ __device__ __forceinline__ BracketRanks bracket_ranks(int64_t S, int64_t k, int6
   const double sd = sqrt(kSampleDeff * mu * (1.0 - p) + 1.0);
   b.rank_hi = (int64_t)floor(mu - kSampleSigma * sd - 2.0);   // < 0: nothing is "sure"
   b.rank_lo = (int64_t)ceil(mu + kSampleSigma * sd + 2.0);    // >= S: everything a candidate
+  if (b.rank_hi < 0) {
+    // Few samples above the k-th (a segment's 512..2048 samples at 1 %: mu ~ 5..20): the normal
+    // margin leaves nothing sure, the candidate histogram then spans every key above lo and its
+    // 1/16-octave bins put thousands of candidates in the boundary bin.  "Sure" fails (n_sure > k)
+    // only when fewer than rank_hi + 1 samples fall among the k largest, an event of probability
+    // P(Poisson(mu) <= rank_hi): take the largest rank_hi with that below kSurePoisson.  A miss is
+    // still exact (the finalize's fallback), only slower.
+    double term = exp(-mu), cdf = term;
+    for (int64_t j = 0; j < 64 && cdf <= kSurePoisson; ++j) {
+      b.rank_hi = j;
+      term *= mu / (double)(j + 1);
+      cdf += term;
+    }
+  }
   const int64_t rank_mid = (int64_t)floor(mu);
   b.r1[0] = (uint32_t)((b.rank_hi < 0 ? 0 : (b.rank_hi >= S ? S - 1 : b.rank_hi)) + 1);
   b.r1[1] = (uint32_t)((b.rank_lo < 0 ? 0 : (b.rank_lo >= S ? S - 1 : b.rank_lo)) + 1);
   b.r1[2] = (uint32_t)((rank_mid < 0 ? 0 : (rank_mid >= S ? S - 1 : rank_mid)) + 1);
   return b;
+}
+// candidate histogram bin of key (lo <= key <= hi): keys above the binned range share the top bin
+__device__ __forceinline__ uint32_t cand_bin(uint32_t key, uint32_t lo, uint32_t sh) {
+  return min((key - lo) >> sh, (uint32_t)kHistBins - 1u);
 }
 // the bracket from the fine bins (key >> 16) holding the three ranks: sure = key > hi (rounded up
 // to the top of its bin: fewer sure), candidates from the bottom of the low bin (more candidates),
@@ -358,12 +377,17 @@ __device__ __forceinline__ BracketRanks bracket_ranks(int64_t S, int64_t k, int6
 __device__ __forceinline__ void bracket_publish(TopkCtl* ctl, const BracketRanks& b, int64_t S, uint32_t d_hi,
                                                 uint32_t d_lo, uint32_t d_mid) {
   uint32_t hi = (d_hi << 16) | 0xFFFFu;
+  // top of the binned key range: hi, or with nothing sure the top of the sample maximum's bin
+  // (r1[0] = 1 then); the keys above it share the top bin (binning clamps), so the 2048 bins
+  // resolve the band the k-th key lies in instead of every key up to +inf
+  uint32_t top = hi;
   uint32_t lo = d_lo << 16;
   if (b.rank_hi < 0) hi = 0x7FFFFFFFu;
   if (b.rank_lo >= S) lo = 0u;
   if (lo > hi) lo = hi;
+  if (top < lo) top = lo;
   uint32_t sh = 0;
-  const uint64_t span = (uint64_t)hi - (uint64_t)lo;   // keys lo..hi -> bins 0..span>>sh
+  const uint64_t span = (uint64_t)top - (uint64_t)lo;   // keys lo..top -> bins 0..span>>sh
   while ((span >> sh) >= (uint64_t)kHistBins) ++sh;
   uint32_t mid = (d_mid << 16) | 0x8000u;
   mid = mid < lo ? lo : (mid > hi ? hi : mid);
@@ -689,7 +713,7 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
             if (pc < (uint32_t)kStage) {
               sm.cand[pc] = e;
             } else {
-              atomicAdd(&sm.hist[(abs_key(tv) - lo) >> sh], 1u);
+              atomicAdd(&sm.hist[cand_bin(abs_key(tv), lo, sh)], 1u);
               if (gcn < (uint32_t)w.cap) w.cand[gcn] = e;
               ++gcn;
             }
@@ -762,7 +786,7 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
   for (uint32_t j = tid; j < nc; j += kMainBlock) {
     const uint32_t gp = sm.cnt[2] + j;
     const int2 e = sm.cand[j];
-    atomicAdd(&sm.hist[(abs_key(u2f((uint32_t)e.y)) - lo) >> sh], 1u);
+    atomicAdd(&sm.hist[cand_bin(abs_key(u2f((uint32_t)e.y)), lo, sh)], 1u);
     if (gp < (uint32_t)w.cap) w.cand[gp] = e;
   }
   __syncthreads();
@@ -1309,7 +1333,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
         for (int u = 0; u < kFinPer; ++u) {
           const uint32_t j = r0 + u * BLOCK + t;
           e[u] = ld_i2<AG>(w.cand + (j < b1 ? j : b0));   // clamped, unconditional
-          const int bin = j < b1 ? (int)((abs_key(u2f((uint32_t)e[u].y)) - thr_lo) >> shift) : -1;
+          const int bin = j < b1 ? (int)cand_bin(abs_key(u2f((uint32_t)e[u].y)), thr_lo, shift) : -1;
           fsel |= (uint32_t)(bin > B) << u;
           fb |= (uint32_t)(bin == B) << u;
           fbelow |= (uint32_t)(j < b1 && bin < B) << u;
@@ -1514,9 +1538,9 @@ __global__ void tag_divide_kernel(const int32_t* idx, int64_t stride, AggCum cum
 // residual (grace_dl/dist/memory/residual.py:10-20).  All tensors sit back to back in one flat
 // buffer (the segments) and the single-bucket engine above runs on every segment at once, in
 // THREE launches, streaming every element once (16 B per element at world 1):
-//   prep     one workgroup per segment: a small segment (n <= kSmallN) is selected exactly in LDS
+//   prep     one workgroup per segment: a small segment (n <= kSegSmallMax) is selected exactly in LDS
 //            and written out completely (small_body); a large one gets its sampled bracket
-//            (n/128 samples, 1024..8192, into a 32768-bin LDS histogram; the engine's ranks and
+//            (n/256 samples, 512..2048, into a 32768-bin LDS histogram; the engine's ranks and
 //            thresholds) and its counters / candidate histogram zeroed;
 //   main     one chunk of one large segment per workgroup: the engine's main pass (main_chunk_v2)
 //            with that segment's bracket, lists and histogram;
@@ -1530,6 +1554,12 @@ __global__ void tag_divide_kernel(const int32_t* idx, int64_t stride, AggCum cum
 #define GRACE_SEG_SAMPLE_MAX 2048
 #endif
 constexpr int kSegSampleMin = 512, kSegSampleMax = GRACE_SEG_SAMPLE_MAX;
+// segments up to this size are selected whole in one prep workgroup (the prep kernel supports up to
+// kSmallN); larger ones take the bracket / main / finalize path.  A 16 K or 32 K segment in one
+// workgroup (four serial rounds of loads, an LDS select over 32 K keys) ended the prep launch
+// ~6 us after the last large segment's bracket, delaying the main pass by that much.
+constexpr int kSegSmallMax = 8192;
+static_assert(kSegSmallMax <= kSmallN, "small segments fit the prep workgroup");
 
 struct SegPlan {
   const float* g;
@@ -1540,7 +1570,7 @@ struct SegPlan {
   float beta, gamma;
   const int64_t* seg_off;   // [nseg + 1] element offsets
   const int64_t* k_off;     // [nseg + 1] payload offsets (k_i prefix sums)
-  const int32_t* large;     // [nL] segments with n > kSmallN
+  const int32_t* large;     // [nL] segments with n > kSegSmallMax (any order: the host sorts by size)
   const int32_t* small;     // [nS] the others
   const int64_t* chk_off;   // [nL + 1] main-pass chunk offsets of the large segments
   const int32_t* chunk_li;  // [nchunks] large-segment slot of every main-pass chunk
@@ -1594,7 +1624,7 @@ __device__ __forceinline__ int64_t seg_sample_n(int64_t n) {
   return S < n / 4 ? S : n / 4;
 }
 
-// A small segment (n <= kSmallN) in one workgroup, built for throughput next to many others in the
+// A small segment (n <= kSegSmallMax) in one workgroup, built for throughput next to many others in the
 // same launch: t staged in LDS with 8 loads per array in flight per thread, the exact threshold by
 // block_select_comp over LDS, then every element written from LDS with independent coalesced
 // stores and the payload placed by one LDS atomic per wave (order within the segment is free: the
@@ -1649,15 +1679,25 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
   __shared__ uint32_t lds[kSmallN + 2048];
   __shared__ uint32_t s_w[kSelBlock / kWave + 1];
   __shared__ uint32_t s_res[8];
-  static_assert(kBracketBins <= kSmallN + 2048, "bracket histogram fits the shared block");
+  static_assert(kBracketBins + kBracketBins / 32 <= kSmallN + 2048, "padded bracket histogram fits the shared block");
   const int b = blockIdx.x, tid = threadIdx.x;
   if (b >= p.nL) {   // a small segment, selected and written completely by this workgroup
+#ifdef GRACE_SEG_NOSMALL   // diagnostic timing build only (small segments left unwritten)
+    return;
+#endif
     const StepArgs a = seg_step_args(p, p.small[b - p.nL]);
     seg_small_body<HAS_RES, MODE>(a, reinterpret_cast<float*>(lds), lds + kSmallN, s_w, s_res);
     return;
   }
   const StepArgs a = seg_step_args(p, p.large[b]);
   const TopkWs w = seg_ws(p, b, a.n, a.k);
+  STAMP_IF(true, w.ctl, 13);
+#ifdef GRACE_STAMPS
+  if (tid == 0) {   // main-pass span of this segment: first chunk start (min), last chunk end (max)
+    reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[16] = ~0ull;
+    reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[17] = 0ull;
+  }
+#endif
   const int64_t S = seg_sample_n(a.n);
   const uint32_t st = (uint32_t)(a.n / S);
   constexpr int kPer = kSegSampleMax / kSelBlock;
@@ -1670,17 +1710,19 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
   // this step's counters and candidate histogram (the segment's previous finalize has completed)
   if (tid >= 3 && tid < 12) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
   for (int j = tid; j < kHistBins; j += kSelBlock) w.hist[j] = 0u;
-  for (int j = tid; j < kBracketBins; j += kSelBlock) lds[j] = 0u;
+  for (int j = tid; j < kBracketBins + kBracketBins / 32; j += kSelBlock) lds[j] = 0u;   // padded layout
   __syncthreads();
+  STAMP_IF(true, w.ctl, 14);
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
-    if ((int64_t)q * kSelBlock + tid < S) atomicAdd(&lds[abs_key(t[q]) >> 16], 1u);
+    if ((int64_t)q * kSelBlock + tid < S) atomicAdd(&lds[hist_pad(abs_key(t[q]) >> 16)], 1u);
   __syncthreads();
   const BracketRanks br = bracket_ranks(S, a.k, a.n);
   int d[3];
   uint32_t above[3];
-  find_bins_desc<kSelBlock, kBracketBins, 3>(lds, br.r1, s_w, s_res, d, above);
+  find_bins_desc<kSelBlock, kBracketBins, 3, true>(lds, br.r1, s_w, s_res, d, above);
   if (tid == 0) bracket_publish(w.ctl, br, S, (uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2]);
+  STAMP_IF(true, w.ctl, 15);
 }
 
 template <bool HAS_RES, int MODE, bool VEC>
@@ -1692,6 +1734,11 @@ __global__ __launch_bounds__(kMainBlock, 4) void seg_main_kernel(SegPlan p) {
   const StepArgs a = seg_step_args(p, s);
   const TopkWs w = seg_ws(p, li, a.n, a.k);
   const int64_t chunk = (int64_t)blockIdx.x - p.chk_off[li];
+#ifdef GRACE_STAMPS
+  if (tid == 0)
+    atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.ctl) + 64) + 16,
+              (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
@@ -1706,6 +1753,11 @@ __global__ __launch_bounds__(kMainBlock, 4) void seg_main_kernel(SegPlan p) {
     const uint32_t h = sm.hist[b];
     if (h) atomicAdd(&w.hist[b * kHistStride], h);
   }
+#ifdef GRACE_STAMPS
+  if (tid == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w.ctl) + 64) + 17,
+              (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // the engine's finalize per large segment, with the segment's fin_off[li + 1] - fin_off[li]
@@ -1720,6 +1772,7 @@ __global__ __launch_bounds__(kSelBlock) void seg_fin_kernel(SegPlan p) {
   const int fcnt = (int)(p.fin_off[li + 1] - p.fin_off[li]);
   const StepArgs a = seg_step_args(p, p.large[li]);
   const TopkWs w = seg_ws(p, li, a.n, a.k);
+  STAMP_IF(fi == 0, w.ctl, 8);
   finalize_run<MODE, kSelBlock, false>(a, w, fi, fcnt, fs, false);
 }
 
@@ -1999,7 +2052,7 @@ grace_status_t grace_sparse_aggregate(const float* vals, const int32_t* idx, int
 
 
 
-int32_t grace_topk_segmented_small_max(void) { return kSmallN; }
+int32_t grace_topk_segmented_small_max(void) { return kSegSmallMax; }
 
 int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out) {
   if (has_residual) return dense_out ? kChunkOf<true, kDenseFused> : kChunkOf<true, kDenseRes>;

@@ -30,6 +30,10 @@ class SegmentedTopK:
         self.residuals = {}
         self._tables = {}
         self.last_payload = None
+        # A/B knobs (tools/ab_seg.py): the small-segment limit (<= the library's kSmallN) and the
+        # order of the large segments' chunks ("size": descending size, "index": tensor order)
+        self._small_max = None
+        self._order = "size"
 
     def tables(self, sizes, device, has_res, dense_out):
         """Device tables of one segment list (cached): offsets, the small / large split, the main
@@ -42,20 +46,27 @@ class SegmentedTopK:
         hit = self._tables.get(key)
         if hit is not None:
             return hit
-        small_max = int(_lib.query("grace_topk_segmented_small_max"))
+        small_max = int(self._small_max or _lib.query("grace_topk_segmented_small_max"))
         chunk = int(_lib.query("grace_topk_segmented_chunk", 1 if has_res else 0, 1 if dense_out else 0))
         seg, kk = [0], [0]
         large, small, chk, chunk_li, ws_off, fin, fin_li = [], [], [0], [], [], [0], []
         ws_total = 0
+        ks = []
         for i, n in enumerate(sizes):
             if n < 1:
                 raise ValueError("empty tensor in the segment table")
             k = min(n, ops.ratio_k(n, self.compress_ratio))        # torch.topk needs k <= n
+            ks.append(k)
             seg.append(seg[-1] + n)
             kk.append(kk[-1] + k)
             if n <= small_max:
                 small.append(i)
-                continue
+        # large segments in descending size: their main-pass chunks are dispatched in slot order,
+        # so the chunks still running at the end of the pass (when the grid has drained and the
+        # few left stream alone) are the small segments' short ones
+        order = (lambda i: (-sizes[i], i)) if self._order == "size" else (lambda i: i)
+        for i in sorted((i for i, n in enumerate(sizes) if n > small_max), key=order):
+            n, k = sizes[i], ks[i]
             li = len(large)
             large.append(i)
             c = (n + chunk - 1) // chunk

@@ -176,7 +176,7 @@ def test_segmented_edge_segments(world):
     payload (global indices) and residual; the exchange itself is covered in test_gpu_w8.py."""
     from grace_amd.dist.segmented import SegmentedTopK
     ratio = 0.01
-    sizes = [3, 40000, 5, 50001, 65536, 7, 60000, 33000, 1]
+    sizes = [3, 40000, 5, 50001, 65536, 7, 60000, 33000, 1, 8193, 20000, 8192]
     rng = np.random.default_rng(31)
     eng = SegmentedTopK(ratio, world_size=world)
     res = [None] * len(sizes)

@@ -47,6 +47,15 @@ for step in range(4):
         print("  finalize stamps (us from the kernel start): seg n findB route last end; latest 6:")
         for r in rel[:6]:
             print("    seg %d n %d  %.1f %.1f %.1f %.1f" % r)
+        # whole-step phases of the large segments, us from the earliest prep start (slot 13):
+        # prep start / samples in / prep end (13, 14, 15), main span (16, 17), finalize start / end (8, 12)
+        sts = [ws[offs[li] + 64:offs[li] + 256].view(np.uint64) for li in range(len(large))]
+        p0 = min(int(x[13]) for x in sts)
+        ph = lambda q: [(int(x[q]) - p0) / 100.0 for x in sts]   # noqa: E731
+        for nm, q in (("prep_start", 13), ("prep_samples", 14), ("prep_end", 15), ("main_first", 16),
+                      ("main_last", 17), ("fin_start", 8), ("fin_end", 12)):
+            v = ph(q)
+            print("  %-13s min %7.1f  median %7.1f  max %7.1f" % (nm, min(v), float(np.median(v)), max(v)))
         print(f"step {step}: {len(rows)} large segments, fallbacks {len(fb)}")
         for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8]:
             print("  seg %d n %d k %d status %d n_sure %d n_cand %d need %d n_bnd %d | fin us: findB %.1f route %.1f "
