@@ -31,9 +31,10 @@ class SegmentedTopK:
         self._tables = {}
         self.last_payload = None
         # A/B knobs (tools/ab_seg.py): the small-segment limit (<= the library's kSmallN) and the
-        # order of the large segments' chunks ("size": descending size, "index": tensor order)
+        # order of the large segments' chunks ("index": tensor order; "size": descending size, which
+        # measured 0.4-4 us slower per step on the ResNet-50 set)
         self._small_max = None
-        self._order = "size"
+        self._order = "index"
 
     def tables(self, sizes, device, has_res, dense_out):
         """Device tables of one segment list (cached): offsets, the small / large split, the main
@@ -61,9 +62,6 @@ class SegmentedTopK:
             kk.append(kk[-1] + k)
             if n <= small_max:
                 small.append(i)
-        # large segments in descending size: their main-pass chunks are dispatched in slot order,
-        # so the chunks still running at the end of the pass (when the grid has drained and the
-        # few left stream alone) are the small segments' short ones
         order = (lambda i: (-sizes[i], i)) if self._order == "size" else (lambda i: i)
         for i in sorted((i for i, n in enumerate(sizes) if n > small_max), key=order):
             n, k = sizes[i], ks[i]

@@ -57,6 +57,7 @@ def _bits(a, b):
     (2, [(1 << 20) + 5, 777777], "normal", 0.001),
     (3, [300001, 300001, 300001], "normal", 0.01),
     (2, [400000, 400000], "ties", 0.5),
+    (2, [1 << 22, (1 << 22) - 3], "normal", 0.3),   # W * cap > 4 Mi entries: the three-launch select
 ])
 def test_sharded_topk_native_matches_single_gpu(world, sizes, case, ratio):
     from grace_amd import ops

@@ -74,6 +74,13 @@ for step in range(6):
         exp[ii] = np.float32(0.0) + gn[ii]
         assert np.array_equal(o0.view(np.uint32), exp.view(np.uint32)), "dense output differs"
     del outs
+    if "stamps" in os.environ.get("GRACE_HIP_LIB", ""):   # the last rank's select, phase by phase
+        ws = ops.workspace("shardsel", ops._lib.query("grace_shard_select_workspace_bytes", W, cap), dev)
+        sv = ws[64:256].cpu().numpy().view(np.uint64)
+        us = lambda a, b: round((int(sv[b]) - int(sv[a])) / 100.0, 1)   # noqa: E731
+        print(f"step {step} one-launch select stamps, us (workgroup 0, then the last arriver): load + coarse hist "
+              f"{us(0, 1)}, barrier {us(1, 2)}, coarse cut + sub-bins {us(2, 3)}, barrier {us(3, 4)}, sub cut + list "
+              f"{us(4, 5)}, to last {us(5, 6)}, last {us(6, 7)}; total {us(0, 7)}")
 med = [statistics.median(r[i] for r in rows[2:]) for i in range(3)]
 print(f"W={W} n={n} k={k} per-rank device time, us (median of steps 2..5): local top-k {med[0]:.1f}, "
       f"dense zero-fill {med[1]:.1f}, select {med[2]:.1f}; serial sum {sum(med):.1f} "
