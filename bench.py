@@ -631,10 +631,20 @@ def bench_topk_sharded(args, world, rank, dev):
     line["config"] = {"workload": f"ShardedTopK(0.1 %) + residual, one {4 * n >> 20} MiB bucket over {world} "
                                   "rank(s), replicated dense decode (BASELINE configs[4])",
                       "numel": n, "k": k, "shard": m, "parallelism": f"{world} contiguous shards"}
-    per_gpu = 12.0 * m + 8.0 * k + 4.0 * n      # shard encode + replicated decode
+    survey = 12.0 * m + 8.0 * k + 4.0 * n       # shard encode + replicated decode
+    recycled = eng._recycler.hits > 0
+    if recycled:
+        # the dropped output comes back (ShardedTopK.recycle_output): instead of a 4n zero-fill, the
+        # select reads the W records (8 B per entry), writes every entry's selection record (4 B) and
+        # the next step's clear reads it (4 B); k new values in, k old ones out (4 B each)
+        per_gpu = 12.0 * m + 8.0 * k + 16.0 * world * k + 8.0 * k
+    else:
+        per_gpu = survey
     line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes_per_gpu": per_gpu}
+                        "algorithmic_bytes_per_gpu": per_gpu, "survey_bytes_per_gpu": survey,
+                        "output": "recycled" if recycled else "dense zero-fill",
+                        "recycled_steps": eng._recycler.hits}
     return line
 
 

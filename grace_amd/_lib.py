@@ -62,7 +62,8 @@ SIGNATURES = {
                                        SZ, P]),
     "grace_shard_record_words": (SZ, [I64]),
     "grace_shard_select_workspace_bytes": (SZ, [I32, I64]),
-    "grace_shard_select": (ST, [P, I32, I32, I64, P, I64, P, P, I64, I64, P, P, SZ, P, P]),
+    "grace_shard_select": (ST, [P, I32, I32, I64, P, I64, P, P, I64, I64, P, P, P, SZ, P, P]),
+    "grace_shard_clear": (ST, [P, I64, I64, P, I64, P]),
     "grace_dgc_workspace_bytes": (SZ, [I64]),
     "grace_dgc_sample": (ST, [P, I64, P, U64, I64, P, P]),
     "grace_dgc_threshold": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),

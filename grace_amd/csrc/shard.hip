@@ -81,6 +81,8 @@ struct ShArgs {
   float* out;           // dense output, zero-filled, global range [out_base, out_base + out_len)
   int64_t out_base, out_len;
   int32_t* pay_idx;     // this rank's record entries: global index if selected, -1 otherwise
+  int32_t* sel_gi;      // optional [world * cap]: every entry's global index if selected, else -1
+                        // (the positions the next step clears in a recycled output)
   ShCtl* ctl;
   uint32_t* hist;       // [kShBins], left zeroed
   uint32_t* hist2;      // [kShSub] sub-bin histogram of the boundary entries, left zeroed
@@ -205,6 +207,12 @@ __device__ __forceinline__ void shard_take(const ShArgs& a, bool sel, uint32_t w
     a.pay_idx[j] = sel ? (int32_t)gi : -1;
     if (!sel) a.r[li] = v;   // the local engine zeroed it (r' = t - t); the global cut rejects it: r' = t
   }
+  if (a.sel_gi) a.sel_gi[(int64_t)w * a.cap + j] = sel ? (int32_t)gi : -1;
+}
+// a padding entry (idx -1: a shard shorter than cap)
+__device__ __forceinline__ void shard_pad(const ShArgs& a, uint32_t w, uint32_t j) {
+  shard_pad(a, w, j);
+  if (a.sel_gi) a.sel_gi[(int64_t)w * a.cap + j] = -1;
 }
 
 struct BndComp {   // composite key of boundary entry j (plain loads: read after the last arriver's acquire)
@@ -263,7 +271,7 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
         uint32_t w, j;
         split_entry(e, cap, w, j);
         if (li[u] < 0) {
-          if ((int32_t)w == a.rank) a.pay_idx[j] = -1;
+          shard_pad(a, w, j);
         } else {
           const uint32_t key = abs_key(v[u]);
           const int kb = (int)(key >> 16);
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(kShBlock) void shard_fused_kernel(ShArgs a) {
       } else {
         uint32_t w, j;
         split_entry(e, cap, w, j);
-        if ((int32_t)w == a.rank) a.pay_idx[j] = -1;
+        shard_pad(a, w, j);
       }
     }
   }
@@ -724,6 +732,26 @@ static bool sh_fused_fits(int64_t grid) {
   return grid >= 1 && grid <= cached[dev];
 }
 
+// recycled output: zero the previous step's selected positions (its sel_gi list), 8 index loads in
+// flight per thread
+__global__ __launch_bounds__(256) void shard_clear_kernel(float* __restrict__ out, int64_t out_base, int64_t out_len,
+                                                         const int32_t* __restrict__ sel_gi, int64_t count) {
+  constexpr int kU = 8;
+  for (int64_t j0 = (int64_t)blockIdx.x * 256 * kU + threadIdx.x; j0 < count; j0 += (int64_t)gridDim.x * 256 * kU) {
+    int32_t gi[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t j = j0 + (int64_t)u * 256;
+      gi[u] = sel_gi[j < count ? j : j0];   // clamped, unconditional
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t o = (int64_t)gi[u] - out_base;
+      if (j0 + (int64_t)u * 256 < count && gi[u] >= 0 && o >= 0 && o < out_len) out[o] = 0.f;
+    }
+  }
+}
+
 static size_t sh_ws_bytes(int64_t world, int64_t cap) {
   return 256 + sizeof(uint32_t) * (kShBins + kShSub) + 2 * ((sizeof(uint32_t) * world * cap + 255) & ~(size_t)255);
 }
@@ -738,9 +766,21 @@ size_t grace_shard_record_words(int64_t cap) { return (size_t)(kShHdr + 2 * cap)
 
 size_t grace_shard_select_workspace_bytes(int32_t world, int64_t cap) { return sh_ws_bytes(world, cap); }
 
+grace_status_t grace_shard_clear(float* out, int64_t out_base, int64_t out_len, const int32_t* sel_gi, int64_t count,
+                                 void* stream) {
+  GRACE_REQUIRE(out && sel_gi && out_base >= 0 && out_len >= 0 && count >= 0, "grace_shard_clear: bad arguments");
+  if (count == 0) return GRACE_OK;
+  int64_t g = (count + 256 * 8 - 1) / (256 * 8);
+  g = g > 1024 ? 1024 : g;
+  shard_clear_kernel<<<(unsigned)g, 256, 0, as_stream(stream)>>>(out, out_base, out_len, sel_gi, count);
+  GRACE_CHECK_LAUNCH("grace_shard_clear");
+  return GRACE_OK;
+}
+
 grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t rank, int64_t cap, const int64_t* tab,
                                   int64_t k, float* residual, float* out, int64_t out_base, int64_t out_len,
-                                  int32_t* pay_idx, void* ws, size_t ws_bytes, int32_t* status_host, void* stream) {
+                                  int32_t* pay_idx, int32_t* sel_gi, void* ws, size_t ws_bytes, int32_t* status_host,
+                                  void* stream) {
   GRACE_REQUIRE(recs && tab && residual && out && pay_idx && ws && world >= 1 && world <= kShMaxWorld &&
                     rank >= 0 && rank < world && cap >= 1 && k >= 1 && out_base >= 0 && out_len >= 0 &&
                     (int64_t)world * cap < ((int64_t)1 << 31),
@@ -760,6 +800,7 @@ grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t ra
   a.out_base = out_base;
   a.out_len = out_len;
   a.pay_idx = pay_idx;
+  a.sel_gi = sel_gi;
   a.ctl = reinterpret_cast<ShCtl*>(p);
   a.hist = reinterpret_cast<uint32_t*>(p + 256);
   a.hist2 = reinterpret_cast<uint32_t*>(p + 256 + sizeof(uint32_t) * kShBins);

@@ -771,6 +771,8 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
   const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
   const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
   if (tid == 0) {
+    // one reservation per chunk and list (5461 per step on each counter: as 8 copies, a timing-only
+    // build, the main pass was 2 us faster in 196 -- within the spread, so the one counter stays)
     sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
     sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
   }
@@ -797,11 +799,16 @@ template <bool HAS_RES, int MODE, bool VEC, bool SKEL = false, bool SPARSE = fal
 __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w) {   // <= 128 VGPRs: 4 WGs/CU
   __shared__ MainShared sm;
   const int tid = threadIdx.x;
-  for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
-  if (tid < 4) sm.cnt[tid] = 0;
+  // SKEL (the in-bench streaming ceiling): only the loads and stores -- no histogram zeroing, list
+  // flushes or barriers, so the ceiling is a strictly lighter kernel than the one it bounds (with
+  // the flushes left in, the real pass beat its fastest launch by 0.5 % on one box)
+  if constexpr (!SKEL) {
+    for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
+    if (tid < 4) sm.cnt[tid] = 0;
+  }
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   const int64_t nchunks = (a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>;
-  __syncthreads();
+  if constexpr (!SKEL) __syncthreads();
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -809,8 +816,9 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
       main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
     else
       main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
-    flush_staged(a, w, sm, lo, sh);
+    if constexpr (!SKEL) flush_staged(a, w, sm, lo, sh);
   }
+  if constexpr (SKEL) return;
   __syncthreads();
   for (int b = tid; b < kHistBins; b += kMainBlock) {
     const uint32_t h = sm.hist[b];

@@ -55,6 +55,7 @@ class NativeShardKernels:
         ops.topk_residual_step(g, res, has_res, 1.0, 1.0, k_loc, out=None, payload=(None, vals, idx))
 
     select = staticmethod(ops.shard_select)
+    clear = staticmethod(ops.shard_clear)
 
     def status(self, device):
         return ops.shard_status(device)
@@ -83,6 +84,14 @@ class _Plan:
         self.pay_idx = torch.full((self.cap,), -1, dtype=torch.int32, device=device)
         self.rec = None
         self.rec_m = None
+        self._sel = None                        # two alternating sel_gi lists (recycled outputs)
+
+    def sel_buffer(self, prev, device):
+        """The sel_gi list this step's select writes: never the one `prev` (the recycled output's
+        list, read by this step's clear) points at."""
+        if self._sel is None:
+            self._sel = [torch.empty(self.world * self.cap, dtype=torch.int32, device=device) for _ in range(2)]
+        return self._sel[1] if prev is self._sel[0] else self._sel[0]
 
     def record(self, m, device, hdr):
         """This rank's send buffer: header word 0 = m, idx -1 padding past k_loc (written once per m)."""
@@ -98,13 +107,20 @@ class _Plan:
 class ShardedTopK:
     """Top-k (ratio) + residual memory over one bucket sharded across the ranks of `group`."""
 
-    def __init__(self, compress_ratio, group=None, dense="replicated", kernels=None, check_sizes=False):
+    def __init__(self, compress_ratio, group=None, dense="replicated", kernels=None, check_sizes=False,
+                 recycle_output=True):
         if dense not in ("replicated", "shard"):
             raise ValueError("dense must be 'replicated' or 'shard'")
         self.compress_ratio = compress_ratio
         self.group = group
         self.dense = dense
         self.check_sizes = check_sizes
+        # A step's dense output is zero except at the W * cap selected positions.  When the caller
+        # dropped the previous result of the same name unmodified (ops.OutputRecycler's rules), the
+        # next step takes it back and zeroes only those positions (grace_shard_clear) instead of
+        # zero-filling all of it: at configs[4] a 256 MiB write per rank and step.
+        self.recycle_output = recycle_output
+        self._recycler = ops.OutputRecycler()
         self.k_ops = kernels or NativeShardKernels()
         self.residuals = {}
         self._plans = {}
@@ -160,17 +176,29 @@ class ShardedTopK:
             torch.cuda.synchronize(device)
         self._check_status(device)
 
+    def _side_stream(self, device):
+        cur = torch.cuda.current_stream(device)
+        side = self._side.get(cur.cuda_stream)
+        if side is None:
+            side = self._side[cur.cuda_stream] = torch.cuda.Stream(device=device)
+        side.wait_stream(cur)
+        return cur, side
+
+    def _clear_out(self, out, out_base, prev_sel, device):
+        """A recycled output: its previous step's selected positions zeroed, on the side stream."""
+        cur, side = self._side_stream(device)
+        with torch.cuda.stream(side):
+            self.k_ops.clear(out, out_base, prev_sel)
+        out.record_stream(side)
+        return out, side
+
     def _zero_out(self, out_len, device):
         """The dense output, zero-filled on a side stream so the fill overlaps the local step and
         the exchange; the current stream waits for it only before the select."""
         K = self.k_ops
         if device.type != "cuda":
             return K.fill_zero(torch.empty(out_len, dtype=torch.float32, device=device)), None
-        cur = torch.cuda.current_stream(device)
-        side = self._side.get(cur.cuda_stream)
-        if side is None:
-            side = self._side[cur.cuda_stream] = torch.cuda.Stream(device=device)
-        side.wait_stream(cur)
+        cur, side = self._side_stream(device)
         with torch.cuda.stream(side):
             out = torch.empty(out_len, dtype=torch.float32, device=device)
             K.fill_zero(out)
@@ -192,7 +220,16 @@ class ShardedTopK:
             self.residuals[name] = res
         out_len = m if self.dense == "shard" else plan.n
         out_base = plan.base if self.dense == "shard" else 0
-        out, side = self._zero_out(out_len, dev)
+        recycle = self.recycle_output and dev.type == "cuda"
+        prev_sel = None
+        if recycle:
+            out, prev_sel = self._recycler.take(name, (out_len, dev), alloc=False)
+        if prev_sel is not None and prev_sel.numel() == plan.world * plan.cap:
+            out, side = self._clear_out(out, out_base, prev_sel, dev)
+        else:
+            prev_sel = None
+            out, side = self._zero_out(out_len, dev)
+        sel = plan.sel_buffer(prev_sel, dev) if recycle else None
         rec = plan.record(m, dev, K.HDR)
         cap = plan.cap
         vals = rec[K.HDR:K.HDR + cap].view(torch.float32)
@@ -205,6 +242,10 @@ class ShardedTopK:
             recs = rec
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)
-        K.select(recs, world, rank, cap, plan.tab, plan.k, res, out, out_base, plan.pay_idx, status)
+        if sel is None:
+            K.select(recs, world, rank, cap, plan.tab, plan.k, res, out, out_base, plan.pay_idx, status)
+        else:
+            K.select(recs, world, rank, cap, plan.tab, plan.k, res, out, out_base, plan.pay_idx, status, sel)
+            self._recycler.keep(name, out, sel)
         self.last_payload = (vals, plan.pay_idx)
         return out

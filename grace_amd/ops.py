@@ -123,18 +123,25 @@ class OutputRecycler:
         self.hits = 0      # steps that got their previous result back (sparse write)
         self.misses = 0    # steps that allocated (first step, result held / edited, other stream)
 
-    def take(self, name, like):
-        """(out tensor, prev_idx or None) for the next step of `name` shaped like `like`."""
+    def take(self, name, like, alloc=True):
+        """(out tensor, prev_idx or None) for the next step of `name` shaped like `like` (a tensor, or
+        a (numel, device) pair for an f32 vector).  A miss allocates (torch.empty_like) unless
+        alloc=False, which returns (None, None) and leaves the allocation to the caller."""
+        numel, device = (like.numel(), like.device) if isinstance(like, torch.Tensor) else (int(like[0]), like[1])
         hit = self._hit.pop(name, None)
         if hit is not None:
             buf, cdata, storage, version, prev_idx, key = hit
             # references to buf: the popped tuple, the local name, getrefcount's argument
-            if (key == (like.numel(), like.device, _stream()) and _getrefcount(buf) == 3
+            if (key == (numel, torch.device(device), _stream()) and _getrefcount(buf) == 3
                     and _storage_uses(cdata) == 2 and buf._version == version):
                 self.hits += 1
                 return buf, prev_idx
         self.misses += 1
-        return torch.empty_like(like), None
+        if not alloc:
+            return None, None
+        if isinstance(like, torch.Tensor):
+            return torch.empty_like(like), None
+        return torch.empty(numel, dtype=F32, device=device), None
 
     def keep(self, name, out, idx):
         """Remember this step's result and its payload indices (int32, length k)."""
@@ -924,15 +931,25 @@ def shard_record_words(cap):
 SHARD_HDR = 8   # shard.hip kShHdr: header words (word 0 = the shard length)
 
 
-def shard_select(recs, world, rank, cap, tab, k, residual, out, out_base, pay_idx, status):
+def shard_select(recs, world, rank, cap, tab, k, residual, out, out_base, pay_idx, status, sel_gi=None):
     """grace_shard_select over the W gathered records: the exact global top-k (dense output into the
     zero-filled `out`, which covers global [out_base, out_base + out.numel())), this rank's residual
     restored where the global cut rejects a local pick, pay_idx = global index or -1 per own entry.
-    `status`: pinned int32 word (bit 1: a record's shard length differs from the agreed `tab`)."""
+    `status`: pinned int32 word (bit 1: a record's shard length differs from the agreed `tab`).
+    sel_gi: optional int32[world * cap] <- every entry's global index if selected, else -1."""
     dev = recs.device
+    if sel_gi is not None and (sel_gi.dtype != torch.int32 or sel_gi.numel() < int(world) * int(cap)):
+        raise ValueError("shard_select: sel_gi must be int32 with world * cap elements")
     ws = workspace("shardsel", _lib.query("grace_shard_select_workspace_bytes", int(world), int(cap)), dev)
     _lib.call("grace_shard_select", _p(recs), int(world), int(rank), int(cap), _p(tab), int(k), _p(residual),
-              _p(out), int(out_base), out.numel(), _p(pay_idx), _p(ws), ws.numel(), status.data_ptr(), _stream())
+              _p(out), int(out_base), out.numel(), _p(pay_idx), _opt(sel_gi), _p(ws), ws.numel(), status.data_ptr(),
+              _stream())
+
+
+def shard_clear(out, out_base, sel_gi):
+    """Zero the positions a previous shard_select wrote (its sel_gi) in a recycled output."""
+    _lib.call("grace_shard_clear", _p(out), int(out_base), out.numel(), _p(sel_gi), sel_gi.numel(), _stream())
+    return out
 
 
 _sh_st = {}

@@ -438,12 +438,19 @@ grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* strea
  * (residual[idx] = v) where the local engine picked an entry the global cut rejects.
  * tab: device int64 [m_0 .. m_{W-1}, base_0 .. base_{W-1}] (the agreed partition).  status_host
  * (pinned, may be NULL): bit 1 = a record's shard length differs from tab, bit 2 = fewer valid
- * entries than k (both set with system-scope atomics; read them with grace_status_take). */
+ * entries than k, bit 3 = a grid-barrier wait of the one-launch select ran out (the result is not
+ * valid) (all set with system-scope atomics; read them with grace_status_take).  sel_gi (may be
+ * NULL): int32 [world * cap], every gathered entry's global index if selected, else -1 -- the
+ * output's non-zero positions, which grace_shard_clear zeroes when the next step reuses `out`
+ * (a recycled output, instead of a zero-fill of out_len elements). */
 size_t grace_shard_record_words(int64_t cap);
 size_t grace_shard_select_workspace_bytes(int32_t world, int64_t cap);
 grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t rank, int64_t cap, const int64_t* tab,
                                   int64_t k, float* residual, float* out, int64_t out_base, int64_t out_len,
-                                  int32_t* pay_idx, void* ws, size_t ws_bytes, int32_t* status_host, void* stream);
+                                  int32_t* pay_idx, int32_t* sel_gi, void* ws, size_t ws_bytes, int32_t* status_host,
+                                  void* stream);
+grace_status_t grace_shard_clear(float* out, int64_t out_base, int64_t out_len, const int32_t* sel_gi, int64_t count,
+                                 void* stream);
 
 /* ---- DGC (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39) -------------------------
  * compress: grace_dgc_sample (|t| at the sampled indices: sample_idx from the caller = torch's

@@ -35,15 +35,17 @@ def _worker(rank, world, path, outdir, sizes, case, ratio, steps):
     res = {}
     for s in range(steps):
         full = _bucket(case, n, 100 + s)
-        out = eng.step(torch.from_numpy(full[base:base + sizes[rank]].copy()).cuda(), "bucket")
+        # the result is dropped right away (as the DDP loop does): the next step recycles it and
+        # zeroes only the previous selection (grace_shard_clear) instead of zero-filling all of it
+        res[f"out{s}"] = eng.step(torch.from_numpy(full[base:base + sizes[rank]].copy()).cuda(), "bucket").cpu().numpy()
         v, i = eng.last_payload
         v, i = v.cpu().numpy(), i.cpu().numpy()
         keep = i >= 0
-        res[f"out{s}"] = out.cpu().numpy()
         res[f"vals{s}"] = v[keep]
         res[f"idx{s}"] = i[keep]
         res[f"res{s}"] = eng.residuals["bucket"].cpu().numpy()
     res["host_reads"] = np.array([eng.host_reads])
+    res["recycled"] = np.array([eng._recycler.hits])
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
@@ -61,7 +63,7 @@ def _bits(a, b):
 ])
 def test_sharded_topk_native_matches_single_gpu(world, sizes, case, ratio):
     from grace_amd import ops
-    steps = 2
+    steps = 3
     with tempfile.TemporaryDirectory() as tmp:
         mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, steps),
                  nprocs=world, join=True)
@@ -95,6 +97,8 @@ def test_sharded_topk_native_matches_single_gpu(world, sizes, case, ratio):
         assert _bits(outs[0][f"out{s}"], out1.cpu().numpy())
     # the partition is agreed once (first step); the later steps read nothing on the host
     assert all(int(o["host_reads"][0]) == (1 if world > 1 else 0) for o in outs)
+    # every step after the first reused its dropped output
+    assert all(int(o["recycled"][0]) == steps - 1 for o in outs)
 
 
 def _resize_worker(rank, world, path, outdir, check_sizes):
