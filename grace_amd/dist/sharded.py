@@ -156,10 +156,6 @@ class ShardedTopK:
     def _check_status(self, device):
         st = self.k_ops.status(device)
         bits = self.k_ops.take_status(st)
-        if bits & 4:
-            raise RuntimeError(
-                "grace_amd ShardedTopK: a grid-barrier wait of the one-launch select ran out (status "
-                f"{bits:#x}); the previous step's result is not valid")
         if bits:
             raise ShardPartitionError(
                 "grace_amd ShardedTopK: a rank's shard length changed after the name's first step (status "

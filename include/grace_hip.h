@@ -438,8 +438,7 @@ grace_status_t grace_normal_fill(float* x, int64_t n, uint64_t seed, void* strea
  * (residual[idx] = v) where the local engine picked an entry the global cut rejects.
  * tab: device int64 [m_0 .. m_{W-1}, base_0 .. base_{W-1}] (the agreed partition).  status_host
  * (pinned, may be NULL): bit 1 = a record's shard length differs from tab, bit 2 = fewer valid
- * entries than k, bit 3 = a grid-barrier wait of the one-launch select ran out (the result is not
- * valid) (all set with system-scope atomics; read them with grace_status_take).  sel_gi (may be
+ * entries than k (both set with system-scope atomics; read them with grace_status_take).  sel_gi (may be
  * NULL): int32 [world * cap], every gathered entry's global index if selected, else -1 -- the
  * output's non-zero positions, which grace_shard_clear zeroes when the next step reuses `out`
  * (a recycled output, instead of a zero-fill of out_len elements). */

@@ -8,4 +8,3 @@ python3 -c "from grace_amd.build import build; build(variant='stamps')"
 GRACE_BUILD_DEFS=GRACE_TERN_FLUSH python3 -c "from grace_amd.build import build; build(variant='ternflush')"
 GRACE_BUILD_DEFS=GRACE_TERN_ENC_NT python3 -c "from grace_amd.build import build; build(variant='ternnt')"
 GRACE_BUILD_DEFS=GRACE_SEG_NOSMALL python3 -c "from grace_amd.build import build; build(variant='segnosmall')"
-GRACE_BUILD_DEFS=GRACE_SHARD_3K python3 -c "from grace_amd.build import build; build(variant='shard3k')"

@@ -78,9 +78,9 @@ for step in range(6):
         ws = ops.workspace("shardsel", ops._lib.query("grace_shard_select_workspace_bytes", W, cap), dev)
         sv = ws[64:256].cpu().numpy().view(np.uint64)
         us = lambda a, b: round((int(sv[b]) - int(sv[a])) / 100.0, 1)   # noqa: E731
-        print(f"step {step} one-launch select stamps, us (workgroup 0, then the last arriver): load + coarse hist "
-              f"{us(0, 1)}, barrier {us(1, 2)}, coarse cut + sub-bins {us(2, 3)}, barrier {us(3, 4)}, sub cut + list "
-              f"{us(4, 5)}, to last {us(5, 6)}, last {us(6, 7)}; total {us(0, 7)}")
+        print(f"step {step} select stamps, us from the coarse launch's start (workgroup 0 unless noted): "
+              f"coarse {us(0, 1)}, boundary {us(1, 2)}, apply {us(2, 3)}, boundary {us(3, 4)}, bnd to arrival "
+              f"{us(4, 5)}, to the last arriver {us(5, 6)}, its ranking {us(6, 7)}; total {us(0, 7)}")
 med = [statistics.median(r[i] for r in rows[2:]) for i in range(3)]
 print(f"W={W} n={n} k={k} per-rank device time, us (median of steps 2..5): local top-k {med[0]:.1f}, "
       f"dense zero-fill {med[1]:.1f}, select {med[2]:.1f}; serial sum {sum(med):.1f} "
