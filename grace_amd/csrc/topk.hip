@@ -1350,6 +1350,8 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
         uint32_t tot;
         const uint32_t ex = block_excl_scan<BLOCK>(packed, fs.s_w, &tot);
         if (t == 0) {
+          // one reservation per workgroup and list (128 on each counter: as 8 copies, a timing-only
+          // build, the finalize was 1 us faster in 11.7 -- not worth a two-level position scheme)
           fs.s_res[0] = (tot & 0xFFFFu) ? atomicAdd(&w.ctl->n_sel, tot & 0xFFFFu) : 0u;
           fs.s_res[1] = (tot >> 16) ? atomicAdd(&w.ctl->n_bacc, tot >> 16) : 0u;
         }
