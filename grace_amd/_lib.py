@@ -58,8 +58,9 @@ SIGNATURES = {
     "grace_topk_segmented_chunk": (I64, [I32, I32]),
     "grace_topk_segmented_seg_ws_bytes": (I64, [I64, I64]),
     "grace_topk_segmented_fin_blocks": (I32, [I64, I64]),
-    "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, I32, P, I32, P, P, I64, P, P, P, I64, I64, P, P, P, P,
-                                       SZ, P]),
+    "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, I32, P, I32, P, P, I64, P, P, P, I64, I64, P, P, P,
+                                       P, P, I32, P, SZ, P]),
+    "grace_topk_segmented_carry_len": (I64, [I64]),
     "grace_shard_record_words": (SZ, [I64]),
     "grace_shard_select_workspace_bytes": (SZ, [I32, I64]),
     "grace_shard_select": (ST, [P, I32, I32, I64, P, I64, P, P, I64, I64, P, P, P, SZ, P, P]),

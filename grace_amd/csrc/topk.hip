@@ -1589,6 +1589,13 @@ struct SegPlan {
   const int32_t* fin_li;    // [nfin] large-segment slot of every finalize workgroup
   char* ws;
   int32_t nL, nS;
+  // residual-sample carry per large segment (grace_topk_residual_step_carry's, per segment): the
+  // prep writes the segment's t at its sample positions to carry + carry_off[li], the finalize the
+  // segment's selection threshold after them; with carry_valid the next prep derives r' there from
+  // them and reads only g (one random read per sample instead of two).  carry may be null.
+  float* carry;
+  const int64_t* carry_off;
+  int32_t carry_valid;
 };
 
 __device__ __forceinline__ StepArgs seg_step_args(const SegPlan& p, int s) {
@@ -1628,11 +1635,22 @@ __device__ __forceinline__ TopkWs seg_ws(const SegPlan& p, int li, int64_t n, in
   w.chist = nullptr;
   return w;
 }
-__device__ __forceinline__ int64_t seg_sample_n(int64_t n) {
+__host__ __device__ __forceinline__ int64_t seg_sample_n(int64_t n) {
   int64_t S = n / 256;
   S = S < kSegSampleMin ? kSegSampleMin : (S > kSegSampleMax ? kSegSampleMax : S);
   return S < n / 4 ? S : n / 4;
 }
+// the step arguments of large segment slot li, with its carry (prep and finalize)
+__device__ __forceinline__ StepArgs seg_large_args(const SegPlan& p, int li) {
+  StepArgs a = seg_step_args(p, p.large[li]);
+  if (p.carry) {
+    a.sample_n = seg_sample_n(a.n);
+    a.rs_out = p.carry + p.carry_off[li];
+    a.rs_in = p.carry_valid ? a.rs_out : nullptr;
+  }
+  return a;
+}
+
 
 // A small segment (n <= kSegSmallMax) in one workgroup, built for throughput next to many others in the
 // same launch: t staged in LDS with 8 loads per array in flight per thread, the exact threshold by
@@ -1699,7 +1717,7 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
     seg_small_body<HAS_RES, MODE>(a, reinterpret_cast<float*>(lds), lds + kSmallN, s_w, s_res);
     return;
   }
-  const StepArgs a = seg_step_args(p, p.large[b]);
+  const StepArgs a = seg_large_args(p, b);
   const TopkWs w = seg_ws(p, b, a.n, a.k);
   STAMP_IF(true, w.ctl, 13);
 #ifdef GRACE_STAMPS
@@ -1715,7 +1733,25 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {   // every sample load issued before any is used (clamped index)
     const int64_t sidx = (int64_t)q * kSelBlock + tid;
-    t[q] = compensate<HAS_RES>(a, sample_pos(sidx < S ? sidx : S - 1, st));
+    const int64_t sc = sidx < S ? sidx : S - 1;
+    const int64_t pos = sample_pos(sc, st);
+    if (HAS_RES && a.rs_in) {
+      // the segment's carried t'(pos) and threshold: r'(pos) as the last step left it, and one
+      // random read (g) per sample instead of two (the headline bracket's carry, per segment)
+      const float tp = a.rs_in[sc];
+      const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + S);
+      const float rp = comp_key(abs_key(tp), (uint32_t)pos) >= Tp ? tp - tp : tp;
+      t[q] = a.beta * rp + a.gamma * a.g[pos];
+    } else {
+      t[q] = compensate<HAS_RES>(a, pos);
+    }
+  }
+  if (a.rs_out) {
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t sidx = (int64_t)q * kSelBlock + tid;
+      if (sidx < S) a.rs_out[sidx] = t[q];
+    }
   }
   // this step's counters and candidate histogram (the segment's previous finalize has completed)
   if (tid >= 3 && tid < 12) reinterpret_cast<uint32_t*>(w.ctl)[tid] = 0u;
@@ -1780,7 +1816,7 @@ __global__ __launch_bounds__(kSelBlock) void seg_fin_kernel(SegPlan p) {
   const int li = p.fin_li[blockIdx.x];
   const int fi = (int)((int64_t)blockIdx.x - p.fin_off[li]);
   const int fcnt = (int)(p.fin_off[li + 1] - p.fin_off[li]);
-  const StepArgs a = seg_step_args(p, p.large[li]);
+  const StepArgs a = seg_large_args(p, li);
   const TopkWs w = seg_ws(p, li, a.n, a.k);
   STAMP_IF(fi == 0, w.ctl, 8);
   finalize_run<MODE, kSelBlock, false>(a, w, fi, fcnt, fs, false);
@@ -2071,6 +2107,9 @@ int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out) {
 
 int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k) { return seg_ws_bytes_one(n, k); }
 
+// f32 words of a large segment's carry: t at its sample positions + the u64 threshold
+int64_t grace_topk_segmented_carry_len(int64_t n) { return seg_sample_n(n) + 2; }
+
 // finalize workgroups for a large segment: one round (kSelBlock * kFinPer candidates) each for the
 // ~2 k the bracket's band holds at most in practice, plus one
 int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k) {
@@ -2086,7 +2125,8 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
                                          int32_t n_small, const int64_t* chk_off, const int32_t* chunk_li,
                                          int64_t nchunks, const int64_t* ws_off, const int64_t* fin_off,
                                          const int32_t* fin_li, int64_t nfin, int64_t n_total, float* vals,
-                                         int32_t* idx, float* out, void* ws, size_t ws_bytes, void* stream) {
+                                         int32_t* idx, float* out, float* carry, const int64_t* carry_off,
+                                         int32_t carry_valid, void* ws, size_t ws_bytes, void* stream) {
   GRACE_REQUIRE(g && residual && seg_off && k_off && vals && idx && n_large >= 0 && n_small >= 0 &&
                     n_large + n_small >= 1 && n_total >= 1 && n_total < ((int64_t)1 << 31) &&
                     (n_large == 0 || (large && chk_off && chunk_li && ws_off && fin_off && fin_li && ws &&
@@ -2113,6 +2153,10 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
   p.ws = reinterpret_cast<char*>(ws);
   p.nL = n_large;
   p.nS = n_small;
+  GRACE_REQUIRE(!carry || carry_off, "grace_topk_segmented_step: carry without carry_off");
+  p.carry = has_residual ? carry : nullptr;   // the carry is a residual's
+  p.carry_off = carry_off;
+  p.carry_valid = carry && has_residual && carry_valid ? 1 : 0;
   (void)ws_bytes;   // sized by the caller from grace_topk_segmented_seg_ws_bytes (checked in the host layer)
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual) |
                      reinterpret_cast<uintptr_t>(out)) & 15u) == 0;

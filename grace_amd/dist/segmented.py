@@ -35,6 +35,11 @@ class SegmentedTopK:
         # measured 0.4-4 us slower per step on the ResNet-50 set)
         self._small_max = None
         self._order = "index"
+        # per name: the residual-sample carry of the large segments (the bracket reads g alone at
+        # its sample positions when the carry holds the previous step of the same residual), the
+        # residual and its version counter when the carry was written, the tables it belongs to
+        self._carries = {}
+        self._use_carry = True   # A/B knob (tools/ab_seg.py)
 
     def tables(self, sizes, device, has_res, dense_out):
         """Device tables of one segment list (cached): offsets, the small / large split, the main
@@ -52,6 +57,7 @@ class SegmentedTopK:
         seg, kk = [0], [0]
         large, small, chk, chunk_li, ws_off, fin, fin_li = [], [], [0], [], [], [0], []
         ws_total = 0
+        carry_off, carry_total = [], 0
         ks = []
         for i, n in enumerate(sizes):
             if n < 1:
@@ -75,13 +81,16 @@ class SegmentedTopK:
             fin.append(fin[-1] + f)
             fin_li += [li] * f
             ws_total += (int(_lib.query("grace_topk_segmented_seg_ws_bytes", n, k)) + 255) // 256 * 256
+            carry_off.append(carry_total)
+            carry_total += (int(_lib.query("grace_topk_segmented_carry_len", n)) + 3) // 4 * 4   # 16-B aligned
         t64 = lambda v: torch.tensor(v, dtype=torch.int64).to(device)   # noqa: E731
         t32 = lambda v: torch.tensor(v, dtype=torch.int32).to(device)   # noqa: E731
         ws = torch.zeros(max(ws_total, 256), dtype=torch.uint8, device=device)
         hit = {"seg_off": t64(seg), "k_off": t64(kk), "large": t32(large or [0]), "n_large": len(large),
                "small": t32(small or [0]), "n_small": len(small), "chk_off": t64(chk), "chunk_li": t32(chunk_li or [0]),
                "nchunks": chk[-1], "ws_off": t64(ws_off or [0]), "fin_off": t64(fin), "fin_li": t32(fin_li or [0]),
-               "nfin": fin[-1], "ws": ws, "k_total": kk[-1], "n": seg[-1]}
+               "nfin": fin[-1], "ws": ws, "k_total": kk[-1], "n": seg[-1],
+               "carry_off": t64(carry_off or [0]), "carry_len": max(carry_total, 4)}
         self._tables[key] = hit
         return hit
 
@@ -102,14 +111,31 @@ class SegmentedTopK:
         k_total = T["k_total"]
         pay = torch.empty(2 * k_total, dtype=torch.float32, device=g.device)
         vals, idx = pay[:k_total], pay[k_total:].view(torch.int32)
+        carry, valid = self._carry_for(name, res, has, T) if self._use_carry else (None, False)
         _lib.call("grace_topk_segmented_step", g.data_ptr(), res.data_ptr(), 1 if has else 0, self.beta, self.gamma,
                   T["seg_off"].data_ptr(), T["k_off"].data_ptr(), T["large"].data_ptr(), T["n_large"],
                   T["small"].data_ptr(), T["n_small"], T["chk_off"].data_ptr(), T["chunk_li"].data_ptr(),
                   T["nchunks"], T["ws_off"].data_ptr(), T["fin_off"].data_ptr(), T["fin_li"].data_ptr(), T["nfin"], n,
                   vals.data_ptr(), idx.data_ptr(),
-                  dense.data_ptr() if dense is not None else None, T["ws"].data_ptr(), T["ws"].numel(), ops._stream())
+                  dense.data_ptr() if dense is not None else None,
+                  carry.data_ptr() if carry is not None else None, T["carry_off"].data_ptr(), 1 if valid else 0,
+                  T["ws"].data_ptr(), T["ws"].numel(), ops._stream())
+        if carry is not None:   # written by this step (the kernels only use it with a residual)
+            self._carries[name] = (carry, res, res._version, id(T))
         self.last_payload = (vals, idx)
         return pay
+
+    def _carry_for(self, name, res, has, T):
+        """This name's carry buffer and whether it holds the previous step of `res` as that step
+        left it: the same residual tensor, unmodified since (version counter), same tables."""
+        ent = self._carries.get(name)
+        if ent is not None and ent[0].numel() == T["carry_len"] and ent[0].device == res.device:
+            carry = ent[0]
+            valid = bool(has) and ent[1] is res and ent[2] == res._version and ent[3] == id(T)
+        else:
+            carry = torch.empty(T["carry_len"], dtype=torch.float32, device=res.device)
+            valid = False
+        return carry, valid
 
     def step(self, flat, sizes, name="bucket", out=None):
         """flat: f32[sum(sizes)] gradients; returns the flat aggregated result (``out`` if given,

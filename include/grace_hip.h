@@ -293,7 +293,11 @@ grace_status_t grace_fp16_decompress_aggregate(const void* half_in, int64_t stri
  * ws_off[n_large] (byte offsets of each large segment's grace_topk_segmented_seg_ws_bytes(n, k)
  * workspace, 256-B aligned, zeroed once), fin_off[n_large + 1] / fin_li[nfin] (the finalize
  * workgroups: grace_topk_segmented_fin_blocks(n, k) per large segment).  Payload (vals f32, idx i32 GLOBAL indices)[k_off[nseg]];
- * out (dense world-1 result, may alias g) or NULL (world > 1: residual and payload only). */
+ * out (dense world-1 result, may alias g) or NULL (world > 1: residual and payload only).
+ * carry (may be NULL; has_residual only): f32, grace_topk_segmented_carry_len(n) words per large
+ * segment at carry_off[n_large] -- the segment's t at its sample positions and its selection
+ * threshold, written by the step; carry_valid: they are the previous step's for this residual
+ * (the next prep then reads g alone at the sample positions). */
 int32_t grace_topk_segmented_small_max(void);
 int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out);
 int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k);
@@ -304,7 +308,9 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
                                          int32_t n_small, const int64_t* chk_off, const int32_t* chunk_li,
                                          int64_t nchunks, const int64_t* ws_off, const int64_t* fin_off,
                                          const int32_t* fin_li, int64_t nfin, int64_t n_total, float* vals,
-                                         int32_t* idx, float* out, void* ws, size_t ws_bytes, void* stream);
+                                         int32_t* idx, float* out, float* carry, const int64_t* carry_off,
+                                         int32_t carry_valid, void* ws, size_t ws_bytes, void* stream);
+int64_t grace_topk_segmented_carry_len(int64_t n);
 
 /* ---------------------------------------------------------------------- random-k / threshold */
 /* Random-k indices (randomk.py:11: randint(numel, [k]), WITH replacement) from a counter-based

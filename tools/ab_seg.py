@@ -1,7 +1,7 @@
 """A/B of the segmented top-k's host-side layout choices in ONE process (interleaved rounds, event
 timing of 20 back-to-back ddp_segmented steps on the ResNet-50 shapes, world 1): the small-segment
-limit (8192 vs 32768) and the order of the large segments' main-pass chunks (descending size vs
-tensor order).  Every variant's output is checked equal to the first one's."""
+limit, the order of the large segments' main-pass chunks and the per-segment residual-sample
+carry (on / off).  Every variant's output is checked equal to the first one's."""
 import os
 import statistics
 import sys
@@ -16,12 +16,12 @@ dev = torch.device("cuda", 0)
 sizes = [int(torch.Size(s).numel()) for s in bench.resnet50_shapes()]
 n = sum(sizes)
 gs = [torch.randn(n, device=dev) for _ in range(3)]
-variants = {"small8k_size": (8192, "size"), "small8k_index": (8192, "index"),
-            "small32k_size": (32768, "size"), "small32k_index": (32768, "index")}
+variants = {"carry": (8192, "index", True), "no_carry": (8192, "index", False),
+            "carry_size_order": (8192, "size", True)}
 engs = {}
-for name, (sm, order) in variants.items():
+for name, (sm, order, carry) in variants.items():
     e = SegmentedTopK(0.01)
-    e._small_max, e._order = sm, order
+    e._small_max, e._order, e._use_carry = sm, order, carry
     engs[name] = e
 outs = {name: e.step(gs[0], sizes) for name, e in engs.items()}
 ref = next(iter(outs.values()))
