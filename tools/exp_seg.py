@@ -57,6 +57,7 @@ for step in range(4):
             v = ph(q)
             print("  %-13s min %7.1f  median %7.1f  max %7.1f" % (nm, min(v), float(np.median(v)), max(v)))
         print(f"step {step}: {len(rows)} large segments, fallbacks {len(fb)}")
-        for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8]:
+        slow = sorted(rows, key=lambda r: -r[-1])[:3]   # the slowest finalizes
+        for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8] + slow:
             print("  seg %d n %d k %d status %d n_sure %d n_cand %d need %d n_bnd %d | fin us: findB %.1f route %.1f "
                   "to_last %.1f bnd %.1f total %.1f" % r)
