@@ -37,6 +37,7 @@ constexpr int kMaxGroupChunks = 32768;                 // LDS histogram bins (12
 
 // pass 1: per-workgroup LDS histogram of chunk ids, flushed with one atomic per non-zero bin; the
 // last workgroup to finish (ticket; agent-scope atomics, no L2 fences) scans the counts in place
+// (the counts live in the caller's zeroed workspace; pass 2 leaves them zeroed again)
 __device__ void scan_counts_block(uint32_t* counts, int64_t nchunks);
 
 template <typename IdxT>
@@ -114,7 +115,9 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
                                                                    const IdxT* __restrict__ idx, int64_t k,
                                                                    int64_t nchunks, uint32_t* __restrict__ cursor,
                                                                    float* __restrict__ vals_out,
-                                                                   uint16_t* __restrict__ off_out) {
+                                                                   uint16_t* __restrict__ off_out,
+                                                                   uint32_t* __restrict__ ends_out,
+                                                                   uint32_t* __restrict__ ticket) {
   extern __shared__ uint32_t h[];
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
   __syncthreads();
@@ -140,6 +143,22 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
     const uint32_t pos = atomicAdd(&h[ii[e] >> kPChunkLog], 1u);
     if (vals_out) vals_out[pos] = vv[e];
     off_out[pos] = (uint16_t)(ii[e] & (kPChunk - 1));   // the offset inside its chunk (13 bits)
+  }
+  // the cursors (device atomics) now hold every chunk's end: the last workgroup to arrive copies
+  // them into the payload's end table and re-zeroes them for the next grouping (the scratch lives
+  // in the caller's workspace, so no memset launch precedes the histogram pass)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) {
+    ends_out[c] = __hip_atomic_load(cursor + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cursor + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -211,22 +230,30 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
 
 // group entries by 8192-element chunk (u16 offsets, chunk end offsets); vals optional.  Shared by
 // grace_sort_payload and the world-1 random-k step (sparse.hip).
+// scratch: [2 tickets | 248 B | counts u32[kMaxGroupChunks]] (group_scratch_bytes), zeroed once and left
+// zeroed: counts -> exclusive offsets (hist pass) -> chunk ends (scatter cursors) -> ends_out
 template <typename IdxT>
 hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t nchunks, float* vals_out,
-                          uint16_t* off_out, uint32_t* ends_out, uint32_t* ticket, hipStream_t s) {
-  uint32_t* counts = ends_out;   // counts -> exclusive offsets (hist) -> chunk ends (scatter cursors)
-  hipError_t e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * nchunks, s);
-  if (e != hipSuccess || k == 0) return e;
+                          uint16_t* off_out, uint32_t* ends_out, uint32_t* scratch, hipStream_t s) {
+  if (k == 0) return hipMemsetAsync(ends_out, 0, sizeof(uint32_t) * nchunks, s);
+  uint32_t* counts = scratch + 64;
   const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
   const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
-  group_hist_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, ticket);
-  e = hipGetLastError();
+  group_hist_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, scratch);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  group_scatter_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out);
+  group_scatter_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out, ends_out,
+                                                          scratch + 1);
   return hipGetLastError();
 }
 template hipError_t group_by_chunk<int64_t>(const float*, const int64_t*, int64_t, int64_t, float*, uint16_t*,
                                             uint32_t*, uint32_t*, hipStream_t);
+// fixed size whatever nchunks is: a caller that places other data after the scratch must never let
+// a larger call's counts land on a smaller call's data (the counts must stay zeroed)
+size_t group_scratch_bytes(int64_t nchunks) {
+  (void)nchunks;
+  return 256 + sizeof(uint32_t) * (size_t)kMaxGroupChunks;
+}
 
 }  // namespace grace
 
@@ -236,8 +263,7 @@ extern "C" {
 
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
   (void)k;
-  (void)n;
-  return 256;   // the arrival ticket, left zeroed by every call
+  return group_scratch_bytes((n + kPChunk - 1) / kPChunk);   // tickets + chunk counts, left zeroed by every call
 }
 
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is

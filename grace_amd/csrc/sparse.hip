@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kSBlock) void randomk_pass_kernel(const float* __re
 template <typename IdxT>
 hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t nchunks, float* vals_out,
                           uint16_t* off_out, uint32_t* ends_out, uint32_t* ticket, hipStream_t s);
+size_t group_scratch_bytes(int64_t nchunks);
 constexpr int kRkChunkLog = 13;                  // = payload.hip kPChunkLog
 constexpr int kRkChunk = 1 << kRkChunkLog;
 constexpr int kRkQ = kRkChunk / (4 * kSBlock);   // quads per thread per array
@@ -667,7 +668,8 @@ grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t ha
 
 size_t grace_randomk_step_w1_dense_workspace_bytes(int64_t n, int64_t k) {
   const int64_t nch = (n + kRkChunk - 1) / kRkChunk;
-  return 256 + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255) + sizeof(uint16_t) * (size_t)(k < 1 ? 1 : k);
+  return group_scratch_bytes(nch) + ((sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255) +
+         sizeof(uint16_t) * (size_t)(k < 1 ? 1 : k);
 }
 
 size_t grace_randomk_group_bytes(int64_t n, int64_t k) {
@@ -687,16 +689,16 @@ grace_status_t grace_randomk_step_w1_dense(const float* g, float* residual, int3
   GRACE_REQUIRE(!prev_grp || grp, "grace_randomk_step_w1_dense: a recycled output needs this step's grouping buffer");
   hipStream_t s = as_stream(stream);
   char* p = reinterpret_cast<char*>(ws);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(p);
+  uint32_t* scratch = reinterpret_cast<uint32_t*>(p);   // the grouping's tickets and counts (left zeroed)
   // this step's grouping: into the caller's per-name buffer `grp` (it becomes the next step's
   // prev_grp), or into the workspace
-  char* q = grp ? reinterpret_cast<char*>(grp) : p + 256;
+  char* q = grp ? reinterpret_cast<char*>(grp) : p + group_scratch_bytes(nch);
   const size_t eb = (sizeof(uint32_t) * (size_t)nch + 255) & ~(size_t)255;
   uint32_t* ends = reinterpret_cast<uint32_t*>(q);
   uint16_t* offs = reinterpret_cast<uint16_t*>(q + eb);
   const uint32_t* pends = prev_grp ? reinterpret_cast<const uint32_t*>(prev_grp) : nullptr;
   const uint16_t* poffs = prev_grp ? reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(prev_grp) + eb) : nullptr;
-  const hipError_t e = group_by_chunk<int64_t>(nullptr, idx, k, nch, nullptr, offs, ends, ticket, s);
+  const hipError_t e = group_by_chunk<int64_t>(nullptr, idx, k, nch, nullptr, offs, ends, scratch, s);
   if (e != hipSuccess) { set_error("grace_randomk_step_w1_dense", e); return GRACE_ERR_HIP; }
   if (prev_grp) {
     if (has_residual)
