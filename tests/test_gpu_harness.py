@@ -214,3 +214,34 @@ def test_segmented_edge_segments(world):
             assert same_bits(rcat[off:off + n], res[j]), (s, j)
             off += n
             koff += k
+
+
+def test_segmented_carry_tracks_the_residual():
+    """The per-tensor residual-sample carry (SegmentedTopK._carries) is used only while the residual
+    is the tensor the previous step left, unmodified: an in-place edit (version counter) or a
+    replaced residual invalidates it, and every step stays bit-exact against the oracle."""
+    from grace_amd.dist.segmented import SegmentedTopK
+    ratio = 0.01
+    sizes = [1 << 20, 4099, (1 << 19) + 3, 100000, 9000]
+    eng = SegmentedTopK(ratio)
+    rng = np.random.default_rng(77)
+    res = [None] * len(sizes)
+    valid_seen = []
+    for s in range(5):
+        gs = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+        r = eng.residuals.get("bucket")
+        if s == 2:
+            r.mul_(2.0)                                   # in place: the carry no longer matches
+            res = [x * np.float32(2.0) for x in res]
+        if s == 3:
+            eng.residuals["bucket"] = r.clone()           # replaced: another tensor
+        if r is not None:
+            T = eng.tables(sizes, r.device, True, True)
+            valid_seen.append(eng._carry_for("bucket", eng.residuals["bucket"], True, T)[1])
+        out = eng.step(torch.from_numpy(np.concatenate(gs)).cuda(), sizes).cpu().numpy()
+        off = 0
+        for j, g in enumerate(gs):
+            _, _, _, res[j], o = O.topk_residual_step(g, res[j], ratio)
+            assert same_bits(out[off:off + g.size], o), (s, j)
+            off += g.size
+    assert valid_seen == [True, False, False, True]
