@@ -90,7 +90,8 @@ class SegmentedTopK:
                "small": t32(small or [0]), "n_small": len(small), "chk_off": t64(chk), "chunk_li": t32(chunk_li or [0]),
                "nchunks": chk[-1], "ws_off": t64(ws_off or [0]), "fin_off": t64(fin), "fin_li": t32(fin_li or [0]),
                "nfin": fin[-1], "ws": ws, "k_total": kk[-1], "n": seg[-1],
-               "carry_off": t64(carry_off or [0]), "carry_len": max(carry_total, 4)}
+               "carry_off": t64(carry_off or [0]), "carry_len": max(carry_total, 4),
+               "carry_key": (sizes, small_max)}   # the carry layout depends on these only
         self._tables[key] = hit
         return hit
 
@@ -121,17 +122,18 @@ class SegmentedTopK:
                   carry.data_ptr() if carry is not None else None, T["carry_off"].data_ptr(), 1 if valid else 0,
                   T["ws"].data_ptr(), T["ws"].numel(), ops._stream())
         if carry is not None:   # written by this step (the kernels only use it with a residual)
-            self._carries[name] = (carry, res, res._version, id(T))
+            self._carries[name] = (carry, res, res._version, T["carry_key"])
         self.last_payload = (vals, idx)
         return pay
 
     def _carry_for(self, name, res, has, T):
         """This name's carry buffer and whether it holds the previous step of `res` as that step
-        left it: the same residual tensor, unmodified since (version counter), same tables."""
+        left it: the same residual tensor, unmodified since (version counter), the same segment
+        layout (sizes and small-segment limit; the tables also differ by has_res, the carry not)."""
         ent = self._carries.get(name)
         if ent is not None and ent[0].numel() == T["carry_len"] and ent[0].device == res.device:
             carry = ent[0]
-            valid = bool(has) and ent[1] is res and ent[2] == res._version and ent[3] == id(T)
+            valid = bool(has) and ent[1] is res and ent[2] == res._version and ent[3] == T["carry_key"]
         else:
             carry = torch.empty(T["carry_len"], dtype=torch.float32, device=res.device)
             valid = False
