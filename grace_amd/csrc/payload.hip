@@ -19,7 +19,12 @@ namespace grace {
 
 constexpr int kPChunkLog = 13;
 constexpr int kPChunk = 1 << kPChunkLog;
-constexpr int kPBlock = 256;
+#ifndef GRACE_P_BLOCK
+#define GRACE_P_BLOCK 256
+#endif
+// decode workgroup (A/B knob; 8 x 671 K entries into 256 MiB, tools/exp_wn_local.py: 256 threads
+// 58 us, 512 68 us, 1024 146 us)
+constexpr int kPBlock = GRACE_P_BLOCK;
 
 #ifndef GRACE_GROUP_BLOCK
 #define GRACE_GROUP_BLOCK 1024
