@@ -195,7 +195,7 @@ def pmc_traffic(workload, alg_bytes):
     WRITE_SIZE passes (tools/prof_r02.sh -> tools/pmc_all.py), with the ratio to the algorithmic
     bytes; None when that workload was not profiled."""
     wl = None
-    for tag in ("r03", "r02"):   # the newest committed passes that cover the workload
+    for tag in ("r04", "r03", "r02"):   # the newest committed passes that cover the workload
         try:
             with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_secondary.json")) as f:
                 wl = json.load(f)["workloads"][workload]
@@ -640,8 +640,10 @@ def bench_topk_sharded(args, world, rank, dev):
         per_gpu = 12.0 * m + 8.0 * k + 16.0 * world * k + 8.0 * k
     else:
         per_gpu = survey
+    traffic, ratio = pmc_traffic("topk_sharded", per_gpu) if world == 1 else (None, None)
     line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio,
                         "algorithmic_bytes_per_gpu": per_gpu, "survey_bytes_per_gpu": survey,
                         "output": "recycled" if recycled else "dense zero-fill",
                         "recycled_steps": eng._recycler.hits}
@@ -682,8 +684,10 @@ def bench_ddp(args, world, rank, dev):
         k_sum = sum(min(p.numel(), max(1, int(p.numel() * 0.01))) for p in bucket.params)
     alg = (16 if world == 1 else 12) * total + 8 * k_sum
     t = elapsed / args.steps
+    traffic, ratio = pmc_traffic(args.workload, alg) if world == 1 else (None, None)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio,
                         "algorithmic_bytes_per_step": alg, "selected_per_step": k_sum,
                         "note": "16 B per element at world 1 (g, r read; r', dense out written) + 8 B per selected entry"}
     return line

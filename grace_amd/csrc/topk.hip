@@ -1024,7 +1024,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
 // provisional decision (key > mid) was wrong, in both directions (fbelow: below the boundary bin).
 template <int MODE>
 __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[kFinPer], uint32_t fsel,
-                                            uint32_t fbelow, uint32_t ps, uint32_t mid) {
+                                            uint32_t fbelow, uint32_t ps, uint32_t mid, TopkCtl* dbg_ctl = nullptr) {
 #pragma unroll
   for (int u = 0; u < kFinPer; ++u) {
     const float v = u2f((uint32_t)e[u].y);
@@ -1045,6 +1045,19 @@ __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[k
       a.out[e[u].x] = 0.f;
     }
   }
+#ifdef GRACE_STAMPS   // diagnostic: fix-up writes of this round (ctl stamp slot 18: selected below mid, 19: rejected above)
+  if (dbg_ctl) {
+    uint32_t f1 = 0, f2 = 0;
+#pragma unroll
+    for (int u = 0; u < kFinPer; ++u) {
+      const bool am = abs_key(u2f((uint32_t)e[u].y)) > mid;
+      f1 += ((fsel >> u) & 1u) && !am;
+      f2 += !((fsel >> u) & 1u) && ((fbelow >> u) & 1u) && am;
+    }
+    if (f1) atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(dbg_ctl) + 64) + 18, (unsigned long long)f1);
+    if (f2) atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(dbg_ctl) + 64) + 19, (unsigned long long)f2);
+  }
+#endif
 }
 
 // ---- parallel exact fallback (the sampled bracket missed or a list overflowed: in practice massive
@@ -1362,7 +1375,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
 #pragma unroll
         for (int u = 0; u < kFinPer; ++u)
           if ((fb >> u) & 1u) st_agent_i2(w.bnd + pb++, e[u]);
-        if (!defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid);
+        if (!defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid, w.ctl);
       }
     }
   }
@@ -1375,7 +1388,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
   __syncthreads();
   const bool last = fs.s_last;
   const bool preloaded = last && boundary_preload<BLOCK>(w, ok, need, nb, fs);
-  if (defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid);
+  if (defer) write_round<MODE>(a, e, fsel, fbelow, ps, mid, w.ctl);
   if (!last) return false;
   STAMP_IF(true, w.ctl, 11);
   boundary_work<MODE, BLOCK, AG>(a, w, ok, need, nb, fs, preloaded, mid);
@@ -1724,6 +1737,8 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
   if (tid == 0) {   // main-pass span of this segment: first chunk start (min), last chunk end (max)
     reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[16] = ~0ull;
     reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[17] = 0ull;
+    reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[18] = 0ull;
+    reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(w.ctl) + 64)[19] = 0ull;
   }
 #endif
   const int64_t S = seg_sample_n(a.n);
@@ -2154,7 +2169,9 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
   p.nL = n_large;
   p.nS = n_small;
   GRACE_REQUIRE(!carry || carry_off, "grace_topk_segmented_step: carry without carry_off");
-  p.carry = has_residual ? carry : nullptr;   // the carry is a residual's
+  // written by every step (a first step without a residual records t = g), read only with a
+  // residual whose previous step wrote it
+  p.carry = carry;
   p.carry_off = carry_off;
   p.carry_valid = carry && has_residual && carry_valid ? 1 : 0;
   (void)ws_bytes;   // sized by the caller from grace_topk_segmented_seg_ws_bytes (checked in the host layer)

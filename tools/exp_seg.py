@@ -58,6 +58,17 @@ for step in range(4):
             print("  %-13s min %7.1f  median %7.1f  max %7.1f" % (nm, min(v), float(np.median(v)), max(v)))
         print(f"step {step}: {len(rows)} large segments, fallbacks {len(fb)}")
         slow = sorted(rows, key=lambda r: -r[-1])[:3]   # the slowest finalizes
+        fix = [(int(large[li]), sizes[large[li]],
+                int(ws[offs[li] + 64:offs[li] + 256].view(np.uint64)[18]),
+                int(ws[offs[li] + 64:offs[li] + 256].view(np.uint64)[19]),
+                int(ws[offs[li]:offs[li] + 64].view(np.uint32)[5]),
+                int(ws[offs[li]:offs[li] + 64].view(np.uint32)[15]),
+                int(ws[offs[li]:offs[li] + 64].view(np.uint32)[0]),
+                int(ws[offs[li]:offs[li] + 64].view(np.uint32)[1])) for li in range(len(large))]
+        print("  fix-up writes: total selected-below-mid %d, rejected-above-mid %d, candidates %d" %
+              (sum(f[2] for f in fix), sum(f[3] for f in fix), sum(f[4] for f in fix)))
+        for f in sorted(fix, key=lambda f: -(f[2] + f[3]))[:5]:
+            print("    seg %d n %d sel<mid %d rej>mid %d n_cand %d mid %#x lo %#x hi %#x" % f)
         for r in sorted(rows, key=lambda r: -r[1])[:8] + fb[:8] + slow:
             print("  seg %d n %d k %d status %d n_sure %d n_cand %d need %d n_bnd %d | fin us: findB %.1f route %.1f "
                   "to_last %.1f bnd %.1f total %.1f" % r)
