@@ -2126,10 +2126,13 @@ int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k) { return seg_ws_
 int64_t grace_topk_segmented_carry_len(int64_t n) { return seg_sample_n(n) + 2; }
 
 // finalize workgroups for a large segment: one round (kSelBlock * kFinPer candidates) each for the
-// ~2 k the bracket's band holds at most in practice, plus one
+// ~2 k the bracket's band holds at most in practice, plus one (A/B knob: budget GRACE_SEG_FIN_MULT k)
+#ifndef GRACE_SEG_FIN_MULT
+#define GRACE_SEG_FIN_MULT 2
+#endif
 int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k) {
   const int64_t per = (int64_t)kSelBlock * kFinPer;
-  int64_t c = 2 * k < n ? 2 * k : n;
+  int64_t c = GRACE_SEG_FIN_MULT * k < n ? GRACE_SEG_FIN_MULT * k : n;
   c = (c + per - 1) / per + 1;
   return (int32_t)(c > kFinBlocks ? kFinBlocks : c);
 }
