@@ -2126,9 +2126,11 @@ int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k) { return seg_ws_
 int64_t grace_topk_segmented_carry_len(int64_t n) { return seg_sample_n(n) + 2; }
 
 // finalize workgroups for a large segment: one round (kSelBlock * kFinPer candidates) each for the
-// ~2 k the bracket's band holds at most in practice, plus one (A/B knob: budget GRACE_SEG_FIN_MULT k)
+// ~2-3 k a segment's small-sample band holds, plus one.  4 k budgeted: at 2 k a second round per
+// workgroup made the largest tensors' routing 8-10 us instead of 3 (ddp_segmented 110.7 -> 106.3 us,
+// profiles/r04_seg_fin_ab.txt).  A/B knob: budget GRACE_SEG_FIN_MULT k
 #ifndef GRACE_SEG_FIN_MULT
-#define GRACE_SEG_FIN_MULT 2
+#define GRACE_SEG_FIN_MULT 4
 #endif
 int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k) {
   const int64_t per = (int64_t)kSelBlock * kFinPer;

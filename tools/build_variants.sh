@@ -8,4 +8,4 @@ python3 -c "from grace_amd.build import build; build(variant='stamps')"
 GRACE_BUILD_DEFS=GRACE_TERN_FLUSH python3 -c "from grace_amd.build import build; build(variant='ternflush')"
 GRACE_BUILD_DEFS=GRACE_TERN_ENC_NT python3 -c "from grace_amd.build import build; build(variant='ternnt')"
 GRACE_BUILD_DEFS=GRACE_SEG_NOSMALL python3 -c "from grace_amd.build import build; build(variant='segnosmall')"
-GRACE_BUILD_DEFS=GRACE_SEG_FIN_MULT=4 python3 -c "from grace_amd.build import build; build(variant='fin4k')"
+GRACE_BUILD_DEFS=GRACE_SEG_FIN_MULT=2 python3 -c "from grace_amd.build import build; build(variant='fin2k')"
