@@ -1,5 +1,7 @@
-"""Diagnostic: host-side cost of the launch-bound 4 MiB signSGD step (bench.py --workload sign).
-Times N back-to-back calls on the host (no sync inside) and the GPU-side step with events."""
+"""Host submission cost per step of a bench workload: the bench's own step function, enqueued
+behind a long device sleep (so the queue never drains and never back-pressures), timed on the
+host.  A workload whose host cost per step is near its ms_per_step is launch-bound on the host.
+Usage: python3 tools/exp_host.py WORKLOAD [WORKLOAD ...]"""
 import os
 import sys
 import time
@@ -7,39 +9,29 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from grace_amd import _lib, ops  # noqa: E402
-from grace_amd.dist.communicator.allgather import Allgather  # noqa: E402
-from grace_amd.dist.compressor.signsgd import SignSGDCompressor  # noqa: E402
-from grace_amd.dist.memory.none import NoneMemory  # noqa: E402
+import bench  # noqa: E402
 
-dev = torch.device("cuda", 0)
-n = 1 << 20
-xs = [torch.randn(n, device=dev) for _ in range(64)]
-out = torch.empty(n, device=dev)
-comm = Allgather(SignSGDCompressor(), NoneMemory(), 1)
-N = 2000
+_timed = bench.timed
+_host = {}
 
 
-def host_us(fn):
-    for i in range(50):
-        fn(i)
+def timed(fn, steps, warmup, world, dev):
+    elapsed = _timed(fn, steps, warmup, world, dev)
+    n = min(steps, 100)
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    for i in range(N):
+    torch.cuda._sleep(int(2e8))            # ~100 ms of device time ahead of the steps
+    t0 = time.perf_counter()
+    for i in range(n):
         fn(i)
-    h = (time.perf_counter() - t) / N * 1e6
+    host = time.perf_counter() - t0
     torch.cuda.synchronize()
-    wall = (time.perf_counter() - t) / N * 1e6
-    return round(h, 2), round(wall, 2)
+    _host["us"] = host / n * 1e6
+    return elapsed
 
 
-s = ops._stream()
-res = {
-    "raw_call": host_us(lambda i: _lib.call("grace_sign_step_w1", xs[i % 64].data_ptr(), None, out.data_ptr(), n, s)),
-    "raw_call+stream": host_us(lambda i: _lib.call("grace_sign_step_w1", xs[i % 64].data_ptr(), None, out.data_ptr(), n,
-                                                   ops._stream())),
-    "empty_like": host_us(lambda i: torch.empty_like(xs[0])),
-    "ops.sign_step_w1": host_us(lambda i: ops.sign_step_w1(xs[i % 64], want_codes=False, reuse_out=True)),
-    "comm.step": host_us(lambda i: comm.step(xs[i % 64], "w")),
-}
-print(res)
+bench.timed = timed
+for wl in sys.argv[1:]:
+    steps = "200" if wl not in ("topk", "topk_sharded", "sign256") else "20"
+    sys.argv = ["bench.py", "--workload", wl, "--steps", steps, "--no-cpu-baseline"]
+    bench.main()
+    print(f"HOST {wl}: {_host.get('us', float('nan')):.1f} us per step submitted", flush=True)
