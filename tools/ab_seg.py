@@ -18,6 +18,8 @@ n = sum(sizes)
 gs = [torch.randn(n, device=dev) for _ in range(3)]
 variants = {"carry": (8192, "index", True), "no_carry": (8192, "index", False),
             "carry_size_order": (8192, "size", True)}
+if os.environ.get("AB_SEG_SMALL"):   # small-segment limit A/B (must stay <= the kernel's 8192)
+    variants = {f"small{v}": (int(v), "index", True) for v in os.environ["AB_SEG_SMALL"].split(",")}
 engs = {}
 for name, (sm, order, carry) in variants.items():
     e = SegmentedTopK(0.01)
