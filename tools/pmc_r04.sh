@@ -26,4 +26,4 @@ for wl in ${PMC_WL:-qsgd terngrad powersgd sign256 qsgd_step terngrad_step}; do
   args="$args $wl=gpurun_out/pmc_r04_${wl}_FETCH_SIZE,gpurun_out/pmc_r04_${wl}_WRITE_SIZE"
 done
 # first-step variants (no residual yet) are not the steady-state step
-python3 tools/pmc_all.py gpurun_out/r04_pmc_secondary.json --last 3 --exclude "threshold:<1>" --exclude "randomk:<false>" --exclude "dgc:spec_kernel<false>" $args
+python3 tools/pmc_all.py gpurun_out/r04_pmc_secondary.json --last 3 --exclude "threshold:<1>" --exclude "randomk:<false>" --exclude "dgc:spec_kernel<false>" --exclude "ddp_segmented:seg_main_kernel<false|seg_prep_kernel<false" --exclude "topk_sharded:topk_main<false|topk_bracket<false|stream_kernel" $args
