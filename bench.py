@@ -165,7 +165,7 @@ def nested_sharded(line, args, world, rank, dev):
             print(json.dumps(line), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)   # non-zero: a hung leg must not read as success (the DP line is printed already)
 
     dog = threading.Timer(limit, expire)
     dog.daemon = True
@@ -182,7 +182,8 @@ def nested_sharded(line, args, world, rank, dev):
     dog.cancel()
     if float(flag.item()) > 0:
         return {"error": err or "failed on another rank"}
-    return {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config", "roofline")}
+    return {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config", "roofline",
+                                     "shard_decode")}
 
 
 # GRACE_BENCH_NO_PROBE=1: skip the in-bench HBM probes (profiling passes, whose per-dispatch
@@ -647,6 +648,19 @@ def bench_topk_sharded(args, world, rank, dev):
                         "algorithmic_bytes_per_gpu": per_gpu, "survey_bytes_per_gpu": survey,
                         "output": "recycled" if recycled else "dense zero-fill",
                         "recycled_steps": eng._recycler.hits}
+    # SURVEY §8e's sharded-decode mode beside it: every rank materialises only its own n/W slice of
+    # the decoded bucket (reduce-scatter semantics), same selection, same single collective
+    eng_s = ShardedTopK(ratio, dense="shard")
+    for j in range(args.buffers):
+        eng_s.step(shards[j], f"s{j}")
+    el_s = timed(lambda i: eng_s.step(shards[i % args.buffers], f"s{i % args.buffers}"), args.steps, args.warmup,
+                 world, dev)
+    t_s = el_s / args.steps
+    per_gpu_s = 12.0 * m + 8.0 * k + 4.0 * m          # shard encode + the own slice of the decode
+    line["shard_decode"] = {"value": round(4.0 * n / t_s / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t_s * 1e3, 4),
+                            "frac": round(per_gpu_s / t_s / 1e9 / HBM_PEAK_GBS, 4),
+                            "algorithmic_bytes_per_gpu": per_gpu_s,
+                            "note": "ShardedTopK(dense='shard'): each rank decodes only its own slice"}
     return line
 
 

@@ -24,6 +24,8 @@ SIGNATURES = {
     "grace_last_error": (ctypes.c_char_p, []),
     "grace_read_status": (ST, [P, P, P]),
     "grace_status_take": (ctypes.c_int32, [P]),
+    "grace_topk_status_word": (ST, [P]),
+    "grace_topk_fallback_spin_limit": (ctypes.c_int64, [ctypes.c_int64]),
     "grace_topk_stream_probe_workspace_bytes": (SZ, [I64]),
     "grace_topk_stream_probe": (ST, [P, P, P, I64, I32, P, SZ, P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
@@ -59,7 +61,8 @@ SIGNATURES = {
     "grace_topk_segmented_seg_ws_bytes": (I64, [I64, I64]),
     "grace_topk_segmented_fin_blocks": (I32, [I64, I64]),
     "grace_topk_segmented_step": (ST, [P, P, I32, F32, F32, P, P, P, I32, P, I32, P, P, I64, P, P, P, I64, I64, P, P, P,
-                                       P, P, I32, P, SZ, P]),
+                                       P, P, I32, P, SZ, I64, P]),
+    "grace_topk_segmented_workspace_bytes": (I64, [P, P, I32]),
     "grace_topk_segmented_carry_len": (I64, [I64]),
     "grace_shard_record_words": (SZ, [I64]),
     "grace_shard_select_workspace_bytes": (SZ, [I32, I64]),

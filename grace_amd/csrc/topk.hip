@@ -95,7 +95,7 @@ struct TopkCtl {
   uint32_t thr_lo;
   uint32_t thr_hi;
   uint32_t shift;
-  int32_t status;      // 0 fast path, 1 exact fallback
+  int32_t status;      // 0 fast path, 1 exact fallback, 2 a parallel-fallback wait ran out (aborted)
   uint32_t n_sure;
   uint32_t n_cand;
   uint32_t n_sel;
@@ -105,8 +105,8 @@ struct TopkCtl {
   uint32_t ticket;     // finalize kernel arrival counter
   uint32_t n_bacc;     // boundary-list fill counter
   uint32_t bticket;    // bracket kernel arrival counter (reset by its last workgroup)
-  uint32_t bar_count;  // finalize grid barrier (parallel exact fallback): arrivals
-  uint32_t bar_gen;    //   and generation
+  uint32_t pad0;       // (unused; the parallel fallback's counters live in TopkWs::fb)
+  uint32_t pad1;
   uint32_t thr_mid;    // provisional selection threshold of the fused main pass (key > thr_mid)
 };
 static_assert(sizeof(TopkCtl) == 64, "ctl layout");
@@ -155,6 +155,9 @@ struct TopkWs {
   int2* cand;
   int2* bnd;
   int64_t cap;
+  uint32_t* fb;        // parallel exact fallback scratch [kFbWords] (zero between uses)
+  int32_t* hstatus;    // registered pinned host status word (grace_topk_status_word) or null
+  uint32_t spin_max;   // bound of every parallel-fallback wait, in polls (grace_topk_fallback_spin_limit)
 };
 
 static inline int64_t topk_cap(int64_t n, int64_t k) {
@@ -164,12 +167,22 @@ static inline int64_t topk_cap(int64_t n, int64_t k) {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// parallel exact fallback scratch (see parallel_exact): tickets, counters, histograms, slice counts
+constexpr int kFbWordsHost = 64 + 3 * 2048 + 2 * 1024;
+// the host word every top-k launch reports a run-out to, and the bound of the fallback's waits
+static int32_t* g_topk_hstatus = nullptr;
+static uint32_t g_fb_spin_max = 1u << 22;
+
 static TopkWs carve(void* ws, int64_t n, int64_t k) {
   char* p = reinterpret_cast<char*>(ws);
   TopkWs w;
   w.cap = topk_cap(n, k);
   w.ctl = reinterpret_cast<TopkCtl*>(p);
   p += 256;
+  // right after ctl, at the same address for every (n, k): the workspace is shared by calls of
+  // every shape, and the fallback's tickets and histograms must be zero wherever a call finds them
+  w.fb = reinterpret_cast<uint32_t*>(p);
+  p += align256(sizeof(uint32_t) * kFbWordsHost);
   w.hist = reinterpret_cast<uint32_t*>(p);
   p += align256(sizeof(uint32_t) * kHistBins * kHistStride);
   w.chist = reinterpret_cast<uint32_t*>(p);
@@ -179,6 +192,8 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   w.cand = reinterpret_cast<int2*>(p);
   p += align256(sizeof(int2) * w.cap);
   w.bnd = reinterpret_cast<int2*>(p);
+  w.hstatus = g_topk_hstatus;
+  w.spin_max = g_fb_spin_max;
   return w;
 }
 
@@ -186,7 +201,7 @@ static size_t ws_bytes(int64_t n, int64_t k) {
   const int64_t cap = topk_cap(n, k);
   return 256 + align256(sizeof(uint32_t) * kHistBins * kHistStride) +
          align256(sizeof(uint32_t) * kCoarseBins) + align256(sizeof(uint32_t) * kBracketBins) +
-         2 * align256(sizeof(int2) * cap);
+         2 * align256(sizeof(int2) * cap) + align256(sizeof(uint32_t) * kFbWordsHost);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -268,7 +283,7 @@ struct StepArgs {
   float* out;          // dense output (kDenseFused, kDenseOut)
   int64_t sample_n;    // stratified sample size (<= kSampleMax)
   int64_t stratum;     // n / sample_n
-  // residual-sample carry (grace_topk_residual_step_carry), f32[sample_n + 2]: the bracket writes
+  // residual-sample carry (grace_topk_residual_step_carry), f32[carry_thr_off(sample_n) + 2]: the bracket writes
   // the step's t[pos(s)] to rs_out[s] (it computes them anyway), the finalize writes the step's
   // composite selection threshold (selected <=> comp_key >= T) as a u64 at rs_out + sample_n;
   // rs_in = the previous step's rs_out for this residual: the next bracket derives r'[pos(s)] from
@@ -288,6 +303,9 @@ struct StepArgs {
 
 // the carry is for large buckets, where the bracket's random reads cost (stratum >= 256)
 constexpr int64_t kCarryMinStratum = 256;
+// word offset of the carry's u64 threshold after S sample words: 8-B aligned for any S (a segment's
+// sample count n / 256 can be odd)
+__host__ __device__ __forceinline__ int64_t carry_thr_off(int64_t S) { return (S + 1) & ~(int64_t)1; }
 
 template <bool HAS_RES>
 __device__ __forceinline__ float compensate(const StepArgs& a, int64_t i) {
@@ -462,7 +480,7 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
         // r'(pos) exactly as its main pass + finalize left it, from one random DRAM read (g) per
         // sample instead of two
         const float tp = a.rs_in[sidx];
-        const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + a.sample_n);
+        const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + carry_thr_off(a.sample_n));
         const float gv = a.g[pos];
         const float rp = comp_key(abs_key(tp), (uint32_t)pos) >= Tp ? tp - tp : tp;
         t[0] = a.beta * rp + a.gamma * gv;
@@ -884,7 +902,7 @@ struct FinShared {
   int2 s_ent[kPairCap];
   uint32_t s_res[2];
   int s_B;
-  uint32_t s_need, s_pos, s_last;
+  uint32_t s_need, s_pos, s_last, s_claim;
 };
 
 template <bool AG>
@@ -929,7 +947,7 @@ struct MainTs {
 
 // the step's composite selection threshold into the residual-sample carry (selected <=> comp >= T)
 __device__ __forceinline__ void carry_threshold(const StepArgs& a, uint64_t T) {
-  if (a.rs_out) *reinterpret_cast<uint64_t*>(a.rs_out + a.sample_n) = T;
+  if (a.rs_out) *reinterpret_cast<uint64_t*>(a.rs_out + carry_thr_off(a.sample_n)) = T;
 }
 
 // the boundary list into LDS (pairwise-ranking case); issued by the last workgroup BEFORE its own
@@ -1061,40 +1079,65 @@ __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[k
 }
 
 // ---- parallel exact fallback (the sampled bracket missed or a list overflowed: in practice massive
-// ties, e.g. a bucket that is mostly exact zeros, or a constant one).  All finalize workgroups
-// (co-resident: 128 of them) radix-select the k-th largest KEY over the whole bucket together, one
-// digit per pass with a grid barrier after each global histogram merge (3 passes); the ties at that
-// key are then taken lowest index first straight from per-slice counts: a count pass and an
-// ordered write pass, each slice in index order after exclusive scans of the (key > T, key == T)
-// counts.  Five streaming passes over t by 64 workgroups instead of one workgroup's radix select
-// and ordered write.  Scratch: the start of the (already re-zeroed) fine sample histogram, zeroed
-// again at the end.
-template <int BLOCK>
-__device__ __forceinline__ void grid_barrier(const TopkWs& w, int fcnt) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t gen = __hip_atomic_load(&w.ctl->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (atomicAdd(&w.ctl->bar_count, 1u) == (uint32_t)fcnt - 1) {
-      __hip_atomic_store(&w.ctl->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&w.ctl->bar_gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      uint32_t spins = 0;
-      while (__hip_atomic_load(&w.ctl->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 26)) { w.ctl->status = 2; break; }   // bounded: never expected
-      }
-    }
-  }
-  __syncthreads();
+// ties, e.g. a bucket that is mostly exact zeros, or a constant one).  The finalize workgroups
+// radix-select the k-th largest KEY over the whole bucket together, one digit per phase (3 phases),
+// then take the ties at that key lowest index first from per-slice counts: a count phase and an
+// ordered write phase.  The bucket is cut into slices that the workgroups CLAIM one at a time
+// (a ticket per phase), and a phase ends when every slice of it is DONE (a second counter per
+// phase), not when every workgroup has arrived.  So a workgroup only ever waits for slices that a
+// running workgroup has claimed: the fallback needs no co-residency and cannot deadlock when other
+// kernels (another process, RCCL) hold CUs -- a workgroup that starts late finds the slices taken
+// and only follows the phases.  Every wait is still bounded (TopkWs::spin_max): a wait that runs out
+// aborts the fallback in every workgroup (no payload written past k) and reports it in ctl->status
+// (2) and in the registered pinned host word (grace_topk_status_word), which the Python layer turns
+// into TopKWaitError.  Scratch: the workspace's fallback region (kFbWords), zero on entry; the last
+// workgroup to leave re-zeroes what was accumulated.
+constexpr int kFbSlicesMax = 1024;
+constexpr int kFbSliceMin = 4096;
+// fallback scratch, uint32 words: claim tickets [0, 8), done counters [16, 24), the abort flag (32)
+// and the exit ticket (48) on 64-B lines of their own, then the three digit histograms and the
+// per-slice (key > T, key == T) counts
+constexpr int kFbClaim = 0, kFbDone = 16, kFbAbort = 32, kFbExit = 48, kFbHist = 64;
+constexpr int kFbCnt = kFbHist + 3 * 2048;
+constexpr int kFbWords = kFbCnt + 2 * kFbSlicesMax;
+static_assert(kFbWords == kFbWordsHost, "fallback scratch size");
+
+__device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int kFbUnroll = 8;   // parallel fallback: elements per thread per ordered-write round
-constexpr int kFbQ = 8;        // parallel fallback: quads in flight per thread (histogram / count passes)
+// one thread: stop the fallback everywhere and report it (device ctl and the host word)
+__device__ __forceinline__ void fb_abort(const TopkWs& w) {
+  __hip_atomic_store(w.fb + kFbAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(&w.ctl->status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (w.hstatus) __hip_atomic_fetch_or(w.hstatus, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
-// one key into the LDS histogram, wave-aggregated for the bin of the wave's first active lane:
-// degenerate buckets (ties: all zeros, a constant) put every key in one bin, and a workgroup's LDS
-// atomics on one address serialise (the loop exits can leave lanes inactive, hence the lead lane)
+// every thread of the workgroup: wait until phase p's done counter reaches `nsl` (sc1 polls of a
+// counter that only receives device atomics, after which the phase's data is read with sc1 loads).
+// false (for every thread) when the fallback was aborted, here or elsewhere.
+template <int BLOCK>
+__device__ bool fb_wait(const TopkWs& w, int p, uint32_t nsl, FinShared<BLOCK>& fs) {
+  if (threadIdx.x == 0) {
+    uint32_t ok = 1, spins = 0;
+    for (;;) {
+      asm volatile("" ::: "memory");
+      if (ld_agent_u32(w.fb + kFbDone + p) >= nsl) break;
+      if (ld_agent_u32(w.fb + kFbAbort)) { ok = 0; break; }
+      if (spins++ >= w.spin_max) { fb_abort(w); ok = 0; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    fs.s_res[0] = ok;
+  }
+  __syncthreads();
+  const bool ok = fs.s_res[0] != 0;
+  __syncthreads();
+  return ok;
+}
+
+// one wave-aggregated key into the LDS histogram, for the bin of the wave's first active lane:
+// degenerate buckets (ties: all zeros, a constant) put every key of a wave in one bin, and a
+// workgroup's LDS atomics on one address serialise (loop exits can leave lanes inactive)
 __device__ __forceinline__ void hist_add_agg(uint32_t* hist, int bin) {
   const int b0 = __builtin_amdgcn_readfirstlane(bin);
   const uint64_t same = __ballot(bin == b0);
@@ -1103,24 +1146,32 @@ __device__ __forceinline__ void hist_add_agg(uint32_t* hist, int bin) {
   if (b0 >= 0 && (int)(threadIdx.x & 63) == lead) atomicAdd(&hist[b0], (uint32_t)__popcll(same));
 }
 
+constexpr int kFbUnroll = 8;   // parallel fallback: elements per thread per ordered-write round
+constexpr int kFbQ = 8;        // parallel fallback: quads in flight per thread (histogram / count passes)
+
 template <int MODE, int BLOCK, bool AG>
-__device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs) {
+__device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fcnt, FinShared<BLOCK>& fs) {
   const int t = threadIdx.x;
   const uint32_t k = (uint32_t)a.k;
+  uint32_t* fb = w.fb;
   // slices of whole quads (16-B loads) when the buffers are 16-B aligned; [q1, s1) is a scalar tail
   const bool vq = !AG && ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r) |
                            reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
-  int64_t per = (a.n + fcnt - 1) / fcnt;
-  if (vq) per = (per + 3) & ~(int64_t)3;
-  const int64_t s0 = min((int64_t)fi * per, a.n), s1 = min(s0 + per, a.n);
-  const int64_t q1 = vq ? s0 + ((s1 - s0) & ~(int64_t)3) : s0;
-  uint32_t* gh = w.shist;                      // [3][2048] key-digit histograms
-  uint32_t* cnt = w.shist + 3 * 2048;          // [fcnt][2] per-slice (key > T, key == T) counts
-  if (fi == 0 && t == 0) w.ctl->status = 1;
+  int64_t L = (a.n + kFbSlicesMax - 1) / kFbSlicesMax;
+  L = L < kFbSliceMin ? kFbSliceMin : ((L + 3) & ~(int64_t)3);
+  const uint32_t nsl = (uint32_t)((a.n + L - 1) / L);
+  if (t == 0) __hip_atomic_fetch_max(&w.ctl->status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const MainTs<MODE, AG> f{a.g, a.r, a.out};
-  // fn(key) for every element of the slice, in no particular order; every load of a round issued
-  // before any key is used
-  auto for_keys = [&](auto&& fn) {
+  auto bounds = [&](uint32_t s, int64_t& s0, int64_t& q1, int64_t& s1) {
+    s0 = (int64_t)s * L;
+    s1 = s0 + L < a.n ? s0 + L : a.n;
+    q1 = vq ? s0 + ((s1 - s0) & ~(int64_t)3) : s0;
+  };
+  // fn(key, in) for every element of slice s, in no particular order; every load of a round
+  // issued before any key is used
+  auto for_keys = [&](uint32_t s, auto&& fn) {
+    int64_t s0, q1, s1;
+    bounds(s, s0, q1, s1);
     for (int64_t b = s0 + 4 * (int64_t)t; b < q1; b += 4 * (int64_t)BLOCK * kFbQ) {
       float4 v[kFbQ];
 #pragma unroll
@@ -1136,23 +1187,52 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     }
     for (int64_t i = q1 + t; i < s1; i += BLOCK) fn(abs_key(f(i)), true);
   };
-  grid_barrier<BLOCK>(w, fcnt);                // every workgroup is past its histogram zeroing
+  // runs body(s) for every slice of phase p this workgroup claims; the next claim is issued before
+  // the current slice's work (its ticket latency hides behind the loads); returns the slice count
+  auto claim_loop = [&](int p, auto&& body) -> uint32_t {
+    if (t == 0) fs.s_claim = atomicAdd(fb + kFbClaim + p, 1u);
+    __syncthreads();
+    uint32_t s = fs.s_claim, mine = 0;
+    __syncthreads();
+    while (s < nsl) {
+      uint32_t nxt = 0;
+      if (t == 0) nxt = atomicAdd(fb + kFbClaim + p, 1u);
+      body(s);
+      ++mine;
+      if (t == 0) fs.s_claim = nxt;
+      __syncthreads();
+      s = fs.s_claim;
+      __syncthreads();
+    }
+    return mine;
+  };
+  // this workgroup's slices of phase p are complete: its stores / atomics performed, then one add
+  auto done = [&](int p, uint32_t mine) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0 && mine) atomicAdd(fb + kFbDone + p, mine);
+  };
+  bool ok = true;
   // 1. the exact k-th largest key T (31-bit keys: digits of 11, 11 and 9 bits)
   uint32_t prefix = 0, pmask = 0, rem = k;
-  for (int p = 0; p < 3; ++p) {
+  for (int p = 0; p < 3 && ok; ++p) {
     const int shift = p == 0 ? 20 : (p == 1 ? 9 : 0);
     const uint32_t dmask = p < 2 ? 2047u : 511u;
     for (int b = t; b < 2048; b += BLOCK) fs.hist[b] = 0;
     __syncthreads();
-    for_keys([&](uint32_t key, bool in) {
-      hist_add_agg(fs.hist, in && (key & pmask) == prefix ? (int)((key >> shift) & dmask) : -1);
+    const uint32_t mine = claim_loop(p, [&](uint32_t s) {
+      for_keys(s, [&](uint32_t key, bool in) {
+        hist_add_agg(fs.hist, in && (key & pmask) == prefix ? (int)((key >> shift) & dmask) : -1);
+      });
     });
     __syncthreads();
-    for (int b = t; b < 2048; b += BLOCK)
-      if (fs.hist[b]) atomicAdd(&gh[p * 2048 + b], fs.hist[b]);
-    grid_barrier<BLOCK>(w, fcnt);
-    for (int b = t; b < 2048; b += BLOCK)
-      fs.hist[b] = __hip_atomic_load(&gh[p * 2048 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mine)
+      for (int b = t; b < 2048; b += BLOCK)
+        if (fs.hist[b]) atomicAdd(fb + kFbHist + p * 2048 + b, fs.hist[b]);
+    done(p, mine);
+    ok = fb_wait<BLOCK>(w, p, nsl, fs);
+    if (!ok) break;
+    for (int b = t; b < 2048; b += BLOCK) fs.hist[b] = ld_agent_u32(fb + kFbHist + p * 2048 + b);
     __syncthreads();
     uint32_t above;
     const int d = find_bin_desc<BLOCK, 2048>(fs.hist, rem, fs.s_w, fs.s_res, &above);
@@ -1161,103 +1241,125 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fi, int f
     pmask |= dmask << shift;
   }
   const uint32_t T = prefix, need_eq = rem;    // take every key > T and the need_eq lowest-index == T
-  if (need_eq == 0 && fi == 0 && t == 0) carry_threshold(a, ((uint64_t)T + 1) << 32);
   // 2. per-slice counts
-  uint32_t ngt = 0, neq = 0;
-  for_keys([&](uint32_t key, bool in) {
-    ngt += in && key > T;
-    neq += in && key == T;
-  });
-  uint32_t tgt, teq;
-  block_excl_scan<BLOCK>(ngt, fs.s_w, &tgt);
-  block_excl_scan<BLOCK>(neq, fs.s_w, &teq);
-  if (t == 0) {
-    __hip_atomic_store(&cnt[2 * fi], tgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&cnt[2 * fi + 1], teq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  grid_barrier<BLOCK>(w, fcnt);
-  uint32_t gt_run = 0, eq_run = 0;             // before this slice
-  for (int j = 0; j < fi; ++j) {
-    gt_run += __hip_atomic_load(&cnt[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    eq_run += __hip_atomic_load(&cnt[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 3. the slice in index order: selected-before = (# key > T before) + min(# key == T before, need_eq);
-  //    each thread owns kFbUnroll consecutive elements of a round (two quads when whole), one block
-  //    scan per round; r' and the dense output leave as 16-B stores for whole quads
-  static_assert(kFbUnroll == 8, "two quads per thread per round");
-  for (int64_t j0 = s0; j0 < s1; j0 += (int64_t)BLOCK * kFbUnroll) {
-    const int64_t ib = j0 + (int64_t)t * kFbUnroll;
-    const bool whole = ib + kFbUnroll <= q1;
-    float v[kFbUnroll];
-    if (whole) {
-      const float4 x0 = f.quad(ib), x1 = f.quad(ib + 4);
-      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    } else {
-#pragma unroll
-      for (int u = 0; u < kFbUnroll; ++u) v[u] = f(ib + u < s1 ? ib + u : s0);
-    }
-    uint32_t cg = 0, ce = 0;
-#pragma unroll
-    for (int u = 0; u < kFbUnroll; ++u) {
-      const uint32_t key = abs_key(v[u]);
-      cg += ib + u < s1 && key > T;
-      ce += ib + u < s1 && key == T;
-    }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<BLOCK>(cg | (ce << 16), fs.s_w, &tot);
-    uint32_t g_before = gt_run + (ex & 0xFFFFu), e_before = eq_run + (ex >> 16);
-    float rv[kFbUnroll], ov[kFbUnroll];
-#pragma unroll
-    for (int u = 0; u < kFbUnroll; ++u) {
-      const int64_t i = ib + u;
-      rv[u] = v[u];
-      ov[u] = 0.f;
-      if (i < s1) {
-        const uint32_t key = abs_key(v[u]);
-        const bool gt = key > T, eq = key == T;
-        if (gt || (eq && e_before < need_eq)) {
-          if (eq && e_before == need_eq - 1) carry_threshold(a, comp_key(T, (uint32_t)i));   // the last tie taken
-          const uint32_t pos = g_before + min(e_before, need_eq);
-          a.vals[pos] = v[u];
-          a.idx[pos] = (int32_t)(i + a.idx_base);
-          rv[u] = v[u] - v[u];
-          ov[u] = 0.f + v[u];   // (0 + d) of the Python sum
-        }
-        g_before += gt;
-        e_before += eq;
+  if (ok) {
+    const uint32_t mine = claim_loop(3, [&](uint32_t s) {
+      uint32_t ngt = 0, neq = 0;
+      for_keys(s, [&](uint32_t key, bool in) {
+        ngt += in && key > T;
+        neq += in && key == T;
+      });
+      uint32_t tgt, teq;
+      block_excl_scan<BLOCK>(ngt, fs.s_w, &tgt);
+      block_excl_scan<BLOCK>(neq, fs.s_w, &teq);
+      if (t == 0) {
+        __hip_atomic_store(fb + kFbCnt + 2 * s, tgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fb + kFbCnt + 2 * s + 1, teq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-    if constexpr (MODE != kDenseNone) {
-      if (whole) {
-        if constexpr (kWritesR<MODE>) {
-          *reinterpret_cast<float4*>(a.r + ib) = make_float4(rv[0], rv[1], rv[2], rv[3]);
-          *reinterpret_cast<float4*>(a.r + ib + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
+    });
+    done(3, mine);
+    ok = fb_wait<BLOCK>(w, 3, nsl, fs);
+  }
+  // 3. each slice in index order: selected-before = (# key > T before) + min(# key == T before,
+  //    need_eq); each thread owns kFbUnroll consecutive elements of a round (two quads when whole),
+  //    one block scan per round; r' and the dense output leave as 16-B stores for whole quads
+  static_assert(kFbUnroll == 8, "two quads per thread per round");
+  if (ok) {
+    claim_loop(4, [&](uint32_t s) {
+      if (s == 0 && t == 0 && need_eq == 0) carry_threshold(a, ((uint64_t)T + 1) << 32);
+      uint32_t pg = 0, pe = 0;                 // counts of the slices before s
+      for (uint32_t j = t; j < s; j += BLOCK) {
+        pg += ld_agent_u32(fb + kFbCnt + 2 * j);
+        pe += ld_agent_u32(fb + kFbCnt + 2 * j + 1);
+      }
+      uint32_t gt_run, eq_run;
+      block_excl_scan<BLOCK>(pg, fs.s_w, &gt_run);
+      block_excl_scan<BLOCK>(pe, fs.s_w, &eq_run);
+      int64_t s0, q1, s1;
+      bounds(s, s0, q1, s1);
+      for (int64_t j0 = s0; j0 < s1; j0 += (int64_t)BLOCK * kFbUnroll) {
+        const int64_t ib = j0 + (int64_t)t * kFbUnroll;
+        const bool whole = ib + kFbUnroll <= q1;
+        float v[kFbUnroll];
+        if (whole) {
+          const float4 x0 = f.quad(ib), x1 = f.quad(ib + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        } else {
+#pragma unroll
+          for (int u = 0; u < kFbUnroll; ++u) v[u] = f(ib + u < s1 ? ib + u : s0);
         }
-        if constexpr (kWritesOut<MODE>) {
-          *reinterpret_cast<float4*>(a.out + ib) = make_float4(ov[0], ov[1], ov[2], ov[3]);
-          *reinterpret_cast<float4*>(a.out + ib + 4) = make_float4(ov[4], ov[5], ov[6], ov[7]);
-        }
-      } else {
+        uint32_t cg = 0, ce = 0;
 #pragma unroll
         for (int u = 0; u < kFbUnroll; ++u) {
-          if (ib + u < s1) {
-            if constexpr (kWritesR<MODE>) a.r[ib + u] = rv[u];
-            if constexpr (kWritesOut<MODE>) a.out[ib + u] = ov[u];
+          const uint32_t key = abs_key(v[u]);
+          cg += ib + u < s1 && key > T;
+          ce += ib + u < s1 && key == T;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<BLOCK>(cg | (ce << 16), fs.s_w, &tot);
+        uint32_t g_before = gt_run + (ex & 0xFFFFu), e_before = eq_run + (ex >> 16);
+        float rv[kFbUnroll], ov[kFbUnroll];
+#pragma unroll
+        for (int u = 0; u < kFbUnroll; ++u) {
+          const int64_t i = ib + u;
+          rv[u] = v[u];
+          ov[u] = 0.f;
+          if (i < s1) {
+            const uint32_t key = abs_key(v[u]);
+            const bool gt = key > T, eq = key == T;
+            if (gt || (eq && e_before < need_eq)) {
+              if (eq && e_before == need_eq - 1) carry_threshold(a, comp_key(T, (uint32_t)i));   // the last tie taken
+              const uint32_t pos = g_before + min(e_before, need_eq);
+              if (pos < k) {   // always, unless the counts were corrupted
+                a.vals[pos] = v[u];
+                a.idx[pos] = (int32_t)(i + a.idx_base);
+              }
+              rv[u] = v[u] - v[u];
+              ov[u] = 0.f + v[u];   // (0 + d) of the Python sum
+            }
+            g_before += gt;
+            e_before += eq;
           }
         }
+        if constexpr (MODE != kDenseNone) {
+          if (whole) {
+            if constexpr (kWritesR<MODE>) {
+              *reinterpret_cast<float4*>(a.r + ib) = make_float4(rv[0], rv[1], rv[2], rv[3]);
+              *reinterpret_cast<float4*>(a.r + ib + 4) = make_float4(rv[4], rv[5], rv[6], rv[7]);
+            }
+            if constexpr (kWritesOut<MODE>) {
+              *reinterpret_cast<float4*>(a.out + ib) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+              *reinterpret_cast<float4*>(a.out + ib + 4) = make_float4(ov[4], ov[5], ov[6], ov[7]);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < kFbUnroll; ++u) {
+              if (ib + u < s1) {
+                if constexpr (kWritesR<MODE>) a.r[ib + u] = rv[u];
+                if constexpr (kWritesOut<MODE>) a.out[ib + u] = ov[u];
+              }
+            }
+          }
+        }
+        gt_run += tot & 0xFFFFu;
+        eq_run += tot >> 16;
       }
-    }
-    gt_run += tot & 0xFFFFu;
-    eq_run += tot >> 16;
+    });
   }
-  grid_barrier<BLOCK>(w, fcnt);                // every slice has read the scratch
-  for (int z = fi * BLOCK + t; z < 3 * 2048 + 2 * fcnt; z += fcnt * BLOCK) gh[z] = 0u;
+  // leave: the last workgroup out (every other one is past its last access to the scratch) re-zeroes
+  // the tickets, counters, flags and histograms (the per-slice counts are rewritten before any read)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) fs.s_last = atomicAdd(fb + kFbExit, 1u) == (uint32_t)fcnt - 1;
+  __syncthreads();
+  if (fs.s_last)
+    for (int z = t; z < kFbCnt; z += BLOCK) __hip_atomic_store(fb + z, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // finalize workgroup `fi` of `fcnt`; returns true in the workgroup that ran the boundary step
 template <int MODE, int BLOCK, bool AG>
 __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcnt, FinShared<BLOCK>& fs,
-                             bool coresident) {
+                             bool parallel) {
   constexpr int PER = kHistBins / BLOCK;
   const int t = threadIdx.x;
   const uint32_t n_sure = ld_u32<AG>(&w.ctl->n_sure), n_cand = ld_u32<AG>(&w.ctl->n_cand);
@@ -1278,11 +1380,11 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
       else __builtin_amdgcn_raw_buffer_store_b128(zero, rc, (z - kBracketBins / 4) * 16, 0, 16);
     }
   }
-  // every finalize workgroup: the parallel fallback -- only when the launch checked that all of
-  // them are resident at once (its grid barriers spin); otherwise the last workgroup alone runs
-  // the single-workgroup exact select below (same result, slower)
-  if (!ok && coresident && fcnt > 1 && fcnt <= kFinBlocks) {
-    parallel_exact<MODE, BLOCK, AG>(a, w, fi, fcnt, fs);
+  // every finalize workgroup: the parallel fallback (slices claimed, so no co-residency needed);
+  // a caller without its scratch (segmented: per-tensor workspaces) lets the last workgroup alone
+  // run the single-workgroup exact select below (same result, slower)
+  if (!ok && parallel && fcnt > 1) {
+    parallel_exact<MODE, BLOCK, AG>(a, w, fcnt, fs);
     return fi == 0;
   }
   int B = -1;
@@ -1398,31 +1500,10 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w, int coresident) {
+__global__ __launch_bounds__(kSelBlock) void topk_finalize(StepArgs a, TopkWs w) {
   __shared__ FinShared<kSelBlock> fs;
   STAMP(w.ctl, 8);
-  finalize_run<MODE, kSelBlock, false>(a, w, blockIdx.x, gridDim.x, fs, coresident != 0);
-}
-
-// Whether all kFinBlocks finalize workgroups are resident at once on this device (the parallel
-// exact fallback's grid barriers need it): the occupancy API's blocks per CU times the CU count,
-// with a 2x margin (the guide's occupancy caveats: the API can be one block per CU high).  Cached
-// per device; the plain launch itself never checks residency.
-template <int MODE>
-static int finalize_coresident() {
-  static int cached[64];
-  static bool init[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!init[dev]) {
-    int per_cu = 0, cus = 0;
-    const bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, topk_finalize<MODE>, kSelBlock, 0) ==
-                        hipSuccess &&
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
-    cached[dev] = ok && (int64_t)per_cu * cus >= 2 * (int64_t)kFinBlocks ? 1 : 0;
-    init[dev] = true;
-  }
-  return cached[dev];
+  finalize_run<MODE, kSelBlock, false>(a, w, blockIdx.x, gridDim.x, fs, true);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1509,7 +1590,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
     launch_timed(topk_main<HAS_RES, MODE, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
   }
   GRACE_CHECK_LAUNCH("topk_main");
-  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w, finalize_coresident<MODE>());
+  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_finalize");
   return GRACE_OK;
 }
@@ -1754,7 +1835,7 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
       // the segment's carried t'(pos) and threshold: r'(pos) as the last step left it, and one
       // random read (g) per sample instead of two (the headline bracket's carry, per segment)
       const float tp = a.rs_in[sc];
-      const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + S);
+      const uint64_t Tp = *reinterpret_cast<const uint64_t*>(a.rs_in + carry_thr_off(S));
       const float rp = comp_key(abs_key(tp), (uint32_t)pos) >= Tp ? tp - tp : tp;
       t[q] = a.beta * rp + a.gamma * a.g[pos];
     } else {
@@ -1898,6 +1979,17 @@ int32_t grace_status_take(int32_t* host_word) {
   return host_word ? __atomic_exchange_n(host_word, 0, __ATOMIC_SEQ_CST) : 0;
 }
 
+grace_status_t grace_topk_status_word(int32_t* host_word) {
+  g_topk_hstatus = host_word;
+  return GRACE_OK;
+}
+
+int64_t grace_topk_fallback_spin_limit(int64_t limit) {
+  const int64_t prev = g_fb_spin_max;
+  if (limit >= 0) g_fb_spin_max = limit > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)limit;
+  return prev;
+}
+
 grace_status_t grace_timer_enable(int enable) {
   if (enable && !g_ev_created) {
     for (int i = 0; i < 2 * kMaxEv; ++i) {
@@ -2013,7 +2105,7 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
 int64_t grace_topk_carry_size(int64_t n, int64_t k) {
   if (n <= kSmallN || k >= n || n >= (int64_t)1 << 31) return 0;   // no sampled bracket on these paths
   const int64_t sn = n < kSampleMax ? n : kSampleMax;
-  return n / sn >= kCarryMinStratum ? sn + 2 : 0;   // t at the sample positions + the u64 threshold
+  return n / sn >= kCarryMinStratum ? carry_thr_off(sn) + 2 : 0;   // t at the sample positions + the u64 threshold
 }
 
 grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, int32_t has_residual,
@@ -2123,7 +2215,7 @@ int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out) {
 int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k) { return seg_ws_bytes_one(n, k); }
 
 // f32 words of a large segment's carry: t at its sample positions + the u64 threshold
-int64_t grace_topk_segmented_carry_len(int64_t n) { return seg_sample_n(n) + 2; }
+int64_t grace_topk_segmented_carry_len(int64_t n) { return carry_thr_off(seg_sample_n(n)) + 2; }
 
 // finalize workgroups for a large segment: one round (kSelBlock * kFinPer candidates) each for the
 // ~2-3 k a segment's small-sample band holds, plus one.  4 k budgeted: at 2 k a second round per
@@ -2132,6 +2224,14 @@ int64_t grace_topk_segmented_carry_len(int64_t n) { return seg_sample_n(n) + 2; 
 #ifndef GRACE_SEG_FIN_MULT
 #define GRACE_SEG_FIN_MULT 4
 #endif
+int64_t grace_topk_segmented_workspace_bytes(const int64_t* sizes, const int64_t* ks, int32_t count) {
+  if (!sizes || !ks || count < 0) return -1;
+  int64_t total = 0;
+  for (int32_t i = 0; i < count; ++i)
+    total += (int64_t)align256((size_t)seg_ws_bytes_one(sizes[i] < 1 ? 1 : sizes[i], ks[i] < 1 ? 1 : ks[i]));
+  return total;
+}
+
 int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k) {
   const int64_t per = (int64_t)kSelBlock * kFinPer;
   int64_t c = GRACE_SEG_FIN_MULT * k < n ? GRACE_SEG_FIN_MULT * k : n;
@@ -2146,7 +2246,8 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
                                          int64_t nchunks, const int64_t* ws_off, const int64_t* fin_off,
                                          const int32_t* fin_li, int64_t nfin, int64_t n_total, float* vals,
                                          int32_t* idx, float* out, float* carry, const int64_t* carry_off,
-                                         int32_t carry_valid, void* ws, size_t ws_bytes, void* stream) {
+                                         int32_t carry_valid, void* ws, size_t ws_bytes, int64_t ws_need,
+                                         void* stream) {
   GRACE_REQUIRE(g && residual && seg_off && k_off && vals && idx && n_large >= 0 && n_small >= 0 &&
                     n_large + n_small >= 1 && n_total >= 1 && n_total < ((int64_t)1 << 31) &&
                     (n_large == 0 || (large && chk_off && chunk_li && ws_off && fin_off && fin_li && ws &&
@@ -2179,7 +2280,8 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
   p.carry = carry;
   p.carry_off = carry_off;
   p.carry_valid = carry && has_residual && carry_valid ? 1 : 0;
-  (void)ws_bytes;   // sized by the caller from grace_topk_segmented_seg_ws_bytes (checked in the host layer)
+  GRACE_REQUIRE(n_large == 0 || (ws_need > 0 && ws_bytes >= (size_t)ws_need),
+                "grace_topk_segmented_step: workspace smaller than grace_topk_segmented_workspace_bytes");
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(residual) |
                      reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   hipStream_t s = as_stream(stream);

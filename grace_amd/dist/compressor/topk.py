@@ -18,10 +18,14 @@ from grace_amd.dist import Compressor
 
 class TopKCompressor(Compressor):
 
-    def __init__(self, compress_ratio, kernel='torch', recycle_output=True):
+    def __init__(self, compress_ratio, kernel='torch', recycle_output=True, check_sync=False):
         super().__init__()
         self.compress_ratio = compress_ratio
         self.kernel = kernel
+        # a run-out of the exact fallback's bounded waits (never expected) raises ops.TopKWaitError
+        # at the next top-k call; check_sync=True waits for the device after every compress / step
+        # and raises on the failing call itself
+        self.check_sync = check_sync
         # world-1 step WITHOUT memory: reuse a dropped, unmodified previous result of the same name
         # and rewrite only its non-zeros (ops.OutputRecycler; A/B r04: 0.1356 -> 0.1272 ms).  The
         # residual step keeps the dense write: next to its g, r, r' streams the scattered writes
@@ -34,6 +38,8 @@ class TopKCompressor(Compressor):
         flat = ops.dev_f32(tensor)
         k = ops.ratio_k(flat.numel(), self.compress_ratio)
         _, vals, idx = ops.topk_compress(flat, k)
+        if self.check_sync:
+            ops.topk_check()
         return [vals, idx], tensor.size()
 
     def decompress(self, tensors, ctx):
@@ -55,6 +61,12 @@ class TopKCompressor(Compressor):
     def fused_step(self, communicator, tensor, name):
         """compensate -> compress -> update -> send_receive for (TopK, Residual, Allgather) at any world
         size, and for (TopK, NoneMemory, Allgather) at world 1."""
+        out = self._fused_step(communicator, tensor, name)
+        if out is not None and self.check_sync:
+            ops.topk_check()
+        return out
+
+    def _fused_step(self, communicator, tensor, name):
         mem = communicator.memory
         if (isinstance(communicator, Allgather) and type(mem) is NoneMemory and int(communicator.world_size) == 1
                 and isinstance(tensor, torch.Tensor) and tensor.is_cuda and tensor.dtype == torch.float32):

@@ -86,6 +86,13 @@ class SegmentedTopK:
             ws_total += (int(_lib.query("grace_topk_segmented_seg_ws_bytes", n, k)) + 255) // 256 * 256
             carry_off.append(carry_total)
             carry_total += (int(_lib.query("grace_topk_segmented_carry_len", n)) + 3) // 4 * 4   # 16-B aligned
+        import ctypes
+        ln = (ctypes.c_int64 * max(1, len(large)))(*[sizes[i] for i in large])
+        lk = (ctypes.c_int64 * max(1, len(large)))(*[ks[i] for i in large])
+        ws_need = int(_lib.query("grace_topk_segmented_workspace_bytes", ctypes.addressof(ln), ctypes.addressof(lk),
+                                 len(large)))
+        if ws_need != ws_total:
+            raise RuntimeError(f"segmented workspace layout mismatch: {ws_need} != {ws_total}")
         t64 = lambda v: torch.tensor(v, dtype=torch.int64).to(device)   # noqa: E731
         t32 = lambda v: torch.tensor(v, dtype=torch.int32).to(device)   # noqa: E731
         ws = torch.zeros(max(ws_total, 256), dtype=torch.uint8, device=device)
@@ -94,7 +101,8 @@ class SegmentedTopK:
                "nchunks": chk[-1], "ws_off": t64(ws_off or [0]), "fin_off": t64(fin), "fin_li": t32(fin_li or [0]),
                "nfin": fin[-1], "ws": ws, "k_total": kk[-1], "n": seg[-1],
                "carry_off": t64(carry_off or [0]), "carry_len": max(carry_total, 4),
-               "carry_key": (sizes, small_max)}   # the carry layout depends on these only
+               "carry_key": (sizes, small_max),   # the carry layout depends on these only
+               "ws_need": ws_need}
         hit["args"] = (hit["seg_off"].data_ptr(), hit["k_off"].data_ptr(), hit["large"].data_ptr(), hit["n_large"],
                        hit["small"].data_ptr(), hit["n_small"], hit["chk_off"].data_ptr(), hit["chunk_li"].data_ptr(),
                        hit["nchunks"], hit["ws_off"].data_ptr(), hit["fin_off"].data_ptr(), hit["fin_li"].data_ptr(),
@@ -125,7 +133,7 @@ class SegmentedTopK:
                   *T["args"], vals.data_ptr(), idx.data_ptr(),
                   dense.data_ptr() if dense is not None else None,
                   carry.data_ptr() if carry is not None else None, T["carry_off"].data_ptr(), 1 if valid else 0,
-                  T["ws"].data_ptr(), T["ws"].numel(), ops._stream())
+                  T["ws"].data_ptr(), T["ws"].numel(), T["ws_need"], ops._stream())
         if carry is not None:   # written by this step (the kernels only use it with a residual)
             self._carries[name] = (carry, res, res._version, T["carry_key"])
         self.last_payload = (vals, idx)

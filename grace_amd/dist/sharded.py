@@ -24,7 +24,11 @@ there is no bracket-miss protocol and no capacity overflow.
 The partition (every rank's shard length) is agreed on a name's first step -- one all_gather and
 one host read, that step only.  Every record carries its shard length, and the select kernel
 checks it against the agreed table: a rank whose shard changes size later is reported on every
-rank by ``ShardPartitionError`` at the next step (never a hang, never a silent mix of partitions).
+rank by ``ShardPartitionError`` (never a hang, never a silent mix of partitions).  The kernels
+set the bit in a pinned word of this engine, one per step parity; step N + 2 waits for step N's
+select (an event: by then step N + 1 is queued, so the device never idles) and takes that word,
+so every rank raises at the same step N + 2 -- step N + 1's bits, which one rank may already see
+and another not, are in the other word.
 ``check_sizes=True`` instead agrees the partition at every step (one small all_gather and one host
 read per step), so a resize is handled in the step where it happens: every rank re-plans with the
 new sizes, a rank whose shard kept its size keeps its error feedback, a resized rank starts from
@@ -43,6 +47,10 @@ class ShardPartitionError(RuntimeError):
     """A rank's shard length differs from the partition agreed on the name's first step."""
 
 
+class ShardRecordError(ShardPartitionError):
+    """The gathered records hold fewer valid entries than k (status bit 2): a corrupt record."""
+
+
 class NativeShardKernels:
     """The HIP kernels behind each protocol step (GPU tensors only)."""
 
@@ -57,8 +65,8 @@ class NativeShardKernels:
     select = staticmethod(ops.shard_select)
     clear = staticmethod(ops.shard_clear)
 
-    def status(self, device):
-        return ops.shard_status(device)
+    def new_status(self, device):
+        return ops.new_status_word()
 
     def take_status(self, st):
         return ops.status_take(st)
@@ -125,6 +133,8 @@ class ShardedTopK:
         self.residuals = {}
         self._plans = {}
         self._side = {}
+        self._status = {}             # device -> (two pinned status words, their select events)
+        self._nstep = 0               # steps of this engine (all names): the status word parity
         self.last_payload = None      # (vals, idx) of this rank's record: idx = global index, or -1
         self.resizes = 0              # steps that found a rank's shard resized (check_sizes=True)
         self.host_reads = 0           # host synchronisations (first step of a name; every step with check_sizes)
@@ -150,27 +160,54 @@ class ShardedTopK:
             if plan is None or sizes != plan.sizes:
                 if plan is not None:
                     self.resizes += 1
+                    # the recycled output's selection was taken under the old partition (its base):
+                    # never clear through it
+                    self._recycler.drop(name)
                 plan = self._plans[name] = _Plan(self.k_ops, sizes, rank, self.compress_ratio, device)
         return plan
 
-    def _check_status(self, device):
-        st = self.k_ops.status(device)
-        bits = self.k_ops.take_status(st)
-        if bits:
+    def _slots(self, device):
+        key = str(device)
+        hit = self._status.get(key)
+        if hit is None:
+            hit = self._status[key] = ([self.k_ops.new_status(device) for _ in range(2)], [None, None])
+        return hit
+
+    def _raise_bits(self, bits):
+        if bits & 1:
             raise ShardPartitionError(
                 "grace_amd ShardedTopK: a rank's shard length changed after the name's first step (status "
-                f"{bits:#x}); the previous step mixed partitions.  Keep every rank's shard length fixed, or "
+                f"{bits:#x}); that step mixed partitions.  Keep every rank's shard length fixed, or "
                 "construct ShardedTopK(check_sizes=True) to re-agree the partition at every step")
-        return st
+        if bits & 2:
+            raise ShardRecordError(
+                f"grace_amd ShardedTopK: the gathered records held fewer valid entries than k (status {bits:#x}): "
+                "a record was corrupted in transit or written by a different build")
+
+    def _check_status(self, device):
+        """The word of this step's parity, after the select of two steps ago has finished (this
+        rank's event), so every rank reports a step's bits at the same later step."""
+        words, events = self._slots(device)
+        slot = self._nstep & 1
+        if events[slot] is not None:
+            events[slot].synchronize()
+            events[slot] = None
+        self._raise_bits(self.k_ops.take_status(words[slot]))
+        return words[slot], slot
 
     def check(self, device=None):
-        """Wait for the device and raise ShardPartitionError if any finished step mixed partitions
-        (the step itself never blocks: its status is otherwise checked when the next step starts)."""
+        """Wait for the device and raise if any finished step mixed partitions or saw corrupt records
+        (a step never blocks on its own status: it is checked two steps later)."""
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         if device.type == "cuda":
             torch.cuda.synchronize(device)
-        self._check_status(device)
+        words, events = self._slots(device)
+        bits = 0
+        for slot in range(2):
+            events[slot] = None
+            bits |= self.k_ops.take_status(words[slot])
+        self._raise_bits(bits)
 
     def _side_stream(self, device):
         cur = torch.cuda.current_stream(device)
@@ -207,7 +244,7 @@ class ShardedTopK:
         g = shard.reshape(-1)
         dev = g.device
         m = g.numel()
-        status = self._check_status(dev)
+        status, slot = self._check_status(dev)
         plan = self._plan(name, m, dev, world, rank)
         res = self.residuals.get(name)
         has_res = res is not None and res.numel() == m
@@ -243,5 +280,10 @@ class ShardedTopK:
         else:
             K.select(recs, world, rank, cap, plan.tab, plan.k, res, out, out_base, plan.pay_idx, status, sel)
             self._recycler.keep(name, out, sel)
+        if dev.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self._slots(dev)[1][slot] = ev
+        self._nstep += 1
         self.last_payload = (vals, plan.pay_idx)
         return out

@@ -148,6 +148,10 @@ class OutputRecycler:
         st = out.untyped_storage()
         self._hit[name] = (out, st._cdata, st, out._version, idx, (out.numel(), out.device, _stream()))
 
+    def drop(self, name):
+        """Forget `name`'s previous result (its next step allocates and writes densely)."""
+        self._hit.pop(name, None)
+
     def clear(self):
         self._hit.clear()
 
@@ -265,7 +269,47 @@ def ratio_k(numel, ratio):
     return max(1, int(numel * ratio))
 
 
+class TopKWaitError(_lib.GraceNativeError):
+    """A wait of the top-k parallel exact fallback ran out in an earlier call (status bit 2 of the
+    registered pinned word, include/grace_hip.h grace_topk_status_word): that call's payload,
+    residual and output are not valid.  Never expected: the fallback's waits are only on slices that
+    running workgroups have claimed (csrc/topk.hip parallel_exact)."""
+
+
+_tk_st = None
+
+
+def _topk_status():
+    """The pinned word every top-k launch of this process reports a fallback run-out to (registered
+    once), checked at every top-k call: it covers the earlier calls whose kernels have finished."""
+    global _tk_st
+    hit = _tk_st
+    if hit is None:
+        st = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        _lib.call("grace_topk_status_word", st.data_ptr())
+        hit = _tk_st = (st, st.numpy())     # numpy view: a plain host read per call
+    if hit[1][0]:
+        v = int(_lib.query("grace_status_take", hit[0].data_ptr()))   # read-and-clear, host atomic
+        if v & 2:
+            raise TopKWaitError("grace_amd: a top-k exact-fallback wait ran out in an earlier call; its "
+                                "payload, residual and output were not valid")
+    return hit[0]
+
+
+def topk_check():
+    """Wait for the device, then raise TopKWaitError if any top-k launch so far aborted
+    (TopKCompressor(check_sync=True) calls this after every step)."""
+    torch.cuda.synchronize()
+    _topk_status()
+
+
+def topk_fallback_spin_limit(limit=-1):
+    """Bound of the parallel exact fallback's waits in polls (tests force 0); returns the previous."""
+    return int(_lib.query("grace_topk_fallback_spin_limit", int(limit)))
+
+
 def topk_workspace(n, k, device):
+    _topk_status()
     return workspace("topk", _lib.query("grace_topk_workspace_bytes", n, k), device)
 
 
@@ -357,9 +401,10 @@ class MainEvent:
 
 
 def topk_status(n, k, device):
-    """Whether the last top-k launch on this stream took the exact fallback (syncs; tests only)."""
+    """Whether the last top-k launch on this stream took the exact fallback: 0 no, 1 yes, 2 it
+    aborted after a wait ran out (syncs; tests only)."""
     import ctypes
-    ws = topk_workspace(n, k, device)
+    ws = workspace("topk", _lib.query("grace_topk_workspace_bytes", n, k), device)
     st = ctypes.c_int32(-1)
     _lib.call("grace_read_status", _p(ws), ctypes.addressof(st), _stream())
     return st.value
@@ -952,16 +997,9 @@ def shard_clear(out, out_base, sel_gi):
     return out
 
 
-_sh_st = {}
-
-
-def shard_status(dev):
-    """The pinned status word the sharded select kernels set bits in (one per device)."""
-    key = str(dev)
-    st = _sh_st.get(key)
-    if st is None:
-        st = _sh_st[key] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-    return st
+def new_status_word():
+    """A pinned, device-visible int32 status word that kernels set bits in (system-scope fetch_or)."""
+    return torch.zeros(1, dtype=torch.int32, pin_memory=True)
 
 
 def status_take(st):

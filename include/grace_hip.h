@@ -42,7 +42,8 @@ typedef int grace_status_t;
 int grace_version(void);
 const char* grace_last_error(void);
 /* Diagnostics (tests only; synchronises the stream): the device-side status word of the last
- * top-k launch on `workspace` (0 = sampled fast path, 1 = exact fallback). */
+ * top-k launch on `workspace` (0 = sampled fast path, 1 = exact fallback, 2 = the parallel
+ * exact fallback aborted after a wait ran out: see grace_topk_status_word). */
 grace_status_t grace_read_status(const void* workspace, int32_t* status_host, void* stream);
 
 /* The streaming skeleton of the headline main pass (bench.py's HBM ceiling): topk_main with the
@@ -56,6 +57,16 @@ grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int
 /* Atomically read and clear a pinned host status word that kernels set bits in (system-scope
  * fetch_or): returns the bits set since the last take.  Host only, never blocks. */
 int32_t grace_status_take(int32_t* host_word);
+
+/* Top-k exact-fallback health.  grace_topk_status_word registers a pinned,
+ * device-accessible host word (NULL unregisters) that every later top-k launch of this process
+ * reports to: bit 2 = a wait of the parallel exact fallback ran out, so that launch's payload /
+ * residual / output are NOT valid (the fallback aborted in every workgroup; its waits are only on
+ * slices that running workgroups claimed, so this is never expected).  The device status word of
+ * grace_read_status then reads 2.  grace_topk_fallback_spin_limit sets the bound of those waits in
+ * polls (limit < 0: unchanged) and returns the previous bound; tests set 0 to force a run-out. */
+grace_status_t grace_topk_status_word(int32_t* host_word);
+int64_t grace_topk_fallback_spin_limit(int64_t limit);
 
 /* Event timer on the kernel's own stream, used by bench.py to time the dominant kernel of a
  * fused step: when enabled, that kernel's launch is bracketed by hipEventRecord. */
@@ -302,6 +313,11 @@ int32_t grace_topk_segmented_small_max(void);
 int64_t grace_topk_segmented_chunk(int32_t has_residual, int32_t dense_out);
 int64_t grace_topk_segmented_seg_ws_bytes(int64_t n, int64_t k);
 int32_t grace_topk_segmented_fin_blocks(int64_t n, int64_t k);
+/* The workspace a segment table needs (host arrays sizes[count], ks[count]: the LARGE segments,
+ * those listed in `large`): the sum of their 256-B aligned grace_topk_segmented_seg_ws_bytes.  Pass
+ * it as ws_need: the step refuses ws_bytes < ws_need (the per-segment offsets ws_off are
+ * device tables the host call cannot read). */
+int64_t grace_topk_segmented_workspace_bytes(const int64_t* sizes, const int64_t* ks, int32_t count);
 grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_t has_residual, float beta,
                                          float gamma, const int64_t* seg_off, const int64_t* k_off,
                                          const int32_t* large, int32_t n_large, const int32_t* small,
@@ -309,7 +325,8 @@ grace_status_t grace_topk_segmented_step(const float* g, float* residual, int32_
                                          int64_t nchunks, const int64_t* ws_off, const int64_t* fin_off,
                                          const int32_t* fin_li, int64_t nfin, int64_t n_total, float* vals,
                                          int32_t* idx, float* out, float* carry, const int64_t* carry_off,
-                                         int32_t carry_valid, void* ws, size_t ws_bytes, void* stream);
+                                         int32_t carry_valid, void* ws, size_t ws_bytes, int64_t ws_need,
+                                         void* stream);
 int64_t grace_topk_segmented_carry_len(int64_t n);
 
 /* ---------------------------------------------------------------------- random-k / threshold */

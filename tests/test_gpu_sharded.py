@@ -25,13 +25,13 @@ def _bucket(case, n, seed):
     return g
 
 
-def _worker(rank, world, path, outdir, sizes, case, ratio, steps):
+def _worker(rank, world, path, outdir, sizes, case, ratio, steps, dense="replicated"):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from grace_amd.dist.sharded import ShardedTopK
     n = sum(sizes)
     base = sum(sizes[:rank])
-    eng = ShardedTopK(ratio)
+    eng = ShardedTopK(ratio, dense=dense)
     res = {}
     for s in range(steps):
         full = _bucket(case, n, 100 + s)
@@ -161,3 +161,70 @@ def test_sharded_resize_native(check_sizes):
     for o in outs:
         assert _bits(o["out1"], out1)
         assert int(o["raised"][0]) == 0 and int(o["raised"][1]) == 1
+
+
+@pytest.mark.parametrize("world,sizes,case,ratio", [
+    (2, [1 << 20, 1 << 20], "normal", 0.01),
+    (2, [(1 << 20) + 5, 777777], "ties", 0.3),
+])
+def test_sharded_topk_native_dense_shard(world, sizes, case, ratio):
+    """SURVEY §8e's sharded-decode mode (dense="shard") with the native kernels:
+    every rank's output is exactly its own slice of the single-bucket decoded result (bit-exact
+    against the oracle), over three steps with recycled outputs; payloads and residuals as the
+    replicated mode."""
+    steps = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, steps, "shard"),
+                 nprocs=world, join=True)
+        outs = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                outs.append({k: z[k] for k in z.files})
+    n = sum(sizes)
+    r_or = None
+    for s in range(steps):
+        g = _bucket(case, n, 100 + s)
+        _, v_or, i_or, r_or, out_or = O.topk_residual_step(g, r_or, ratio)
+        idx = np.concatenate([o[f"idx{s}"] for o in outs]).astype(np.int64)
+        vals = np.concatenate([o[f"vals{s}"] for o in outs])
+        order = np.argsort(idx)
+        assert np.array_equal(idx[order], i_or.astype(np.int64)), s
+        assert _bits(vals[order], v_or)
+        assert _bits(np.concatenate([o[f"res{s}"] for o in outs]), r_or)
+        for w, o in enumerate(outs):
+            assert o[f"out{s}"].size == sizes[w]
+        assert _bits(np.concatenate([o[f"out{s}"] for o in outs]), out_or), s
+    assert all(int(o["recycled"][0]) == steps - 1 for o in outs)
+
+
+def _raise_worker(rank, world, path, outdir):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from grace_amd.dist.sharded import ShardedTopK, ShardPartitionError
+    eng = ShardedTopK(0.01)
+    raised_at = -1
+    for s in range(6):
+        sizes = [300000, 300000] if s == 0 else [300000, 200000]
+        base = sum(sizes[:rank])
+        full = _bucket("normal", sum(sizes), 100 + s)
+        try:
+            eng.step(torch.from_numpy(full[base:base + sizes[rank]].copy()).cuda(), "bucket")
+        except ShardPartitionError:
+            raised_at = s
+            break
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), raised_at=np.array([raised_at]))
+    dist.destroy_process_group()
+
+
+def test_sharded_resize_raised_by_step_on_every_rank():
+    """with no check() call, a resize at step 1 is raised by step() itself, at the same
+    step on both ranks (step N's status word is taken at step N + 2 after step N's select event),
+    so neither rank is left blocked in the next all-gather."""
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_raise_worker, args=(world, os.path.join(tmp, "rdv"), tmp), nprocs=world, join=True)
+        got = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                got.append(int(z["raised_at"][0]))
+    assert got == [3, 3]

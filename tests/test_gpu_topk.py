@@ -227,3 +227,82 @@ def test_topk_parallel_fallback_sparse_256mib():
     res, o = _np(r), _np(out)
     assert same_bits(res[~sel], g0[~sel]) and not np.any(res[sel])
     assert same_bits(o[sel], g0[sel]) and not np.any(o[~sel])
+
+
+@pytest.mark.parametrize("n,offset", [(70001, 0), (100003, 1), ((1 << 22) + 5, 0), ((1 << 22) + 7, 3)])
+def test_topk_parallel_fallback_slices(n, offset):
+    """The claimed-slice parallel fallback (csrc/topk.hip parallel_exact) at sizes whose slices do
+    not tile the bucket, on 16-B aligned and unaligned views (scalar path), with the ties at the
+    k-th key (zeros) spread over every slice: bit-exact against the oracle, residual and output too."""
+    from grace_amd import ops
+    rng = np.random.default_rng(n + offset)
+    base = np.zeros(n + offset, dtype=np.float32)
+    nz = rng.choice(n, size=n // 300, replace=False) + offset
+    base[nz] = rng.standard_normal(nz.size).astype(np.float32)
+    base[offset + rng.choice(n, size=n // 400, replace=False)] = 0.5   # ties above the cut
+    x = base[offset:]
+    k = O.ratio_k(n, 0.01)                   # > the non-zeros: the cut is at key 0, tied everywhere
+    buf = torch.from_numpy(base).to(DEV)
+    g = buf[offset:]
+    rbuf = torch.zeros(n + offset, device=DEV)
+    r = rbuf[offset:]
+    obuf = torch.empty(n + offset, device=DEV)
+    out = obuf[offset:]
+    _, vals, idx = ops.topk_residual_step(g, r, True, 1.0, 1.0, k, out=out)
+    torch.cuda.synchronize()
+    assert ops.topk_status(n, k, g.device) == 1
+    ov, oi = O.topk_select(x, k)
+    v, i = _sorted_payload(vals, idx)
+    assert np.array_equal(i, oi.astype(np.int64))
+    assert same_bits(v, ov)
+    sel = np.zeros(n, dtype=bool)
+    sel[oi] = True
+    res, o = _np(r), _np(out)
+    assert same_bits(res[~sel], x[~sel]) and not np.any(res[sel])
+    assert same_bits(o[sel], x[sel]) and not np.any(o[~sel])
+
+
+def test_topk_fallback_runout_raises():
+    """a wait of the parallel exact fallback that runs out must never pass as a
+    result.  With the wait bound forced to 0 polls, the sparse step (fallback taken) aborts: the
+    device status reads 2, the next top-k call raises TopKWaitError, and TopKCompressor with
+    check_sync=True raises on the failing call itself.  With the bound restored, the fallback's
+    scratch (re-zeroed by the last workgroup out, also after an abort) gives exact results again."""
+    from grace_amd import ops
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    n = 1 << 22
+    k = O.ratio_k(n, 0.01)
+    rng = np.random.default_rng(5)
+    g0 = np.zeros(n, dtype=np.float32)
+    pos = rng.choice(n, size=n // 400, replace=False)
+    g0[pos] = rng.standard_normal(pos.size).astype(np.float32)
+    g = torch.from_numpy(g0).to(DEV)
+    ops.topk_check()                         # nothing pending from earlier tests
+    prev = ops.topk_fallback_spin_limit(0)
+    try:
+        ops.topk_residual_step(g, torch.zeros_like(g), True, 1.0, 1.0, k, out=torch.empty_like(g))
+        torch.cuda.synchronize()
+        assert ops.topk_status(n, k, g.device) == 2
+        with pytest.raises(ops.TopKWaitError):
+            ops.topk_compress(g, k)          # the next call reports the earlier abort
+        comm = Allgather(TopKCompressor(0.01, check_sync=True), ResidualMemory(), 1)
+        with pytest.raises(ops.TopKWaitError):
+            comm.step(g, "w")                # check_sync: the failing call itself raises
+    finally:
+        ops.topk_fallback_spin_limit(prev)
+    assert ops.topk_fallback_spin_limit() == prev
+    torch.cuda.synchronize()
+    ops._topk_status()                       # the word was taken by the raise: nothing pending
+    r = torch.zeros_like(g)
+    out = torch.empty_like(g)
+    _, vals, idx = ops.topk_residual_step(g, r, True, 1.0, 1.0, k, out=out)
+    ops.topk_check()
+    assert ops.topk_status(n, k, g.device) == 1
+    check_topk(g0, k, vals, idx)
+    ov, oi = O.topk_select(g0, k)
+    sel = np.zeros(n, dtype=bool)
+    sel[oi] = True
+    o = _np(out)
+    assert same_bits(o[sel], g0[sel]) and not np.any(o[~sel])

@@ -29,7 +29,7 @@ class OracleShardKernels:
     HDR = HDR
 
     def __init__(self):
-        self.st = torch.zeros(1, dtype=torch.int32)
+        pass
 
     def record_words(self, cap):
         return HDR + 2 * cap
@@ -68,8 +68,8 @@ class OracleShardKernels:
         rej = valid[rank] & ~sel[rank]
         res.numpy()[li[rank][rej]] = v[rank][rej]
 
-    def status(self, device):
-        return self.st
+    def new_status(self, device):
+        return torch.zeros(1, dtype=torch.int32)
 
     def take_status(self, st):
         bits = int(st[0])
@@ -92,11 +92,25 @@ def _bucket(case, n, seed):
     return g
 
 
-def _worker(rank, world, path, outdir, sizes, case, ratio, dense, sizes2=None, check_sizes=False):
+def _worker(rank, world, path, outdir, sizes, case, ratio, dense, sizes2=None, check_sizes=False, steps=2):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded import ShardedTopK, ShardPartitionError
     eng = ShardedTopK(ratio, dense=dense, kernels=OracleShardKernels(), check_sizes=check_sizes)
     res = {}
+    if steps > 2:    # step until one raises: record which (every rank must agree, nobody may hang)
+        raised_at = -1
+        for s in range(steps):
+            part = sizes2 if (s >= 1 and sizes2 is not None) else sizes
+            full = _bucket(case, sum(part), 100 + s)
+            base = sum(part[:rank])
+            try:
+                eng.step(torch.from_numpy(full[base:base + part[rank]].copy()), "bucket")
+            except ShardPartitionError:
+                raised_at = s
+                break
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), raised_at=np.array([raised_at]))
+        dist.destroy_process_group()
+        return
     for s in range(2):
         part = sizes2 if (s == 1 and sizes2 is not None) else sizes
         n = sum(part)
@@ -121,9 +135,10 @@ def _worker(rank, world, path, outdir, sizes, case, ratio, dense, sizes2=None, c
     dist.destroy_process_group()
 
 
-def _run(world, sizes, case, ratio, dense="replicated", sizes2=None, check_sizes=False):
+def _run(world, sizes, case, ratio, dense="replicated", sizes2=None, check_sizes=False, steps=2):
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, dense, sizes2, check_sizes),
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, case, ratio, dense, sizes2, check_sizes,
+                                steps),
                  nprocs=world, join=True)
         outs = []
         for r in range(world):
@@ -207,3 +222,12 @@ def test_sharded_resize_without_check_sizes_is_reported():
     step neither hangs nor passes silently."""
     outs = _run(2, [40000, 40000], "normal", 0.01, sizes2=[40000, 25000])
     assert all(int(o["raised"][0]) == 1 for o in outs)
+
+
+def test_sharded_resize_reported_at_the_same_step_on_every_rank():
+    """without check(), the status of step N is taken at step N + 2 from a word only step
+    N wrote (one per step parity), after step N's select has finished on that rank -- so every rank
+    raises at the same step and none is left waiting in the next all-gather.  Rank 1's shard
+    shrinks at step 1; both ranks raise at step 3."""
+    outs = _run(2, [40000, 40000], "normal", 0.01, sizes2=[40000, 25000], steps=6)
+    assert [int(o["raised_at"][0]) for o in outs] == [3, 3]

@@ -32,7 +32,7 @@ gen.manual_seed(5)
 g = torch.randn(n, device=dev, generator=gen)
 res = [torch.zeros(sizes[r], device=dev) for r in range(W)]
 pay = [torch.full((cap,), -1, dtype=torch.int32, device=dev) for r in range(W)]
-st = ops.shard_status(dev)
+st = ops.new_status_word()
 ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
 rows = []
 for step in range(6):
