@@ -209,6 +209,32 @@ def pmc_traffic(workload, alg_bytes):
     return t, round(t / alg_bytes, 3)
 
 
+def gpu_clocks(dev):
+    """The device's current shader / memory clock levels from sysfs (pp_dpm_sclk / pp_dpm_mclk, the
+    level marked '*'), read right after a timed region: VERDICT r4 item 4 (the main pass is bimodal
+    across boxes).  Found through the device's PCI address; None where sysfs does not show it."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        dom, bus, devid = (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", None),
+                           getattr(p, "pci_device_id", None))
+        if bus is None or devid is None:
+            return None
+        base = f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{devid:02x}.0"
+        out = {"pci": base.rsplit("/", 1)[1]}
+        for clk in ("sclk", "mclk", "fclk", "socclk"):
+            try:
+                with open(f"{base}/pp_dpm_{clk}") as f:
+                    rows = [r.strip() for r in f if r.strip()]
+                cur = [r for r in rows if r.endswith("*")]
+                out[f"{clk}_current"] = cur[0].split(":", 1)[1].strip(" *") if cur else None
+                out[f"{clk}_levels"] = len(rows)
+            except OSError:
+                out[f"{clk}_current"] = None
+        return out
+    except Exception as e:   # diagnostics only: never fail the bench line
+        return {"error": str(e)[:120]}
+
+
 def base_line(args, world, elapsed, nbytes_per_rank, metric=METRIC):
     ms = elapsed / args.steps * 1e3
     return {
@@ -250,6 +276,7 @@ def bench_topk(args, world, rank, dev):
     elapsed = timed(step, args.steps, 0, world, dev)
     main_ms, launches = ops.timer_collect()
     ops.timer_enable(False)
+    clocks = gpu_clocks(dev)
     # world 1: each step's result is consumed and dropped, so every timed step reuses its bucket's
     # previous result (ops.OutputRecycler): the main pass writes only its selection into the output
     recycled = world == 1 and rec.hits - hits0 == args.steps
@@ -309,6 +336,7 @@ def bench_topk(args, world, rank, dev):
     roofline["frac_of_measured_copy"] = round(achieved / skel, 4) if skel else None
     roofline["frac_of_measured_copy_median"] = round(achieved / skel_med, 4) if skel_med else None
     line["roofline"] = roofline
+    line["clocks"] = clocks
     if world == 1 and not args.no_overlap:
         line["two_streams"] = bench_topk_two_streams(args, grads, names)
     line["cpu_baseline"] = None

@@ -78,7 +78,7 @@ constexpr int kVecOf = kBytesOf<HAS_RES, MODE> >= 16 ? kMainVec
                        : (kBytesOf<HAS_RES, MODE> >= 12 ? GRACE_MAIN_VEC_12B : GRACE_MAIN_VEC_NORES);
 template <bool HAS_RES, int MODE> constexpr int kChunkOf = kMainBlock * 4 * kVecOf<HAS_RES, MODE>;
 constexpr int kHistBins = 2048;                            // candidate histogram
-constexpr int kStage = 512;                                // LDS staging entries per list
+constexpr int kStage = 1024;                               // LDS staging entries per list (all waves)
 constexpr int kSelBlock = 1024;                            // single-workgroup selectors
 constexpr int kSmallN = 32768;                             // single-workgroup path
 constexpr int kSampleRunLen = 16;
@@ -129,6 +129,12 @@ static_assert(sizeof(TopkCtl) == 64, "ctl layout");
 #define GRACE_SAMPLE_MAX 131072
 #endif
 constexpr int kSampleMax = GRACE_SAMPLE_MAX;               // stratified sample size
+// The sample a bucket's bracket draws: every element up to kSampleMax, else kSampleMax.  (r05
+// A/B at BASELINE configs[4]'s 8.4 M-element shard: one sample per 256 elements, 32 K instead of
+// 131 K, took the bracket from 16.6 to 14.1 us but doubled the candidates, finalize 11.8 -> 17.0
+// us: local step 59.5 -> 58.7 us, within the spread -- the bracket's cost is its fixed LDS zeroing,
+// flush and fan-in, not its random reads.)
+__host__ __device__ inline int64_t bracket_sample_n(int64_t n) { return n < kSampleMax ? n : kSampleMax; }
 constexpr int kSampleBlock = 1024;
 #ifndef GRACE_BRACKET_BLOCK
 #define GRACE_BRACKET_BLOCK 1024
@@ -589,9 +595,9 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
 //
 // Each workgroup streams one 12288-element chunk: 3 groups of 4 float4 per lane per array, with
 // the next group's loads issued before the current group is classified (16-B loads, 8 in flight
-// per lane).  Per group every lane counts its sure / candidate elements, one wave-wide prefix
-// scan (packed 16|16 bits) places them, and ONE LDS atomic per wave per group reserves staging
-// space; the staged entries leave with one global atomic per workgroup at the end.
+// per lane).  Per group every lane flags its elements with key >= lo, a DPP wave scan of the
+// counts places them in the wave's own LDS region (no atomic), and the staged entries leave with
+// one global atomic per list and workgroup at the end, sorted into sure / candidate there.
 #ifndef GRACE_MAIN_GROUP
 #define GRACE_MAIN_GROUP 4
 #endif
@@ -640,27 +646,54 @@ __device__ __forceinline__ void load_group(const StepArgs& a, int64_t gbase, flo
   }
 }
 
+constexpr int kMainWaves = kMainBlock / 64;
+constexpr int kStageWave = kStage / kMainWaves;            // each wave's own region of each list
+
 struct MainShared {
   uint32_t hist[kHistBins];
   int2 sure[kStage];
   int2 cand[kStage];
-  uint32_t cnt[4];   // packed staged counts (sure | cand << 16), base_sure, base_cand
+  uint32_t wcnt[kMainWaves];   // each wave's packed staged counts (sure | cand << 16), for the flush
+  uint32_t gbase[2];           // the chunk's reservations in the global sure / candidate lists
 };
 
-// v2 classification of one group (kGroup float4 per lane per array, already loaded): per-lane LDS
-// reservation (one ds_add_rtn of the packed 16|16 counts by each lane that has entries, no wave
-// scan), one branch per flagged element position for both lists; the candidate histogram is built
-// from the staged entries at the flush instead of a masked ds_add per element in the stream.
-template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false>
-__device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
-                                               uint32_t hi, uint32_t sh, uint32_t mid, int64_t gbase,
-                                               const float4 (&rc)[kGroup], const float4 (&gc)[kGroup]) {
+// wave-wide inclusive scan of one uint32 per lane: DPP row shifts within each 16-lane row, then
+// the row broadcasts (gfx9 row_bcast:15 / row_bcast:31) -- 6 VALU, no LDS, no loop
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return v;
+}
+
+// v2 classification of one group (kGroup float4 per lane per array, already loaded): a DPP wave
+// scan of the lanes' packed 16|16 counts places the entries in the wave's OWN regions of the two
+// LDS lists at its running fill (wfill, wave-uniform) -- no reservation atomic (r05: the per-lane
+// ds_add_rtn of r04 became the compiler's atomic-optimizer loop, a readlane / writelane per active
+// lane); one branch per flagged element position for both lists; the candidate histogram is built
+// from the staged entries at the flush instead of a masked ds_add per element.  Returns the wave's
+// new fill.
+// UNIT: beta = gamma = 1, t = r + g (1 * x is x bit for bit, so this is the reference's
+// beta * r + gamma * g).
+template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false>
+__device__ __forceinline__ uint32_t classify_group(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                                   uint32_t hi, uint32_t sh, uint32_t mid, int64_t gbase,
+                                                   const float4 (&rc)[kGroup], const float4 (&gc)[kGroup],
+                                                   uint32_t wfill) {
   const int64_t n = a.n;
   float4 t[kGroup];
   uint32_t msure = 0, mcand = 0;   // bit u*4+j
 #pragma unroll
   for (int u = 0; u < kGroup; ++u) {
-    if constexpr (HAS_RES) {
+    if constexpr (HAS_RES && UNIT) {
+      t[u].x = rc[u].x + gc[u].x;
+      t[u].y = rc[u].y + gc[u].y;
+      t[u].z = rc[u].z + gc[u].z;
+      t[u].w = rc[u].w + gc[u].w;
+    } else if constexpr (HAS_RES) {
       t[u].x = a.beta * rc[u].x + a.gamma * gc[u].x;
       t[u].y = a.beta * rc[u].y + a.gamma * gc[u].y;
       t[u].z = a.beta * rc[u].z + a.gamma * gc[u].z;
@@ -674,7 +707,6 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
     for (int j = 0; j < 4; ++j) {
       const float tv = comp4(t[u], j);
       const uint32_t key = abs_key(tv);
-      const bool valid = FAST || i0 + j < n;
 #ifdef GRACE_MAIN_STREAM_ONLY   // diagnostic A/B build only: the streaming ceiling of this layout
       constexpr bool kSkel = true;
 #else
@@ -682,32 +714,43 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
 #endif
       // SKEL (grace_topk_stream_probe): the same loads and stores with no classification -- the
       // streaming ceiling of this exact layout (nothing is listed; the per-chunk flushes still run)
-      const bool sure = kSkel ? false : (valid && key > hi);
-      const bool cand = kSkel ? false : (valid && !sure && key >= lo);
-      msure |= (uint32_t)sure << (u * 4 + j);
-      mcand |= (uint32_t)cand << (u * 4 + j);
+      //
+      // The flags are integer arithmetic on the 31-bit keys (sign bits of differences that cannot
+      // overflow), not comparisons: 16 comparisons per group became 16 live 64-bit lane masks, and
+      // the compiler spilled SGPRs to VGPR lanes (r05: 31 spills, 349 v_readlane in topk_main).
+      const uint32_t vbit = (FAST || i0 + j < n) ? 1u : 0u;
+      const uint32_t f_sure = kSkel ? 0u : ((hi - key) >> 31) & vbit;              // key > hi
+      const uint32_t f_lo = kSkel ? 0u : (((key - lo) >> 31) ^ 1u) & vbit;         // key >= lo
+      msure |= f_sure << (u * 4 + j);
+      mcand |= (f_lo & (f_sure ^ 1u)) << (u * 4 + j);
       if constexpr (kWritesOut<MODE>) {
         // sure elements, and candidates above the provisional threshold, are written as selected;
-        // the finalize fixes up only the candidates whose final decision differs
-        if (sure || (cand && key > mid)) {
-          set4(rout, j, tv - tv);
-          set4(dout, j, 0.f + tv);
-          // recycled output: only the selected elements are written (the rest is already zero)
-          if constexpr (SPARSE) if (valid) a.out[i0 + j] = 0.f + tv;
-        }
+        // the finalize fixes up only the candidates whose final decision differs.  lo <= mid <= hi
+        // (bracket_publish), so "sure or (candidate and key > mid)" is key > mid: an all-ones
+        // mask selects r' = t - t and out = 0 + t bitwise
+        const uint32_t m = kSkel ? 0u : (uint32_t)((int32_t)(mid - key) >> 31) & (0u - vbit);
+        set4(rout, j, u2f((f2u(tv - tv) & m) | (f2u(tv) & ~m)));
+        set4(dout, j, u2f(f2u(0.f + tv) & m));
+        // recycled output: only the selected elements are written (the rest is already zero)
+        if constexpr (SPARSE) if (m) a.out[i0 + j] = 0.f + tv;
       }
     }
     if constexpr (kWritesR<MODE>) st4<FAST>(a.r, i0, n, rout);
     if constexpr (kWritesOut<MODE> && !SPARSE) st4<FAST>(a.out, i0, n, dout);
   }
+  if constexpr (SKEL) return wfill;
   const uint32_t msel = msure | mcand;
+  const uint32_t cnt = __popc(msure) | (__popc(mcand) << 16);
+  const uint32_t incl = wave_incl_scan_dpp(cnt);
+  const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
   if (msel) {
-    const uint32_t cs = __popc(msure), cc = __popc(mcand);
-    const uint32_t bse = atomicAdd(&sm.cnt[0], cs | (cc << 16));
+    const uint32_t cs = cnt & 0xFFFFu, cc = cnt >> 16;
+    const uint32_t bse = wfill + incl - cnt;   // this lane's first slots in the wave's regions
     uint32_t ps = bse & 0xFFFFu, pc = bse >> 16;
-    // entries past kStage spill to the global lists (rare: one global atomic per spilling lane)
-    const uint32_t over_s = ps + cs > (uint32_t)kStage ? min(ps + cs - (uint32_t)kStage, cs) : 0u;
-    const uint32_t over_c = pc + cc > (uint32_t)kStage ? min(pc + cc - (uint32_t)kStage, cc) : 0u;
+    const uint32_t wb = (threadIdx.x >> 6) * kStageWave;
+    // entries past the wave's region spill to the global lists (rare: one global atomic per lane)
+    const uint32_t over_s = ps + cs > (uint32_t)kStageWave ? min(ps + cs - (uint32_t)kStageWave, cs) : 0u;
+    const uint32_t over_c = pc + cc > (uint32_t)kStageWave ? min(pc + cc - (uint32_t)kStageWave, cc) : 0u;
     uint32_t gs = 0, gcn = 0;
     if (over_s) gs = atomicAdd(&w.ctl->n_sure, over_s);
     if (over_c) gcn = atomicAdd(&w.ctl->n_cand, over_c);
@@ -721,15 +764,15 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
           const float tv = comp4(t[u], j);
           const int2 e = make_int2((int)i, (int)f2u(tv));
           if ((msure >> b) & 1u) {
-            if (ps < (uint32_t)kStage) {
-              sm.sure[ps] = e;
+            if (ps < (uint32_t)kStageWave) {
+              sm.sure[wb + ps] = e;
             } else if (gs < (uint32_t)a.k) {
               a.vals[gs] = tv; a.idx[gs] = (int32_t)(e.x + a.idx_base); ++gs;
             }
             ++ps;
           } else {
-            if (pc < (uint32_t)kStage) {
-              sm.cand[pc] = e;
+            if (pc < (uint32_t)kStageWave) {
+              sm.cand[wb + pc] = e;
             } else {
               atomicAdd(&sm.hist[cand_bin(abs_key(tv), lo, sh)], 1u);
               if (gcn < (uint32_t)w.cap) w.cand[gcn] = e;
@@ -741,15 +784,17 @@ __device__ __forceinline__ void classify_group(const StepArgs& a, const TopkWs& 
       }
     }
   }
+  return wfill + tot;
 }
 
-template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false>
-__device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
-                                              uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
+template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false>
+__device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
+                                                  uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
   constexpr int NG = kVecOf<HAS_RES, MODE> / kGroup;
   static_assert(NG * kGroup == kVecOf<HAS_RES, MODE>, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
   const int64_t cbase = chunk * kChunkOf<HAS_RES, MODE> + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
+  uint32_t wfill = 0;
 #ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
   if constexpr (!HAS_RES && NG >= 3) {
     // one input stream (g only): the loads run TWO groups ahead, so a lane keeps as many bytes in
@@ -761,11 +806,11 @@ __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w
     for (int q = 0; q < NG; ++q) {
       const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
       if (q + 2 < NG) load_group<false, FAST>(a, gbase + 2 * kGroup * (kMainBlock * 4), rc, g2);
-      classify_group<false, MODE, FAST, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc);
+      wfill = classify_group<false, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
 #pragma unroll
       for (int u = 0; u < kGroup; ++u) { gc[u] = g1[u]; g1[u] = g2[u]; }
     }
-    return;
+    return wfill;
   }
 #endif
   load_group<HAS_RES, FAST>(a, cbase, rc, gc);
@@ -774,43 +819,62 @@ __device__ __forceinline__ void main_chunk_v2(const StepArgs& a, const TopkWs& w
     const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
     float4 rn[kGroup], gn[kGroup];
     if (q + 1 < NG) load_group<HAS_RES, FAST>(a, gbase + kGroup * (kMainBlock * 4), rn, gn);
-    classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc);
+    wfill = classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
 #pragma unroll
     for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
   }
+  return wfill;
 }
 
-// the staged lists of one chunk leave with one global atomic per list (v2: the staged candidates
-// are counted into the LDS histogram here); leaves sm.cnt zeroed for the next chunk
+// the staged lists of one chunk leave with one global atomic per list: the waves' regions are
+// concatenated in wave order (v2: the staged candidates are counted into the LDS histogram here)
 __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
-                                             uint32_t sh) {
+                                             uint32_t sh, uint32_t wfill) {
   const int tid = threadIdx.x;
+  if ((tid & 63) == 0) sm.wcnt[tid >> 6] = wfill;
   __syncthreads();
-  const uint32_t ns = min(sm.cnt[0] & 0xFFFFu, (uint32_t)kStage);
-  const uint32_t nc = min(sm.cnt[0] >> 16, (uint32_t)kStage);
+  uint32_t os[kMainWaves + 1], oc[kMainWaves + 1];
+  os[0] = oc[0] = 0;
+#pragma unroll
+  for (int v = 0; v < kMainWaves; ++v) {
+    const uint32_t f = sm.wcnt[v];
+    os[v + 1] = os[v] + min(f & 0xFFFFu, (uint32_t)kStageWave);
+    oc[v + 1] = oc[v] + min(f >> 16, (uint32_t)kStageWave);
+  }
+  const uint32_t ns = os[kMainWaves], nc = oc[kMainWaves];
   if (tid == 0) {
     // one reservation per chunk and list (5461 per step on each counter: as 8 copies, a timing-only
     // build, the main pass was 2 us faster in 196 -- within the spread, so the one counter stays)
-    sm.cnt[1] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
-    sm.cnt[2] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+#ifdef GRACE_DIAG_NORESERVE   // timing-only A/B build (wrong results): no atomic return to wait for
+    sm.gbase[0] = (uint32_t)((blockIdx.x * 97u) % (uint32_t)(a.k > 2048 ? a.k - 2048 : 1));
+    sm.gbase[1] = (uint32_t)((blockIdx.x * 53u) % (uint32_t)(w.cap > 2048 ? w.cap - 2048 : 1));
+#else
+    sm.gbase[0] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
+    sm.gbase[1] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+#endif
   }
   __syncthreads();
   for (uint32_t j = tid; j < ns; j += kMainBlock) {
-    const uint32_t gp = sm.cnt[1] + j;
+    const uint32_t gp = sm.gbase[0] + j;
     if (gp < (uint32_t)a.k) {
-      const int2 e = sm.sure[j];
+      int v = 0;
+#pragma unroll
+      for (int x = 1; x < kMainWaves; ++x) v += j >= os[x];
+      const int2 e = sm.sure[v * kStageWave + (j - os[v])];
       a.vals[gp] = u2f((uint32_t)e.y);
       a.idx[gp] = (int32_t)(e.x + a.idx_base);
     }
   }
   for (uint32_t j = tid; j < nc; j += kMainBlock) {
-    const uint32_t gp = sm.cnt[2] + j;
-    const int2 e = sm.cand[j];
+    const uint32_t gp = sm.gbase[1] + j;
+    int v = 0;
+#pragma unroll
+    for (int x = 1; x < kMainWaves; ++x) v += j >= oc[x];
+    const int2 e = sm.cand[v * kStageWave + (j - oc[v])];
     atomicAdd(&sm.hist[cand_bin(abs_key(u2f((uint32_t)e.y)), lo, sh)], 1u);
     if (gp < (uint32_t)w.cap) w.cand[gp] = e;
   }
-  __syncthreads();
-  if (tid < 4) sm.cnt[tid] = 0;
+  __syncthreads();   // the lists and wcnt are free for the next chunk
 }
 
 template <bool HAS_RES, int MODE, bool VEC, bool SKEL = false, bool SPARSE = false>
@@ -822,19 +886,23 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   // the flushes left in, the real pass beat its fastest launch by 0.5 % on one box)
   if constexpr (!SKEL) {
     for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
-    if (tid < 4) sm.cnt[tid] = 0;
   }
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   const int64_t nchunks = (a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>;
+  const bool unit = HAS_RES && a.beta == 1.f && a.gamma == 1.f;
   if constexpr (!SKEL) __syncthreads();
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n)
-      main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
+    uint32_t wfill;
+    if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n && unit)
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE, true>(a, w, sm, lo, hi, sh, mid, chunk);
+    else if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n)
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
     else
-      main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
-    if constexpr (!SKEL) flush_staged(a, w, sm, lo, sh);
+      wfill = main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
+    if constexpr (!SKEL) flush_staged(a, w, sm, lo, sh, wfill);
+    (void)wfill;
   }
   if constexpr (SKEL) return;
   __syncthreads();
@@ -1559,7 +1627,7 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   TopkWs w = carve(ws, a.n, a.k);
   const bool vec = ((reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.r) |
                      reinterpret_cast<uintptr_t>(a.out)) & 15u) == 0;
-  a.sample_n = a.n < kSampleMax ? a.n : kSampleMax;
+  a.sample_n = bracket_sample_n(a.n);
   a.stratum = a.n / a.sample_n;
   if (a.stratum < kCarryMinStratum) a.rs_in = a.rs_out = nullptr;   // (grace_topk_carry_size says 0)
   // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
@@ -1882,14 +1950,18 @@ __global__ __launch_bounds__(kMainBlock, 4) void seg_main_kernel(SegPlan p) {
               (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
   for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
-  if (tid < 4) sm.cnt[tid] = 0;
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   __syncthreads();
-  if (VEC && (p.seg_off[s] & 3) == 0 && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n)
-    main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
-  else
-    main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
-  flush_staged(a, w, sm, lo, sh);
+  uint32_t wfill;
+  if (VEC && (p.seg_off[s] & 3) == 0 && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n) {
+    if (HAS_RES && a.beta == 1.f && a.gamma == 1.f)
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC, false, false, true>(a, w, sm, lo, hi, sh, mid, chunk);
+    else
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
+  } else {
+    wfill = main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
+  }
+  flush_staged(a, w, sm, lo, sh, wfill);
   __syncthreads();
   for (int b = tid; b < kHistBins; b += kMainBlock) {
     const uint32_t h = sm.hist[b];
@@ -2104,7 +2176,7 @@ grace_status_t grace_topk_residual_step(const float* g, float* residual, int32_t
 
 int64_t grace_topk_carry_size(int64_t n, int64_t k) {
   if (n <= kSmallN || k >= n || n >= (int64_t)1 << 31) return 0;   // no sampled bracket on these paths
-  const int64_t sn = n < kSampleMax ? n : kSampleMax;
+  const int64_t sn = bracket_sample_n(n);
   return n / sn >= kCarryMinStratum ? carry_thr_off(sn) + 2 : 0;   // t at the sample positions + the u64 threshold
 }
 

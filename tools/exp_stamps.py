@@ -16,10 +16,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from grace_amd import ops  # noqa: E402
 
-n = 64 * 1024 * 1024
+n = int(os.environ.get("N", 64 * 1024 * 1024))
 ratio = float(os.environ.get("RATIO", "0.01"))
 path = os.environ.get("PATH_KIND", "bench")
-k = ops.ratio_k(n, ratio)
+k = int(os.environ.get("K", 0)) or ops.ratio_k(n, ratio)
+res_only = os.environ.get("RES_ONLY", "0") == "1"   # the sharded / W > 1 local step: no dense output
 dev = torch.device("cuda", 0)
 gs = [torch.randn(n, device=dev) for _ in range(3)]
 names = ["thr_lo", "thr_hi", "shift", "status", "n_sure", "n_cand", "n_sel", "n_bnd", "B", "need"]
@@ -31,7 +32,7 @@ if path == "bench":
     run = lambda it: comm.step(gs[it % 3], "b")   # noqa: E731
 else:
     r = 0.1 * torch.randn(n, device=dev)
-    out = torch.empty_like(gs[0])
+    out = None if res_only else torch.empty_like(gs[0])
     run = lambda it: ops.topk_residual_step(gs[it % 3], r, True, 1.0, 1.0, k, out=out)   # noqa: E731
 rows = []
 for it in range(12):
@@ -50,5 +51,5 @@ for it in range(12):
                  "fin_b0_findB": us(8, 9), "fin_b0_route": us(9, 10), "fin_b0_to_last": us(10, 11),
                  "fin_last_bnd": us(11, 12), "fin_total": us(8, 12), "k": k, **counters})
 keys = [q for q in rows[0] if q not in ("thr_lo", "thr_hi", "shift", "B")]
-print(json.dumps({"lib": os.environ.get("GRACE_HIP_LIB", "default"), "path": path,
+print(json.dumps({"lib": os.environ.get("GRACE_HIP_LIB", "default"), "path": path, "n": n, "res_only": res_only,
                   "median_of_steps_3_to_11": {q: round(statistics.median(r[q] for r in rows[3:]), 2) for q in keys}}))

@@ -1,0 +1,41 @@
+#!/bin/bash
+# r05 GPU measurement session: tools/r05_session.sh STEP...  (each step under its own timeout;
+# outputs under gpurun_out/r05/).  Steps:
+#   fallback   tools/exp_fallback.py (degenerate buckets through the claimed-slice exact fallback)
+#   stamps     phase stamps of the local top-k at configs[4] (m = 2^23, k = 67,108, residual only)
+#              and of the W > 1 DP local step (2^26, k = 671,088, residual only)
+#   shard      tools/exp_shard_local.py 8
+#   wn         tools/exp_wn_local.py (DP-replica per-rank device time at W = 8)
+#   sq         SQ / GRBM counter passes over the headline bench (topk_main and its stream skeleton)
+#   bench      the default bench line
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r05; mkdir -p $O
+export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?
+        echo "$name rc=$rc"; tail -4 "$O/$name.log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+for s in "$@"; do
+  case $s in
+    fallback) run fallback 180 python3 tools/exp_fallback.py ;;
+    stamps)
+      GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so N=8388608 K=67108 RES_ONLY=1 PATH_KIND=plain \
+        run stamps_shard_local 120 python3 tools/exp_stamps.py
+      GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so RES_ONLY=1 PATH_KIND=plain \
+        run stamps_wn_local 120 python3 tools/exp_stamps.py ;;
+    shard) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
+    wn) run wn_local 180 python3 tools/exp_wn_local.py ;;
+    sq)
+      i=0
+      for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+               "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"; do
+        i=$((i + 1))
+        run sq_head_$i 120 rocprofv3 --pmc $c --output-format csv -d $O/sq_head_$i -o pmc \
+            -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-overlap
+      done
+      run sq_head_kt 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sq_head_kt -o run \
+          -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
+      python3 tools/pmc_sq_summary.py $O/sq_head > $O/sq_head_summary.json; echo "sq summary rc=$?" ;;
+    bench) run bench 300 python3 bench.py ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
