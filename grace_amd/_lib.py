@@ -119,6 +119,10 @@ SIGNATURES = {
     "grace_threshold_write_i64": (ST, [P, I64, P, P, P, P]),
     "grace_terngrad_unit": (I32, []),
     "grace_terngrad_workspace_bytes": (SZ, [I64]),
+    "grace_terngrad_slot_bytes": (I32, []),
+    "grace_terngrad_shard_stats": (ST, [P, I64, P, P, I32, I64, I64, P, P]),
+    "grace_terngrad_shard_encode": (ST, [P, I64, P, P, I32, I64, I64, P, P, U64, P, P, P]),
+    "grace_terngrad_scalars": (ST, [P, P, I32, P, P, P, P]),
     "grace_terngrad_compress": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_step_w1": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_decompress": (ST, [P, P, I64, I64, I32, P, I32, I64, I32, F32, P, P]),

@@ -1043,6 +1043,15 @@ __device__ __forceinline__ QuadSplit quad_split(int64_t base, int64_t end) {
   if (a1 < a0) a1 = a0;
   return QuadSplit{a0, a1};
 }
+// the same with quads at the indices congruent to ph mod 4 (a shard whose element xoff sits at its
+// 16-B aligned start: ph = xoff & 3)
+__device__ __forceinline__ QuadSplit quad_split_ph(int64_t base, int64_t end, int64_t ph) {
+  int64_t a0 = base + ((ph - base) & 3);
+  if (a0 > end) a0 = end;
+  int64_t a1 = end - ((end - ph) & 3);
+  if (a1 < a0) a1 = a0;
+  return QuadSplit{a0, a1};
+}
 
 __device__ __forceinline__ void tern_acc(float v, double& sum, double& sq, float& amax, uint32_t& nan) {
   sum += (double)v;
@@ -1091,19 +1100,23 @@ __host__ __device__ inline size_t tern_ws_bytes(int64_t nunits) { return sizeof(
 // deterministic) and publishes (c, scalar) for stage 2.  Partials cross workgroups -- and XCDs,
 // whose L2s are not coherent -- so they are written and read back at agent scope (write-through),
 // ordered by vmcnt(0) before the arrival ticket: no cache-wide fences.
+// unit0 / xoff (sharded TernGrad, grace_terngrad_shard_*): this launch runs the global units unit0,
+// unit0 + 1, ... and x points at global element xoff (its shard); 0 / 0 for a whole bucket
 __global__ __launch_bounds__(kQBlock) void tern_stats_kernel(const float* __restrict__ x,
                                                             const int64_t* __restrict__ seg_off,
                                                             const int64_t* __restrict__ unit_off, int nseg,
                                                             const float* __restrict__ clip_in, TernSlot* __restrict__ w,
-                                                            float* __restrict__ scalars) {
+                                                            float* __restrict__ scalars, int64_t unit0 = 0,
+                                                            int64_t xoff = 0) {
   __shared__ SegTables tab;
   __shared__ uint32_t s_last;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
-  const int64_t unit = blockIdx.x;
+  const int64_t unit = unit0 + blockIdx.x;
   const int s = find_seg(sv.sub, nseg, unit);
   const int64_t base = sv.seg[s] + (unit - sv.sub[s]) * kTernUnit;
   const int64_t end = min(base + (int64_t)kTernUnit, sv.seg[s + 1]);
-  const QuadSplit qs = quad_split(base, end);
+  const QuadSplit qs = quad_split_ph(base, end, xoff & 3);
+  x -= xoff;   // indexed by global element from here on (never below xoff)
   double sum = 0.0, sq = 0.0;
   float amax = 0.f;
   uint32_t nan = 0;
@@ -1188,14 +1201,19 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ unit_off,
     int nseg, const TernSlot* __restrict__ w, const float* __restrict__ u, uint64_t seed,
     int8_t* __restrict__ codes, float* __restrict__ out, const float* __restrict__ clip_in,
-    float* __restrict__ scalars) {
+    float* __restrict__ scalars, int64_t unit0 = 0, int64_t xoff = 0) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, unit_off, nseg);
-  const int64_t unit = blockIdx.x;
+  const int64_t unit = unit0 + blockIdx.x;
   const int s = find_seg(sv.sub, nseg, unit);
   const int64_t base = sv.seg[s] + (unit - sv.sub[s]) * kTernUnit;
   const int64_t end = min(base + (int64_t)kTernUnit, sv.seg[s + 1]);
-  const QuadSplit qs = quad_split(base, end);
+  const QuadSplit qs = quad_split_ph(base, end, xoff & 3);
+  // x, u, codes and out hold the elements from global xoff on (a shard); indexed globally below
+  x -= xoff;
+  if constexpr (HAS_U) u -= xoff;
+  if constexpr (FUSED) out -= xoff;
+  else codes -= xoff;
   const int t = threadIdx.x;
   const int64_t nq = (qs.a1 - qs.a0) >> 2;
   // The unit's quads in kTernSteps sub-chunks of kTernSub per thread, software pipelined: the next
@@ -1245,7 +1263,7 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
       c = (float)(2.5 * (double)(float)sqrt(var));
     }
     scalar = (q.nan || c != c) ? __int_as_float(0x7FC00000) : fminf(q.amax, c);   // (NaN bound: NaN)
-    if (t == 0 && unit == sv.sub[s]) scalars[s] = scalar;
+    if (t == 0 && unit == sv.sub[s] && scalars) scalars[s] = scalar;
   } else {
     const TernScale sc = w[sv.sub[s]].scale;   // published by the segment's last stats unit
     c = sc.c;
@@ -1328,6 +1346,40 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
       if (jq < nqi) encode_quad(jq, curb[k]);
     }
   }
+}
+
+// Every segment's scalar from the per-unit partials in w -- the encoder's reduction verbatim (a
+// kTernBlock workgroup, the units in the same thread order, block_tern_reduce), so the scalars are
+// bit-identical to the ones the single-GPU encoder publishes.  Sharded TernGrad: every rank derives
+// all scalars after the slot all-gather, none travels.
+__global__ __launch_bounds__(kTernBlock) void tern_scalars_kernel(const int64_t* __restrict__ seg_off,
+                                                                  const int64_t* __restrict__ unit_off,
+                                                                  const TernSlot* __restrict__ w,
+                                                                  const float* __restrict__ clip_in,
+                                                                  float* __restrict__ scalars) {
+  const int s = blockIdx.x;
+  const int t = threadIdx.x;
+  const int64_t u0 = unit_off[s], u1 = unit_off[s + 1];
+  if (u0 == u1) return;   // an empty segment has no units (the encoder publishes nothing either)
+  double ps = 0.0, pq = 0.0;
+  float pm = 0.f;
+  uint32_t pn = 0;
+  for (int64_t j = u0 + t; j < u1; j += kTernBlock) {
+    const TernPartial pj = w[j].part;
+    ps += pj.sum; pq += pj.sq; pm = fmaxf(pm, pj.amax); pn |= pj.nan;
+  }
+  const TernPartial q = block_tern_reduce<kTernBlock>(ps, pq, pm, pn);
+  float c;
+  if (clip_in) {
+    c = clip_in[s];
+  } else {
+    const double nn = (double)(seg_off[s + 1] - seg_off[s]);
+    const double mean = q.sum / nn;
+    double var = q.sq / nn - mean * mean;
+    if (var < 0.0) var = 0.0;
+    c = (float)(2.5 * (double)(float)sqrt(var));
+  }
+  if (t == 0) scalars[s] = (q.nan || c != c) ? __int_as_float(0x7FC00000) : fminf(q.amax, c);
 }
 
 // Row decoder: a 16-lane row owns a 128-element chunk of the flat buffer (each lane the quads l16
@@ -2035,6 +2087,50 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
     tern_encode_kernel<false, false><<<(unsigned)nunits, kTernBlock, 0, as_stream(stream)>>>(
         x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, scalars);
   GRACE_CHECK_LAUNCH("grace_terngrad_compress");
+  return GRACE_OK;
+}
+
+int32_t grace_terngrad_slot_bytes(void) { return (int32_t)sizeof(TernSlot); }
+
+grace_status_t grace_terngrad_shard_stats(const float* x, int64_t xoff, const int64_t* seg_off,
+                                          const int64_t* unit_off, int32_t nseg, int64_t unit0, int64_t nunits_local,
+                                          void* ws, void* stream) {
+  GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && unit0 >= 0 && nunits_local >= 0 && xoff >= 0 && ws &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+                "grace_terngrad_shard_stats: bad arguments (16-B aligned shard)");
+  if (nunits_local == 0) return GRACE_OK;
+  tern_stats_kernel<<<(unsigned)nunits_local, kQBlock, 0, as_stream(stream)>>>(
+      x, seg_off, unit_off, nseg, nullptr, reinterpret_cast<TernSlot*>(ws), nullptr, unit0, xoff);
+  GRACE_CHECK_LAUNCH("grace_terngrad_shard_stats");
+  return GRACE_OK;
+}
+
+grace_status_t grace_terngrad_shard_encode(const float* x, int64_t xoff, const int64_t* seg_off,
+                                           const int64_t* unit_off, int32_t nseg, int64_t unit0,
+                                           int64_t nunits_local, const float* clip_in, const float* u, uint64_t seed,
+                                           int8_t* codes, const void* ws, void* stream) {
+  GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && unit0 >= 0 && nunits_local >= 0 && xoff >= 0 && codes &&
+                    ws && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(u) |
+                            reinterpret_cast<uintptr_t>(codes)) & 15) == 0,
+                "grace_terngrad_shard_encode: bad arguments (16-B aligned shard, u and codes)");
+  if (nunits_local == 0) return GRACE_OK;
+  const TernSlot* w = reinterpret_cast<const TernSlot*>(ws);
+  if (u)
+    tern_encode_kernel<false, true><<<(unsigned)nunits_local, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, nullptr, unit0, xoff);
+  else
+    tern_encode_kernel<false, false><<<(unsigned)nunits_local, kTernBlock, 0, as_stream(stream)>>>(
+        x, seg_off, unit_off, nseg, w, u, seed, codes, nullptr, clip_in, nullptr, unit0, xoff);
+  GRACE_CHECK_LAUNCH("grace_terngrad_shard_encode");
+  return GRACE_OK;
+}
+
+grace_status_t grace_terngrad_scalars(const int64_t* seg_off, const int64_t* unit_off, int32_t nseg,
+                                      const float* clip_in, const void* ws, float* scalars, void* stream) {
+  GRACE_REQUIRE(seg_off && unit_off && nseg >= 1 && ws && scalars, "grace_terngrad_scalars: bad arguments");
+  tern_scalars_kernel<<<(unsigned)nseg, kTernBlock, 0, as_stream(stream)>>>(
+      seg_off, unit_off, reinterpret_cast<const TernSlot*>(ws), clip_in, scalars);
+  GRACE_CHECK_LAUNCH("grace_terngrad_scalars");
   return GRACE_OK;
 }
 

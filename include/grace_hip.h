@@ -262,6 +262,25 @@ grace_status_t grace_terngrad_compress(const float* x, const int64_t* seg_off, c
 grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, const int64_t* unit_off, int32_t nseg,
                                      int64_t nunits, const float* clip_in, const float* u, uint64_t seed,
                                      float* scalars, void* ws, float* out, void* stream);
+/* Sharded TernGrad (grace_amd/dist/sharded_terngrad.py).  One bucket's work units are
+ * split over the ranks in contiguous blocks; a rank runs the GLOBAL units [unit0, unit0 +
+ * nunits_local) of the bucket's tables, whose elements start at global element xoff (x, u and codes
+ * point there, 16-B aligned).  ws = the GLOBAL slot array (grace_terngrad_workspace_bytes(nunits),
+ * grace_terngrad_slot_bytes() per unit): shard_stats writes this rank's units' slots; after the
+ * caller has all-gathered every rank's slots into it, shard_encode writes this rank's codes with
+ * every segment's scale reduced exactly as the single-GPU encoder (bit-identical codes), and
+ * grace_terngrad_scalars derives every segment's scalar the same way (nothing but the slots
+ * travels before the codes). */
+int32_t grace_terngrad_slot_bytes(void);
+grace_status_t grace_terngrad_shard_stats(const float* x, int64_t xoff, const int64_t* seg_off,
+                                          const int64_t* unit_off, int32_t nseg, int64_t unit0, int64_t nunits_local,
+                                          void* ws, void* stream);
+grace_status_t grace_terngrad_shard_encode(const float* x, int64_t xoff, const int64_t* seg_off,
+                                           const int64_t* unit_off, int32_t nseg, int64_t unit0,
+                                           int64_t nunits_local, const float* clip_in, const float* u, uint64_t seed,
+                                           int8_t* codes, const void* ws, void* stream);
+grace_status_t grace_terngrad_scalars(const int64_t* seg_off, const int64_t* unit_off, int32_t nseg,
+                                      const float* clip_in, const void* ws, float* scalars, void* stream);
 grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scalars, int64_t code_stride,
                                          int64_t scal_stride, int32_t world, const int64_t* seg_off,
                                          int32_t nseg, int64_t n, int32_t aggregate, float divisor, float* out,
