@@ -55,6 +55,7 @@ SIGNATURES = {
     "grace_topk_step_dense": (ST, [P, I64, I64, P, P, P, P, I64, P, SZ, P]),
     "grace_topk_residual_step": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, SZ, P]),
     "grace_topk_carry_size": (I64, [I64, I64]),
+    "grace_topk_residual_step_swap": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, I64, I32, P, SZ, P]),
     "grace_topk_residual_step_carry": (ST, [P, P, I32, F32, F32, I64, I64, P, P, P, P, I64, I32, P, I64, P, SZ, P]),
     "grace_topk_segmented_small_max": (I32, []),
     "grace_topk_segmented_chunk": (I64, [I32, I32]),

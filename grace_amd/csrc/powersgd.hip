@@ -1230,6 +1230,24 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
   // rather than 4 S scattered 16-row runs)
   const int64_t L = 4 * (int64_t)S;
   bool qstaged = false;
+  // q rows of this column group: loaded BEFORE M's rows, so that staging them into LDS waits only
+  // for this one older load (vmcnt counts in order).  Loaded after them (r04), the staging waited
+  // for all 16 rows of M first, and the q load was issued only then (a spilled address reload
+  // with vmcnt(0) in front of it): one full memory latency per workgroup on the critical path.
+  f32x4v qr = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int64_t jq = (int64_t)cg * kW1Cols + threadIdx.x;
+    if (jq < m) {
+      if constexpr (DRAWQ) {
+        float z0, z1, z2, z3;
+        normal_pair(seed, (uint64_t)jq * 2, z0, z1);
+        normal_pair(seed, (uint64_t)jq * 2 + 1, z2, z3);
+        qr = f32x4v{z0, z1, z2, z3};
+      } else {
+        qr = *reinterpret_cast<const f32x4v*>(q + 4 * jq);
+      }
+    }
+  }
   for (int s = sy; s < S; s += SG) {
     const int64_t lrow = 4 * (int64_t)s + rw;
     f32x4v v[kW1Rows];
@@ -1247,20 +1265,8 @@ __global__ __launch_bounds__(kW1Block) void psgd_w1_pass(const float* __restrict
       v[d] = *reinterpret_cast<const f32x4v*>(rowp + jo);
 #endif
     }
-    if (!qstaged) {   // q rows of the group into LDS (drawn or loaded) while M's loads are in flight
+    if (!qstaged) {   // q rows of the group into LDS while M's loads are in flight
       qstaged = true;
-      const int64_t jq = (int64_t)cg * kW1Cols + threadIdx.x;
-      f32x4v qr = {0.f, 0.f, 0.f, 0.f};
-      if (jq < m) {
-        if constexpr (DRAWQ) {
-          float z0, z1, z2, z3;
-          normal_pair(seed, (uint64_t)jq * 2, z0, z1);
-          normal_pair(seed, (uint64_t)jq * 2 + 1, z2, z3);
-          qr = f32x4v{z0, z1, z2, z3};
-        } else {
-          qr = *reinterpret_cast<const f32x4v*>(q + 4 * jq);
-        }
-      }
       qsh[threadIdx.x] = qr;
     }
     // no masking of v (a masked copy would double the rows' registers): a column past m has zero

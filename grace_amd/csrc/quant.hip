@@ -1285,13 +1285,34 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
     if constexpr (FUSED) out[i] = 0.f + (float)cd * scalar;
     else codes[i] = cd;
   };
+  // The device generator draws a quad's four uniforms at once (uniform01x4 at the GLOBAL quad index,
+  // a multiple of 4) and a unit's head / tail elements one by one: so element e's draw depends on
+  // the unit's globally aligned split, not on where a shard's quads fall.  u1(e) is that draw; a
+  // shard whose quads are out of phase with the global quads (ph != 0) composes each of its quads
+  // from the two global quads it straddles.
+  const QuadSplit gq = quad_split(base, end);   // the single-GPU encoder's split of this unit
+  const int64_t ph = xoff & 3;
+  const bool key32 = qs.a1 <= ((int64_t)1 << 32) && gq.a1 <= ((int64_t)1 << 32);
+  const uint64_t key = mix64(seed);
+  auto quad_u = [&](int64_t q, float (&r4)[4]) {
+    if (key32) uniform01x4_k(key, (uint32_t)q, r4);
+    else uniform01x4(seed, (uint64_t)q, r4);
+  };
+  // lane j of a register quad by selects (a dynamic index would put the array in scratch memory)
+  auto pick = [](const float (&a)[4], int64_t j) { return j == 0 ? a[0] : (j == 1 ? a[1] : (j == 2 ? a[2] : a[3])); };
+  auto u1 = [&](int64_t e) -> float {
+    if (e < gq.a0 || e >= gq.a1) return uniform01(seed, (uint64_t)e);
+    float r4[4];
+    quad_u(e & ~(int64_t)3, r4);
+    return pick(r4, e & 3);
+  };
   if (base + t < qs.a0) {
     const int64_t i = base + t;
-    put1(i, enc(x[i], HAS_U ? u[i] : uniform01(seed, (uint64_t)i)));
+    put1(i, enc(x[i], HAS_U ? u[i] : u1(i)));
   }
   if (qs.a1 + t < end) {
     const int64_t i = qs.a1 + t;
-    put1(i, enc(x[i], HAS_U ? u[i] : uniform01(seed, (uint64_t)i)));
+    put1(i, enc(x[i], HAS_U ? u[i] : u1(i)));
   }
   // The quads: the same codes as enc() with fewer instructions.  With s = scalar > 0 (then
   // c >= scalar > 0): enc() is sign(x) where u s < min(|x|, c) and 0 elsewhere (x = +-0 never
@@ -1300,8 +1321,6 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
   // 0x01 or 0xFF from its sign bit.  32-bit quad offsets; the generator key is hoisted
   // (uniform01x4_k = uniform01x4 for element indices below 2^32).
   const float sc_eff = scalar > 0.f ? scalar : __int_as_float(0x7FC00000);
-  const bool key32 = qs.a1 <= ((int64_t)1 << 32);
-  const uint64_t key = mix64(seed);
   auto codes4 = [&](const f4v& v, const f4v& uu) -> uint32_t {
     uint32_t cw = 0;
 #pragma unroll
@@ -1319,8 +1338,19 @@ __global__ __launch_bounds__(kTernBlock) void tern_encode_kernel(
       uu = *reinterpret_cast<const f4v*>(u + i);
     } else {
       float r4[4];
-      if (key32) uniform01x4_k(key, (uint32_t)i, r4);
-      else uniform01x4(seed, (uint64_t)i, r4);
+      if (ph == 0) {   // (the whole-bucket encoder: its quads are the global quads)
+        quad_u(i, r4);
+      } else {
+        float ra[4], rb[4];
+        quad_u(i - ph, ra);
+        quad_u(i - ph + 4, rb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t e = i + j;
+          const float qv = j < 4 - ph ? pick(ra, (ph + j) & 3) : pick(rb, (j + ph) & 3);
+          r4[j] = (e < gq.a0 || e >= gq.a1) ? uniform01(seed, (uint64_t)e) : qv;
+        }
+      }
       uu = f4v{r4[0], r4[1], r4[2], r4[3]};
     }
     const uint32_t cw = codes4(v, uu);

@@ -42,9 +42,16 @@ namespace grace {
 // dense outputs written by a top-k launch
 // kDenseOut: no memory (Allgather(TopK, NoneMemory) at world 1): t = g, only the dense output is
 // written next to the payload, the input stays read-only
-enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2, kDenseOut = 3 };
-template <int MODE> constexpr bool kWritesR = MODE == kDenseRes || MODE == kDenseFused;
+// kResSwap: the W > 1 residual step into a SECOND residual buffer (read g and r_in, write r; no dense
+// output): like kDenseFused the main pass writes every provisional pick (key > thr_mid) as selected
+// (r = t - t) and the finalize fixes up the candidates it decides otherwise, because t stays
+// recoverable from g and the untouched r_in; kDenseRes (in place) must keep t in r and zero the k
+// selected positions in the finalize instead (537 K scattered stores at 2^26, 1 %)
+enum DenseMode : int { kDenseNone = 0, kDenseRes = 1, kDenseFused = 2, kDenseOut = 3, kResSwap = 4 };
+template <int MODE> constexpr bool kWritesR = MODE == kDenseRes || MODE == kDenseFused || MODE == kResSwap;
 template <int MODE> constexpr bool kWritesOut = MODE == kDenseFused || MODE == kDenseOut;
+// the main pass writes provisional picks as selected; the finalize fixes up its candidates
+template <int MODE> constexpr bool kProv = kWritesOut<MODE> || MODE == kResSwap;
 
 #ifndef GRACE_MAIN_BLOCK
 #define GRACE_MAIN_BLOCK 256
@@ -305,6 +312,9 @@ struct StepArgs {
   // zeroes those and the main pass writes only the elements it selects (sparse), not 4 B each
   const int32_t* prev_idx;
   int64_t prev_count;
+  // the residual the step READS (kResSwap: a second buffer; every other mode: r itself, set by
+  // run_topk / seg_step_args)
+  const float* r_in;
 };
 
 // the carry is for large buckets, where the bracket's random reads cost (stratum >= 256)
@@ -315,7 +325,7 @@ __host__ __device__ __forceinline__ int64_t carry_thr_off(int64_t S) { return (S
 
 template <bool HAS_RES>
 __device__ __forceinline__ float compensate(const StepArgs& a, int64_t i) {
-  if constexpr (HAS_RES) return a.beta * a.r[i] + a.gamma * a.g[i];
+  if constexpr (HAS_RES) return a.beta * a.r_in[i] + a.gamma * a.g[i];
   return a.g[i];
 }
 
@@ -535,6 +545,7 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   const int64_t S = a.sample_n;
   const BracketRanks br = bracket_ranks(S, a.k, a.n);
   const uint32_t(&r1)[3] = br.r1;
+  const uint32_t rk0 = br.r1[0], rk1 = br.r1[1], rk2 = br.r1[2];
   // coarse: thread t owns kCPT consecutive bins from top down (descending); one block scan finds
   // the three coarse bins
   constexpr int kCPT = kCoarseBins / kBracketBlock;
@@ -576,7 +587,10 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
       if (j >= o) v += u;
     }
     const int qc = act ? q : 0;
-    const uint64_t bal = __ballot(act && s_fc[2 * qc + 1] + v >= r1[qc]);
+    // (selects of SSA values: a dynamic index, or selects of r1's elements that the compiler folds
+    // back into one, keep r1 in scratch memory)
+    const uint32_t rq = qc == 0 ? rk0 : (qc == 1 ? rk1 : rk2);
+    const uint64_t bal = __ballot(act && s_fc[2 * qc + 1] + v >= rq);
     const uint32_t hm = (uint32_t)(bal >> (16 * q)) & 0xFFFFu;
     if (act && j == __ffs(hm) - 1) s_res[q] = bin;
   }
@@ -641,7 +655,7 @@ __device__ __forceinline__ void load_group(const StepArgs& a, int64_t gbase, flo
 #pragma unroll
   for (int u = 0; u < kGroup; ++u) {
     const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
-    if constexpr (HAS_RES) rv[u] = ld4<FAST>(a.r, i0, a.n);
+    if constexpr (HAS_RES) rv[u] = ld4<FAST>(a.r_in, i0, a.n);
     gv[u] = ld4<FAST>(a.g, i0, a.n);
   }
 }
@@ -723,16 +737,18 @@ __device__ __forceinline__ uint32_t classify_group(const StepArgs& a, const Topk
       const uint32_t f_lo = kSkel ? 0u : (((key - lo) >> 31) ^ 1u) & vbit;         // key >= lo
       msure |= f_sure << (u * 4 + j);
       mcand |= (f_lo & (f_sure ^ 1u)) << (u * 4 + j);
-      if constexpr (kWritesOut<MODE>) {
+      if constexpr (kProv<MODE>) {
         // sure elements, and candidates above the provisional threshold, are written as selected;
         // the finalize fixes up only the candidates whose final decision differs.  lo <= mid <= hi
         // (bracket_publish), so "sure or (candidate and key > mid)" is key > mid: an all-ones
         // mask selects r' = t - t and out = 0 + t bitwise
         const uint32_t m = kSkel ? 0u : (uint32_t)((int32_t)(mid - key) >> 31) & (0u - vbit);
         set4(rout, j, u2f((f2u(tv - tv) & m) | (f2u(tv) & ~m)));
-        set4(dout, j, u2f(f2u(0.f + tv) & m));
-        // recycled output: only the selected elements are written (the rest is already zero)
-        if constexpr (SPARSE) if (m) a.out[i0 + j] = 0.f + tv;
+        if constexpr (kWritesOut<MODE>) {
+          set4(dout, j, u2f(f2u(0.f + tv) & m));
+          // recycled output: only the selected elements are written (the rest is already zero)
+          if constexpr (SPARSE) if (m) a.out[i0 + j] = 0.f + tv;
+        }
       }
     }
     if constexpr (kWritesR<MODE>) st4<FAST>(a.r, i0, n, rout);
@@ -993,8 +1009,10 @@ __device__ __forceinline__ int2 ld_i2(const int2* p) {
 template <int MODE, bool AG>
 struct MainTs {
   const float* g; const float* r; const float* out;
+  const float* rin; float beta, gamma;   // kResSwap: t recomputed from g and the untouched r_in
   __device__ float operator()(int64_t i) const {
     if constexpr (MODE == kDenseNone || MODE == kDenseOut) return g[i];
+    if constexpr (MODE == kResSwap) return rin ? beta * rin[i] + gamma * g[i] : g[i];
     if constexpr (MODE == kDenseRes) return ld_f32<AG>(r + i);
     const float o = ld_f32<AG>(out + i), rr = ld_f32<AG>(r + i);   // both issued: no dependent load
     return f2u(o) != 0u ? o : rr;
@@ -1005,6 +1023,13 @@ struct MainTs {
       return make_float4((*this)(i), (*this)(i + 1), (*this)(i + 2), (*this)(i + 3));
     } else {
       if constexpr (MODE == kDenseNone || MODE == kDenseOut) return *reinterpret_cast<const float4*>(g + i);
+      if constexpr (MODE == kResSwap) {
+        const float4 gg = *reinterpret_cast<const float4*>(g + i);
+        if (!rin) return gg;
+        const float4 rr = *reinterpret_cast<const float4*>(rin + i);
+        return make_float4(beta * rr.x + gamma * gg.x, beta * rr.y + gamma * gg.y, beta * rr.z + gamma * gg.z,
+                           beta * rr.w + gamma * gg.w);
+      }
       if constexpr (MODE == kDenseRes) return *reinterpret_cast<const float4*>(r + i);
       const float4 o = *reinterpret_cast<const float4*>(out + i), rr = *reinterpret_cast<const float4*>(r + i);
       return make_float4(f2u(o.x) != 0u ? o.x : rr.x, f2u(o.y) != 0u ? o.y : rr.y, f2u(o.z) != 0u ? o.z : rr.z,
@@ -1035,11 +1060,11 @@ __device__ __forceinline__ bool boundary_preload(const TopkWs& w, bool ok, uint3
 // boundary-bin entry not selected: in the fused mode undo a provisional selection (key > mid)
 template <int MODE>
 __device__ __forceinline__ void unselect(const StepArgs& a, int2 e, uint32_t mid) {
-  if constexpr (kWritesOut<MODE>) {
+  if constexpr (kProv<MODE>) {
     const float v = u2f((uint32_t)e.y);
     if (abs_key(v) > mid) {
       if constexpr (kWritesR<MODE>) a.r[e.x] = v;
-      a.out[e.x] = 0.f;
+      if constexpr (kWritesOut<MODE>) a.out[e.x] = 0.f;
     }
   }
 }
@@ -1098,7 +1123,7 @@ __device__ void boundary_work(const StepArgs& a, const TopkWs& w, bool ok, uint3
   }
   // ---- exact fallback over the whole bucket (bracket failed or a list overflowed)
   if (threadIdx.x == 0) w.ctl->status = 1;
-  const MainTs<MODE, AG> f{a.g, a.r, a.out};
+  const MainTs<MODE, AG> f{a.g, a.r, a.out, a.r_in != a.r ? a.r_in : nullptr, a.beta, a.gamma};
   auto src = [f](int64_t i) { return comp_key(abs_key(f(i)), (uint32_t)i); };
   const uint64_t T = block_select_comp<BLOCK>(src, a.n, k, fs.hist, fs.s_w, fs.s_res);
   if (threadIdx.x == 0) carry_threshold(a, T);
@@ -1119,16 +1144,16 @@ __device__ __forceinline__ void write_round(const StepArgs& a, const int2 (&e)[k
       a.vals[ps] = v;
       a.idx[ps] = (int32_t)(e[u].x + a.idx_base);
       if constexpr (MODE == kDenseRes) a.r[e[u].x] = v - v;
-      if constexpr (kWritesOut<MODE>) {
+      if constexpr (kProv<MODE>) {
         if (!above_mid) {
           if constexpr (kWritesR<MODE>) a.r[e[u].x] = v - v;
-          a.out[e[u].x] = 0.f + v;
+          if constexpr (kWritesOut<MODE>) a.out[e[u].x] = 0.f + v;
         }
       }
       ++ps;
-    } else if (kWritesOut<MODE> && ((fbelow >> u) & 1u) && above_mid) {
+    } else if (kProv<MODE> && ((fbelow >> u) & 1u) && above_mid) {
       if constexpr (kWritesR<MODE>) a.r[e[u].x] = v;
-      a.out[e[u].x] = 0.f;
+      if constexpr (kWritesOut<MODE>) a.out[e[u].x] = 0.f;
     }
   }
 #ifdef GRACE_STAMPS   // diagnostic: fix-up writes of this round (ctl stamp slot 18: selected below mid, 19: rejected above)
@@ -1229,7 +1254,7 @@ __device__ void parallel_exact(const StepArgs& a, const TopkWs& w, int fcnt, Fin
   L = L < kFbSliceMin ? kFbSliceMin : ((L + 3) & ~(int64_t)3);
   const uint32_t nsl = (uint32_t)((a.n + L - 1) / L);
   if (t == 0) __hip_atomic_fetch_max(&w.ctl->status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const MainTs<MODE, AG> f{a.g, a.r, a.out};
+  const MainTs<MODE, AG> f{a.g, a.r, a.out, a.r_in != a.r ? a.r_in : nullptr, a.beta, a.gamma};
   auto bounds = [&](uint32_t s, int64_t& s0, int64_t& q1, int64_t& s1) {
     s0 = (int64_t)s * L;
     s1 = s0 + L < a.n ? s0 + L : a.n;
@@ -1488,7 +1513,7 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
     STAMP_IF(fi == 0, w.ctl, 9);
     // fused mode, no candidate needed (k sure elements): every candidate is unselected, but the
     // provisionally selected ones still need their fix-ups -> route with the boundary above all bins
-    if (kWritesOut<MODE> && B < 0) B = kHistBins;
+    if (kProv<MODE> && B < 0) B = kHistBins;
     // residual-only mode: sure entries still hold t in r; zero them now
     // (kFinPer entries per thread per round, every load issued before any store: one dependent
     // load -> store chain per entry made this 14 us of the finalize at k = 671 K)
@@ -1610,6 +1635,7 @@ __global__ __launch_bounds__(256) void topk_all(StepArgs a) {
 
 template <bool HAS_RES, int MODE>
 static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s) {
+  if (!a.r_in) a.r_in = a.r;
   if (a.n <= kSmallN) {
     topk_small<HAS_RES, MODE><<<1, kSelBlock, 0, s>>>(a);
     GRACE_CHECK_LAUNCH("topk_small");
@@ -1765,6 +1791,7 @@ __device__ __forceinline__ StepArgs seg_step_args(const SegPlan& p, int s) {
   StepArgs a{};
   a.g = p.g + o;
   a.r = p.r + o;
+  a.r_in = a.r;
   a.beta = p.beta;
   a.gamma = p.gamma;
   a.n = p.seg_off[s + 1] - o;
@@ -1953,11 +1980,10 @@ __global__ __launch_bounds__(kMainBlock, 4) void seg_main_kernel(SegPlan p) {
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
   __syncthreads();
   uint32_t wfill;
+  // (no beta = gamma = 1 instantiation here: next to the segment bookkeeping it pushed this kernel
+  // to 128 VGPRs and 96 B of scratch per lane)
   if (VEC && (p.seg_off[s] & 3) == 0 && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n) {
-    if (HAS_RES && a.beta == 1.f && a.gamma == 1.f)
-      wfill = main_chunk_v2<HAS_RES, MODE, VEC, false, false, true>(a, w, sm, lo, hi, sh, mid, chunk);
-    else
-      wfill = main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
+    wfill = main_chunk_v2<HAS_RES, MODE, VEC>(a, w, sm, lo, hi, sh, mid, chunk);
   } else {
     wfill = main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
   }
@@ -2035,6 +2061,7 @@ grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int
   GRACE_REQUIRE(ws_bytes_ >= ws_bytes(n, 1), "grace_topk_stream_probe: workspace too small");
   TopkWs w = carve(ws, n, 1);
   StepArgs a{g, r, 1.f, 1.f, n, 1, nullptr, nullptr, out};
+  a.r_in = r;
   const unsigned nblk = (unsigned)((n + kChunkOf<true, kDenseFused> - 1) / kChunkOf<true, kDenseFused>);
   // timed like the real pass (the event timer rides on the dispatch packet when it is enabled)
   if (sparse)   // the recycled-output layout: g, r read, r' written, out untouched
@@ -2204,6 +2231,28 @@ grace_status_t grace_topk_residual_step_carry(const float* g, float* residual, i
   }
   return has_residual ? run_topk<true, kDenseRes>(a, ws, ws_bytes_, s)
                       : run_topk<false, kDenseRes>(a, ws, ws_bytes_, s);
+}
+
+grace_status_t grace_topk_residual_step_swap(const float* g, const float* r_in, int32_t has_residual, float beta,
+                                             float gamma, int64_t n, int64_t k, float* vals, int32_t* idx,
+                                             float* r_out, float* carry, int64_t carry_len, int32_t carry_valid,
+                                             void* ws, size_t ws_bytes_, void* stream) {
+  GRACE_REQUIRE(g && r_out && (!has_residual || r_in) && r_in != r_out && vals && idx && n > 0 && k >= 1 &&
+                    k <= n && n < (int64_t)1 << 31,
+                "grace_topk_residual_step_swap: bad arguments (r_in and r_out distinct)");
+  GRACE_REQUIRE(!carry || carry_len >= grace_topk_carry_size(n, k),
+                "grace_topk_residual_step_swap: carry shorter than grace_topk_carry_size(n, k)");
+  GRACE_REQUIRE(n <= kSmallN || ws, "grace_topk_residual_step_swap: workspace required");
+  StepArgs a{g, r_out, beta, gamma, n, k, vals, idx, nullptr};
+  a.r_in = has_residual ? r_in : nullptr;
+  if (carry && grace_topk_carry_size(n, k) > 0) {
+    a.rs_out = carry;
+    a.rs_in = has_residual && carry_valid ? carry : nullptr;
+  }
+  hipStream_t s = as_stream(stream);
+  if (has_residual) return run_topk<true, kResSwap>(a, ws, ws_bytes_, s);
+  a.r_in = a.r;   // (never read without a residual; distinct from nothing)
+  return run_topk<false, kResSwap>(a, ws, ws_bytes_, s);
 }
 
 grace_status_t grace_sparse_decode(const float* vals, const int32_t* idx, int64_t count, float* out,

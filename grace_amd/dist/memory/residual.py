@@ -33,6 +33,31 @@ class ResidualMemory(Memory):
                 self._carries = {}
             self._carries[name] = (carry, weakref.ref(residual), residual._version)
 
+    def spare_for(self, name, like):
+        """A buffer for this step's NEW residual (the world > 1 top-k step writes it beside the old
+        one, ops.topk_residual_step_swap): the name's residual before the current one, retired by
+        the last step, when nothing outside this memory holds it or a view of it (the reference
+        allocates a new residual every step, so a caller that kept an old one keeps its values);
+        otherwise a new tensor."""
+        spare = getattr(self, "_spare", None)
+        ent = spare.pop(name, None) if spare else None
+        if ent is not None:
+            buf, cdata, _st = ent
+            # references to buf: the popped tuple, the local name, getrefcount's argument
+            if (buf.numel() == like.numel() and buf.device == like.device and ops._getrefcount(buf) == 3
+                    and ops._storage_uses(cdata) == 2):
+                return buf
+        return torch.empty_like(like)
+
+    def retire(self, name, old):
+        """Keep `name`'s previous residual as the next step's spare_for buffer."""
+        if old is None:
+            return
+        if getattr(self, "_spare", None) is None:
+            self._spare = {}
+        st = old.untyped_storage()
+        self._spare[name] = (old, st._cdata, st)
+
     def compensate(self, tensor, name):
         """t = beta * r + gamma * g; the first step returns the tensor itself (residual.py:10-14)."""
         if name in self.residuals:
@@ -52,3 +77,4 @@ class ResidualMemory(Memory):
     def load_state_dict(self, state):
         self.residuals = {k: v.clone() for k, v in state.items()}
         self._carries = {}
+        self._spare = {}

@@ -367,6 +367,22 @@ def topk_residual_step(g, residual, has_residual, beta, gamma, k, out=None, payl
     return buf, vals, idx
 
 
+def topk_residual_step_swap(g, residual, has_residual, beta, gamma, k, residual_out, payload=None, carry=None,
+                            carry_valid=False):
+    """The world > 1 residual step into a second residual buffer (grace_topk_residual_step_swap):
+    reads g and `residual`, writes `residual_out` (distinct) and the payload."""
+    g = dev_f32(g)
+    n = g.numel()
+    buf, vals, idx = new_payload(k, g.device) if payload is None else payload
+    ws = topk_workspace(n, k, g.device)
+    if residual_out is None or residual_out.data_ptr() == (residual.data_ptr() if residual is not None else 0):
+        raise ValueError("grace_amd: topk_residual_step_swap needs a distinct residual_out")
+    _lib.call("grace_topk_residual_step_swap", _p(g), _p(residual) if has_residual else None, 1 if has_residual else 0,
+              float(beta), float(gamma), n, k, _p(vals), _p(idx), _p(residual_out), _p(carry),
+              carry.numel() if carry is not None else 0, 1 if carry_valid else 0, _p(ws), ws.numel(), _stream())
+    return buf, vals, idx
+
+
 @functools.lru_cache(maxsize=256)
 def topk_carry_size(n, k):
     """Length of the residual-sample carry for an (n, k) step, 0 where the step has none."""

@@ -143,6 +143,17 @@ grace_status_t grace_onebit_decode(const uint8_t* mask0, const float* mean0_dev,
  * among equal |t|); same set as torch.topk(sorted=False) (topk.py:36) modulo ties at the k-th
  * value.  Payload layout = reference's [values f32[k], indices int32[k]] (topk.py:41-42). */
 size_t grace_topk_workspace_bytes(int64_t n, int64_t k);
+/* The world > 1 residual step with the new residual written to a SECOND buffer (ResidualMemory's
+ * update, residual.py:16-20, allocates a new tensor too): reads g and r_in, writes r_out and the
+ * payload; r_out = t - decompress(compress(t)) exactly as grace_topk_residual_step leaves the
+ * residual in place, but the main pass zeroes its provisional picks at once and the finalize fixes
+ * up only the candidates it decides otherwise (t stays recoverable from g and r_in), instead of
+ * zeroing every selected position afterwards.  has_residual = 0: t = g (r_in unused).  carry as
+ * grace_topk_residual_step_carry (kept with the residual it describes: r_out after this step). */
+grace_status_t grace_topk_residual_step_swap(const float* g, const float* r_in, int32_t has_residual, float beta,
+                                             float gamma, int64_t n, int64_t k, float* vals, int32_t* idx,
+                                             float* r_out, float* carry, int64_t carry_len, int32_t carry_valid,
+                                             void* ws, size_t ws_bytes, void* stream);
 /* TopKCompressor.compress on its own: x is only read. */
 grace_status_t grace_topk_compress(const float* x, int64_t n, int64_t k, float* vals, int32_t* idx,
                                    void* ws, size_t ws_bytes, void* stream);

@@ -306,3 +306,29 @@ def test_topk_fallback_runout_raises():
     sel[oi] = True
     o = _np(out)
     assert same_bits(o[sel], g0[sel]) and not np.any(o[~sel])
+
+
+@pytest.mark.parametrize("n,case", [(1 << 22, "normal"), ((1 << 22) + 3, "normal"), (1 << 22, "sparse"),
+                                    (20000, "normal"), (100003, "ties"), ((1 << 20) + 1, "special")])
+def test_topk_residual_step_swap_equals_in_place(n, case):
+    """The world > 1 step into a second residual buffer (grace_topk_residual_step_swap: provisional
+    picks zeroed in the main pass, finalize fix-ups from t = g + r_in) leaves exactly the residual
+    and payload of the in-place step, over a 3-step chain (first step without a residual, then
+    with), including the exact fallback (sparse) and the single-workgroup path (n <= 32768);
+    r_in is never written."""
+    from grace_amd import ops
+    k = O.ratio_k(n, 0.01)
+    r_a = torch.zeros(n, device=DEV)              # in place
+    r_b = [torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)]
+    for step in range(3):
+        g0 = _inputs(n, case, 40 + step)
+        g = torch.from_numpy(g0).to(DEV)
+        _, va, ia = ops.topk_residual_step(g, r_a, step > 0, 1.0, 1.0, k, out=None)
+        r_in, r_out = r_b[step % 2], r_b[(step + 1) % 2]
+        before = r_in.clone()
+        _, vb, ib = ops.topk_residual_step_swap(g, r_in, step > 0, 1.0, 1.0, k, r_out)
+        torch.cuda.synchronize()
+        assert same_bits(_np(r_in), _np(before)), "r_in was written"
+        assert same_bits(_np(r_out), _np(r_a)), (step, "residual differs")
+        sa, sb = _sorted_payload(va, ia), _sorted_payload(vb, ib)
+        assert np.array_equal(sa[1], sb[1]) and same_bits(sa[0], sb[0]), (step, "payload differs")

@@ -32,12 +32,18 @@ def ev():
     return torch.cuda.Event(enable_timing=True)
 
 
+SWAP = os.environ.get("SWAP", "1") == "1"   # the r05 step into a second residual buffer
+rs2 = [torch.empty_like(r) for r in rs] if SWAP else None
 res = {"main_step": [], "sort": [], "decode": [], "total": []}
 for rnd in range(12):
     j = rnd % 3
     e = [ev() for _ in range(4)]
     e[0].record()
-    buf, _, _ = ops.topk_residual_step(gs[j], rs[j], True, 1.0, 1.0, k, out=None)
+    if SWAP:
+        buf, _, _ = ops.topk_residual_step_swap(gs[j], rs[j], True, 1.0, 1.0, k, rs2[j])
+        rs[j], rs2[j] = rs2[j], rs[j]
+    else:
+        buf, _, _ = ops.topk_residual_step(gs[j], rs[j], True, 1.0, 1.0, k, out=None)
     e[1].record()
     sb = ops.sort_payload(buf, k, n)
     e[2].record()
@@ -49,4 +55,4 @@ for rnd in range(12):
         res["sort"].append(e[1].elapsed_time(e[2]) * 1e3)
         res["decode"].append(e[2].elapsed_time(e[3]) * 1e3)
         res["total"].append(e[0].elapsed_time(e[3]) * 1e3)
-print({"W": W, **{kk: round(statistics.median(v), 1) for kk, v in res.items()}}, flush=True)
+print({"W": W, "swap": SWAP, **{kk: round(statistics.median(v), 1) for kk, v in res.items()}}, flush=True)
