@@ -59,8 +59,10 @@ class NativeShardKernels:
     def record_words(self, cap):
         return ops.shard_record_words(cap)
 
-    def local_step(self, g, res, has_res, k_loc, vals, idx):
-        ops.topk_residual_step(g, res, has_res, 1.0, 1.0, k_loc, out=None, payload=(None, vals, idx))
+    def local_step(self, g, res, has_res, k_loc, vals, idx, res_out):
+        # the new residual into a second buffer: the main pass zeroes its provisional picks at
+        # once instead of the finalize zeroing every selected position (grace_topk_residual_step_swap)
+        ops.topk_residual_step_swap(g, res, has_res, 1.0, 1.0, k_loc, res_out, payload=(None, vals, idx))
 
     select = staticmethod(ops.shard_select)
     clear = staticmethod(ops.shard_clear)
@@ -133,6 +135,7 @@ class ShardedTopK:
         self.residuals = {}
         self._plans = {}
         self._side = {}
+        self._spare = {}              # name -> the residual before the current one (next step's output buffer)
         self._status = {}             # device -> (two pinned status words, their select events)
         self._nstep = 0               # steps of this engine (all names): the status word parity
         self.last_payload = None      # (vals, idx) of this rank's record: idx = global index, or -1
@@ -209,6 +212,15 @@ class ShardedTopK:
             bits |= self.k_ops.take_status(words[slot])
         self._raise_bits(bits)
 
+    def _spare_residual(self, name, m, device):
+        ent = self._spare.pop(name, None)
+        if ent is not None:
+            buf, cdata, _st = ent
+            # references to buf: the popped tuple, the local name, getrefcount's argument
+            if buf.numel() == m and buf.device == device and ops._getrefcount(buf) == 3 and ops._storage_uses(cdata) == 2:
+                return buf
+        return torch.empty(m, dtype=torch.float32, device=device)
+
     def _side_stream(self, device):
         cur = torch.cuda.current_stream(device)
         side = self._side.get(cur.cuda_stream)
@@ -248,9 +260,11 @@ class ShardedTopK:
         plan = self._plan(name, m, dev, world, rank)
         res = self.residuals.get(name)
         has_res = res is not None and res.numel() == m
+        # this step's residual goes to a second buffer (the one the name had before the current one,
+        # when nobody outside holds it): the local step reads res and writes res_new
+        res_new = self._spare_residual(name, m, dev)
         if not has_res:
-            res = torch.empty(m, dtype=torch.float32, device=dev)
-            self.residuals[name] = res
+            res = None
         out_len = m if self.dense == "shard" else plan.n
         out_base = plan.base if self.dense == "shard" else 0
         recycle = self.recycle_output and dev.type == "cuda"
@@ -267,7 +281,12 @@ class ShardedTopK:
         cap = plan.cap
         vals = rec[K.HDR:K.HDR + cap].view(torch.float32)
         idx = rec[K.HDR + cap:K.HDR + 2 * cap]
-        K.local_step(g, res, has_res, min(cap, m), vals, idx)
+        K.local_step(g, res, has_res, min(cap, m), vals, idx, res_new)
+        if res is not None:
+            st = res.untyped_storage()
+            self._spare[name] = (res, st._cdata, st)
+        self.residuals[name] = res_new
+        res = res_new
         if world > 1:
             dist.all_gather_into_tensor(plan.recs, rec, group=self.group)
             recs = plan.recs

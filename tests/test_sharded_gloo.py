@@ -34,12 +34,12 @@ class OracleShardKernels:
     def record_words(self, cap):
         return HDR + 2 * cap
 
-    def local_step(self, g, res, has_res, k_loc, vals, idx):
+    def local_step(self, g, res, has_res, k_loc, vals, idx, res_out):
         t = O.residual_compensate(g.numpy().astype(np.float32), res.numpy() if has_res else None).ravel()
         v, i = O.topk_select(t, k_loc)
         r = t.copy()
         r[i] = t[i] - t[i]
-        res.copy_(torch.from_numpy(r))
+        res_out.copy_(torch.from_numpy(r))
         vals[:k_loc] = torch.from_numpy(np.asarray(v, np.float32))
         idx[:k_loc] = torch.from_numpy(np.asarray(i, np.int64).astype(np.int32))
 

@@ -31,6 +31,7 @@ gen = torch.Generator(device=dev)
 gen.manual_seed(5)
 g = torch.randn(n, device=dev, generator=gen)
 res = [torch.zeros(sizes[r], device=dev) for r in range(W)]
+res2 = [torch.zeros(sizes[r], device=dev) for r in range(W)]
 pay = [torch.full((cap,), -1, dtype=torch.int32, device=dev) for r in range(W)]
 st = ops.new_status_word()
 ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
@@ -43,8 +44,10 @@ for step in range(6):
         idx = recs[o + cap:o + 2 * cap]
         a, b = ev(), ev()
         a.record()
-        ops.topk_residual_step(g[bases[r]:bases[r] + sizes[r]], res[r], step > 0, 1.0, 1.0, min(cap, sizes[r]),
-                               out=None, payload=(None, vals, idx))
+        # (the product's local step: the new residual into a second buffer, ShardedTopK r05)
+        ops.topk_residual_step_swap(g[bases[r]:bases[r] + sizes[r]], res[r], step > 0, 1.0, 1.0, min(cap, sizes[r]),
+                                    res2[r], payload=(None, vals, idx))
+        res[r], res2[r] = res2[r], res[r]
         b.record()
         t_local.append((a, b))
     outs = []

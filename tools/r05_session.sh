@@ -36,6 +36,14 @@ for s in "$@"; do
           -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
       python3 tools/pmc_sq_summary.py $O/sq_head > $O/sq_head_summary.json; echo "sq summary rc=$?" ;;
     bench) run bench 300 python3 bench.py ;;
+    pytest) run pytest_gpu 1100 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    secondary)
+      : > $O/secondary.jsonl
+      for wl in ${WL:-topk_sharded ddp_segmented sign sign256 qsgd qsgd_step terngrad terngrad_step powersgd randomk threshold dgc topk_nomem}; do
+        st=20; case $wl in sign) st=200 ;; esac
+        run "bench_$wl" 300 python3 bench.py --workload $wl --steps $st --no-cpu-baseline
+        grep '^{' "$O/bench_$wl.log" | tail -1 >> $O/secondary.jsonl
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
