@@ -669,10 +669,10 @@ def bench_topk_sharded(args, world, rank, dev):
         per_gpu = 12.0 * m + 8.0 * k + 16.0 * world * k + 8.0 * k
     else:
         per_gpu = survey
-    traffic, ratio = pmc_traffic("topk_sharded", per_gpu) if world == 1 else (None, None)
+    traffic, t_ratio = pmc_traffic("topk_sharded", per_gpu) if world == 1 else (None, None)
     line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio,
+                        "traffic_over_algorithmic": t_ratio,
                         "algorithmic_bytes_per_gpu": per_gpu, "survey_bytes_per_gpu": survey,
                         "output": "recycled" if recycled else "dense zero-fill",
                         "recycled_steps": eng._recycler.hits}

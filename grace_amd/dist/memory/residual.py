@@ -44,7 +44,7 @@ class ResidualMemory(Memory):
         if ent is not None:
             buf, cdata, _st = ent
             # references to buf: the popped tuple, the local name, getrefcount's argument
-            if (buf.numel() == like.numel() and buf.device == like.device and ops._getrefcount(buf) == 3
+            if (ops.REUSE_OK and buf.numel() == like.numel() and buf.device == like.device and ops._getrefcount(buf) == 3
                     and ops._storage_uses(cdata) == 2):
                 return buf
         return torch.empty_like(like)

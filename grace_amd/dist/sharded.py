@@ -217,7 +217,8 @@ class ShardedTopK:
         if ent is not None:
             buf, cdata, _st = ent
             # references to buf: the popped tuple, the local name, getrefcount's argument
-            if buf.numel() == m and buf.device == device and ops._getrefcount(buf) == 3 and ops._storage_uses(cdata) == 2:
+            if (ops.REUSE_OK and buf.numel() == m and buf.device == device and ops._getrefcount(buf) == 3
+                    and ops._storage_uses(cdata) == 2):
                 return buf
         return torch.empty(m, dtype=torch.float32, device=device)
 

@@ -73,6 +73,43 @@ _getrefcount = __import__("sys").getrefcount
 _storage_uses = torch._C._storage_Use_Count
 
 
+def _refcount_selftest():
+    """Whether this interpreter and torch count references the way the output / residual reuse
+    checks assume (only CPython 3.10 / torch 2.10 were exercised).  Replays the exact
+    pattern of OutputRecycler.take -- an entry (tensor, storage cdata, storage) popped from a dict
+    and unpacked -- for a dropped tensor (must read "unheld": refcount 3, storage uses 2), a held one
+    and a held view (both must read "held").  Any other answer turns every reuse path off: the
+    callers then allocate and write densely, exactly as without reuse."""
+    def unheld(d):
+        ent = d.pop("x")
+        buf, cdata, _st = ent
+        return _getrefcount(buf) == 3 and _storage_uses(cdata) == 2
+
+    def entry():
+        t = torch.empty(8)
+        st = t.untyped_storage()
+        return t, {"x": (t, st._cdata, st)}
+    try:
+        t, d = entry()
+        del t
+        dropped = unheld(d)
+        t, d = entry()
+        held = unheld(d)
+        t, d = entry()
+        v = t[1:]
+        del t
+        view = unheld(d)
+        del v
+        return dropped and not held and not view
+    except Exception:
+        return False
+
+
+# every reuse path (reusable_output, OutputRecycler, ResidualMemory.spare_for, ShardedTopK's spare
+# residual) is gated on this
+REUSE_OK = _refcount_selftest()
+
+
 _sign_w1 = None
 
 
@@ -102,7 +139,7 @@ def reusable_output(slot, shape, dtype, device):
     hit = _reuse.get(key)
     if hit is not None:
         buf = hit[0]
-        if _getrefcount(buf) == 3 and _storage_uses(hit[1]) == 2:
+        if REUSE_OK and _getrefcount(buf) == 3 and _storage_uses(hit[1]) == 2:
             return buf
     buf = torch.empty(shape, dtype=dtype, device=device)
     _reuse[key] = (buf, buf.untyped_storage()._cdata, buf.untyped_storage())
@@ -132,7 +169,7 @@ class OutputRecycler:
         if hit is not None:
             buf, cdata, storage, version, prev_idx, key = hit
             # references to buf: the popped tuple, the local name, getrefcount's argument
-            if (key == (numel, torch.device(device), _stream()) and _getrefcount(buf) == 3
+            if (REUSE_OK and key == (numel, torch.device(device), _stream()) and _getrefcount(buf) == 3
                     and _storage_uses(cdata) == 2 and buf._version == version):
                 self.hits += 1
                 return buf, prev_idx

@@ -70,3 +70,41 @@ def test_other_name_size_or_stream_allocates(_cpu_stream):
     _cpu_stream["s"] = 7                                 # another stream
     _, prev = _step(rec, "c", torch.empty(100))
     assert prev is None
+
+
+def test_refcount_model_selftest_and_gate(monkeypatch):
+    """the reuse checks rest on CPython / torch reference counts.  The import-time
+    self-test replays their exact pattern and must accept this interpreter; with the gate off
+    (as it would be on an interpreter that counts differently) nothing is ever handed back."""
+    assert ops._refcount_selftest() and ops.REUSE_OK
+    monkeypatch.setattr(ops, "REUSE_OK", False)
+    rec = ops.OutputRecycler()
+    like = torch.empty(100)
+    out, _ = _step(rec, "b", like)
+    del out
+    out, prev = _step(rec, "b", like)
+    assert prev is None and rec.hits == 0 and rec.misses == 2
+
+
+def test_residual_spare_buffer_respects_holders():
+    """ResidualMemory.spare_for (the world > 1 step's second residual buffer) reuses the name's
+    previous residual only when nothing outside the memory holds it or a view of it."""
+    from grace_amd.dist.memory.residual import ResidualMemory
+    mem = ResidualMemory()
+    like = torch.empty(64)
+    a = mem.spare_for("w", like)
+    mem.retire("w", a)
+    pa = a.data_ptr()
+    del a
+    b = mem.spare_for("w", like)
+    assert b.data_ptr() == pa                     # dropped: reused
+    mem.retire("w", b)
+    held = b                                      # the caller keeps its old residual
+    del b
+    c = mem.spare_for("w", like)
+    assert c.data_ptr() != held.data_ptr()        # held: a fresh buffer
+    mem.retire("w", c)
+    v = c[3:]
+    del c
+    d = mem.spare_for("w", like)
+    assert d.data_ptr() != v.data_ptr() - 12      # a view held: a fresh buffer
