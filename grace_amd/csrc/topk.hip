@@ -84,6 +84,10 @@ template <bool HAS_RES, int MODE>
 constexpr int kVecOf = kBytesOf<HAS_RES, MODE> >= 16 ? kMainVec
                        : (kBytesOf<HAS_RES, MODE> >= 12 ? GRACE_MAIN_VEC_12B : GRACE_MAIN_VEC_NORES);
 template <bool HAS_RES, int MODE> constexpr int kChunkOf = kMainBlock * 4 * kVecOf<HAS_RES, MODE>;
+// (r05 A/B at BASELINE configs[4]'s 8.4 M-element shard, 12 B per element: 410 chunks of 20480
+// leave CUs with 1-2 workgroups, yet chunks of 16384 (512, two per CU) or 12288 (683) ran the local
+// step in 57.5-58.4 / 59.2-60.3 us against 57.3-57.4 -- the small bucket's main pass is bound by
+// its per-workgroup latency, not by the balance; 8192 spills 176-200 B with the residual stream)
 constexpr int kHistBins = 2048;                            // candidate histogram
 constexpr int kStage = 1024;                               // LDS staging entries per list (all waves)
 constexpr int kSelBlock = 1024;                            // single-workgroup selectors
@@ -803,12 +807,13 @@ __device__ __forceinline__ uint32_t classify_group(const StepArgs& a, const Topk
   return wfill + tot;
 }
 
-template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false>
+template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false,
+          int NV = kVecOf<HAS_RES, MODE>>
 __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
                                                   uint32_t lo, uint32_t hi, uint32_t sh, uint32_t mid, int64_t chunk) {
-  constexpr int NG = kVecOf<HAS_RES, MODE> / kGroup;
-  static_assert(NG * kGroup == kVecOf<HAS_RES, MODE>, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
-  const int64_t cbase = chunk * kChunkOf<HAS_RES, MODE> + (int64_t)threadIdx.x * 4;
+  constexpr int NG = NV / kGroup;
+  static_assert(NG * kGroup == NV, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
+  const int64_t cbase = chunk * (kMainBlock * 4 * NV) + (int64_t)threadIdx.x * 4;
   float4 rc[kGroup], gc[kGroup];
   uint32_t wfill = 0;
 #ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
@@ -893,7 +898,8 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
   __syncthreads();   // the lists and wcnt are free for the next chunk
 }
 
-template <bool HAS_RES, int MODE, bool VEC, bool SKEL = false, bool SPARSE = false>
+// NV: float4 per lane per chunk
+template <bool HAS_RES, int MODE, bool VEC, bool SKEL = false, bool SPARSE = false, int NV = kVecOf<HAS_RES, MODE>>
 __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w) {   // <= 128 VGPRs: 4 WGs/CU
   __shared__ MainShared sm;
   const int tid = threadIdx.x;
@@ -904,19 +910,20 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
     for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   }
   const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
-  const int64_t nchunks = (a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>;
+  constexpr int64_t kCh = (int64_t)kMainBlock * 4 * NV;
+  const int64_t nchunks = (a.n + kCh - 1) / kCh;
   const bool unit = HAS_RES && a.beta == 1.f && a.gamma == 1.f;
   if constexpr (!SKEL) __syncthreads();
   // one chunk per workgroup (grid-stride if the grid is capped); the staged lists leave after
   // every chunk, the histogram once at the end
   for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     uint32_t wfill;
-    if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n && unit)
-      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE, true>(a, w, sm, lo, hi, sh, mid, chunk);
-    else if (VEC && (chunk + 1) * kChunkOf<HAS_RES, MODE> <= a.n)
-      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
+    if (VEC && (chunk + 1) * kCh <= a.n && unit)
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE, true, NV>(a, w, sm, lo, hi, sh, mid, chunk);
+    else if (VEC && (chunk + 1) * kCh <= a.n)
+      wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE, false, NV>(a, w, sm, lo, hi, sh, mid, chunk);
     else
-      wfill = main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE>(a, w, sm, lo, hi, sh, mid, chunk);
+      wfill = main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE, false, NV>(a, w, sm, lo, hi, sh, mid, chunk);
     if constexpr (!SKEL) flush_staged(a, w, sm, lo, sh, wfill);
     (void)wfill;
   }
@@ -1684,7 +1691,17 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
     launch_timed(topk_main<HAS_RES, MODE, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
   }
   GRACE_CHECK_LAUNCH("topk_main");
-  topk_finalize<MODE><<<kFinBlocks, kSelBlock, 0, s>>>(a, w);
+  // finalize workgroups by the candidate capacity -- one routing round (kSelBlock * kFinPer
+  // candidates) each for the band the bracket can produce -- and by the bucket (at most 2^19
+  // elements each for the exact fallback's slices), so a small bucket's last arrival waits for
+  // 16-25 workgroups instead of 128 (the 2^26 headline keeps 128).  r05 A/B at configs[4]'s 8.4 M
+  // shard: local step 57.7 / 57.8 -> 56.7 / 57.0 us.
+  int fblocks = kFinBlocks;
+  {
+    const int64_t c = std::max(w.cap / ((int64_t)kSelBlock * kFinPer) + 1, a.n >> 19);
+    fblocks = (int)(c < 16 ? 16 : (c > kFinBlocks ? kFinBlocks : c));
+  }
+  topk_finalize<MODE><<<fblocks, kSelBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_finalize");
   return GRACE_OK;
 }
