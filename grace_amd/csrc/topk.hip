@@ -620,6 +620,10 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
 #define GRACE_MAIN_GROUP 4
 #endif
 constexpr int kGroup = GRACE_MAIN_GROUP;
+#ifndef GRACE_MAIN_RING
+#define GRACE_MAIN_RING 0
+#endif
+constexpr bool kMainRing = GRACE_MAIN_RING != 0;   // main_chunk_v2's copy-free load ring (A/B knob)
 
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -814,8 +818,34 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
   constexpr int NG = NV / kGroup;
   static_assert(NG * kGroup == NV, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
   const int64_t cbase = chunk * (kMainBlock * 4 * NV) + (int64_t)threadIdx.x * 4;
-  float4 rc[kGroup], gc[kGroup];
   uint32_t wfill = 0;
+  if constexpr (kMainRing) {
+    // A static ring of R group buffers, R - 1 groups' loads in flight ahead of the one being
+    // classified: the loop body is unrolled over the R slots, so no buffer is ever copied.  (The
+    // rotating copies of the loops below, next -> current after each group, made hipcc wait
+    // vmcnt(0) -- for the next group's loads AND the stores just issued -- before every group: each
+    // wave's memory pipeline drained once per group.)
+    constexpr int R = HAS_RES ? 2 : 3;   // buffers: 2 x (r, g) or 3 x g, 64 / 48 VGPRs
+    constexpr int64_t S = (int64_t)kGroup * (kMainBlock * 4);
+    float4 rb[R][kGroup], gb[R][kGroup];
+#pragma unroll
+    for (int p = 0; p < R - 1; ++p)
+      if (p < NG) load_group<HAS_RES, FAST>(a, cbase + p * S, rb[p], gb[p]);
+#pragma unroll 1
+    for (int q0 = 0; q0 < NG; q0 += R) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int q = q0 + j;
+        if (q < NG) {   // workgroup-uniform
+          if (q + R - 1 < NG) load_group<HAS_RES, FAST>(a, cbase + (q + R - 1) * S, rb[(j + R - 1) % R], gb[(j + R - 1) % R]);
+          wfill = classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, cbase + q * S,
+                                                                          rb[j], gb[j], wfill);
+        }
+      }
+    }
+    return wfill;
+  }
+  float4 rc[kGroup], gc[kGroup];
 #ifndef GRACE_MAIN_PREFETCH1   // A/B build only: one group ahead on every stream
   if constexpr (!HAS_RES && NG >= 3) {
     // one input stream (g only): the loads run TWO groups ahead, so a lane keeps as many bytes in

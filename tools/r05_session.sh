@@ -23,6 +23,7 @@ for s in "$@"; do
       GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so RES_ONLY=1 PATH_KIND=plain \
         run stamps_wn_local 120 python3 tools/exp_stamps.py ;;
     shard) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
+    shardstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run shard_local_stamps 180 python3 tools/exp_shard_local.py 8 ;;
     wn) run wn_local 180 python3 tools/exp_wn_local.py ;;
     toptests) run toptests 600 python3 -u -m pytest tests/test_gpu_topk.py tests/test_gpu_sharded.py tests/test_gpu_topk_carry.py tests/test_gpu_configs.py \
         -q -x --timeout 200 --timeout-method thread ;;
