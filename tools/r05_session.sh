@@ -25,8 +25,6 @@ for s in "$@"; do
     shard) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
     shardstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run shard_local_stamps 180 python3 tools/exp_shard_local.py 8 ;;
     wn) run wn_local 180 python3 tools/exp_wn_local.py ;;
-    toptests) run toptests 600 python3 -u -m pytest tests/test_gpu_topk.py tests/test_gpu_sharded.py tests/test_gpu_topk_carry.py tests/test_gpu_configs.py \
-        -q -x --timeout 200 --timeout-method thread ;;
     sq)
       i=0
       for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
