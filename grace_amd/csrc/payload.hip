@@ -175,23 +175,46 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
 // Python's sum, since indices are unique within a rank and a barrier separates the ranks.  Ranks
 // with more than kPBlock entries in the chunk finish their remaining rounds in order before the
 // next rank.  The tile is divided and written densely (the zero-fill included).
+// SMALLW (world <= 64): every wave keeps the ranks' bounds in registers (lane w holds rank w's,
+// read with readlane), so the tile is the workgroup's only LDS -- 32 KB, five workgroups per CU
+// instead of four with the 8 KB bounds table beside it.
 constexpr int kRankBatch = 8;
 constexpr int kMaxRanks = 1024;
+template <bool SMALLW>
 __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* __restrict__ vals,
                                                                   const uint16_t* __restrict__ off,
                                                                   const int32_t* __restrict__ ends, int64_t stride,
                                                                   int world, float divisor,
                                                                   float* __restrict__ out, int64_t n) {
   __shared__ float tile[kPChunk];
-  __shared__ int32_t s_b[2 * kMaxRanks];
+  __shared__ int32_t s_b[SMALLW ? 1 : 2 * kMaxRanks];
   const int t = threadIdx.x;
   const int64_t ch = blockIdx.x;
   const int64_t c0 = ch << kPChunkLog;
-  for (int w = t; w < world; w += kPBlock) {
-    const int32_t* ew = ends + (int64_t)w * stride;
-    s_b[2 * w] = ch > 0 ? ew[ch - 1] : 0;
-    s_b[2 * w + 1] = ew[ch];
+  int32_t bl = 0, el = 0;   // SMALLW: lane w's rank-w bounds
+  if constexpr (SMALLW) {
+    const int lane = t & 63;
+    if (lane < world) {
+      const int32_t* ew = ends + (int64_t)lane * stride;
+      bl = ch > 0 ? ew[ch - 1] : 0;
+      el = ew[ch];
+    }
+  } else {
+    for (int w = t; w < world; w += kPBlock) {
+      const int32_t* ew = ends + (int64_t)w * stride;
+      s_b[2 * w] = ch > 0 ? ew[ch - 1] : 0;
+      s_b[2 * w + 1] = ew[ch];
+    }
   }
+  auto bnd = [&](int w, int32_t& b, int32_t& e) {   // w wave-uniform
+    if constexpr (SMALLW) {
+      b = __builtin_amdgcn_readlane(bl, w);
+      e = __builtin_amdgcn_readlane(el, w);
+    } else {
+      b = s_b[2 * w];
+      e = s_b[2 * w + 1];
+    }
+  };
   for (int e = t; e < kPChunk; e += kPBlock) tile[e] = 0.f;
   __syncthreads();
   for (int w0 = 0; w0 < world; w0 += kRankBatch) {
@@ -200,8 +223,10 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
 #pragma unroll
     for (int q = 0; q < kRankBatch; ++q) {   // unconditional (clamped) loads: all in flight at once
       const int w = w0 + q < world ? w0 + q : w0;
-      const int32_t p = s_b[2 * w] + t;
-      const bool ok = w0 + q < world && p < s_b[2 * w + 1];
+      int32_t b, e;
+      bnd(w, b, e);
+      const int32_t p = b + t;
+      const bool ok = w0 + q < world && p < e;
       const int64_t pc = (int64_t)w * stride + (ok ? p : 0);
       const int32_t li = off[2 * (int64_t)w * stride + (ok ? p : 0)];   // rank w's u16 offsets: 2 w stride on
       v[q] = vals[pc];
@@ -212,8 +237,9 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
       const int w = w0 + q;
       if (w >= world) break;
       if (l[q] >= 0) tile[l[q]] = tile[l[q]] + v[q];
-      const int32_t s1 = s_b[2 * w + 1];
-      for (int32_t p = s_b[2 * w] + kPBlock + t; p < s1; p += kPBlock) {   // rare: > 256 entries
+      int32_t s0, s1;
+      bnd(w, s0, s1);
+      for (int32_t p = s0 + kPBlock + t; p < s1; p += kPBlock) {   // rare: > 256 entries
         const int32_t lp = off[2 * (int64_t)w * stride + p];
         tile[lp] = tile[lp] + vals[(int64_t)w * stride + p];
       }
@@ -292,8 +318,15 @@ grace_status_t grace_sparse_aggregate_sorted(const float* vals, const uint16_t* 
                     (n + kPChunk - 1) / kPChunk <= kMaxGroupChunks,
                 "grace_sparse_aggregate_sorted: bad arguments (1 <= world <= 1024, n <= 2^28)");
   const int64_t nchunks = (n + kPChunk - 1) / kPChunk;
-  chunk_accumulate_kernel<<<(unsigned)nchunks, kPBlock, 0, as_stream(stream)>>>(
-      vals, off, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
+#ifndef GRACE_DEC_SMALLW
+#define GRACE_DEC_SMALLW 1
+#endif
+  if (GRACE_DEC_SMALLW && world <= kWave)
+    chunk_accumulate_kernel<true><<<(unsigned)nchunks, kPBlock, 0, as_stream(stream)>>>(
+        vals, off, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
+  else
+    chunk_accumulate_kernel<false><<<(unsigned)nchunks, kPBlock, 0, as_stream(stream)>>>(
+        vals, off, reinterpret_cast<const int32_t*>(ends), stride, world, divisor, out, n);
   GRACE_CHECK_LAUNCH("grace_sparse_aggregate_sorted");
   return GRACE_OK;
 }

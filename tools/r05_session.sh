@@ -25,6 +25,15 @@ for s in "$@"; do
     shard) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
     shardstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run shard_local_stamps 180 python3 tools/exp_shard_local.py 8 ;;
     wn) run wn_local 180 python3 tools/exp_wn_local.py ;;
+    decab)   # the decode: one workgroup per chunk (decnopipe) vs the persistent pipelined form (4 / 5 / 8 per CU)
+      for i in 1 2; do
+        for v in decnopipe decpipe4 "" decpipe8; do
+          lib=grace_amd/lib/libgrace_hip${v:+_$v}.so
+          GRACE_HIP_LIB=$lib run wn_${v:-decpipe5}_$i 180 python3 tools/exp_wn_local.py
+        done
+      done ;;
+    sparsetests) run sparsetests 600 python3 -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_world2.py \
+        tests/test_gpu_w8.py -q -x --timeout 300 --timeout-method thread ;;
     sq)
       i=0
       for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
