@@ -104,6 +104,7 @@ SIGNATURES = {
     "grace_qsgd_step_w1": (ST, [P, P, P, I32, I64, I32, I32, P, U64, P, P]),
     "grace_qsgd_seg_max": (I32, []),
     "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
+    "grace_qsgd_compress_at": (ST, [P, I64, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
     "grace_qsgd_decompress": (ST, [P, P, I64, I64, I32, P, P, I32, I64, I32, I32, I32, I32, F32, P, P]),
     "grace_qsgd_global_workspace_bytes": (SZ, []),
     "grace_qsgd_global_compress": (ST, [P, I64, I32, P, U64, P, P, P, P, P]),
@@ -128,7 +129,9 @@ SIGNATURES = {
     "grace_terngrad_step_w1": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_decompress": (ST, [P, P, I64, I64, I32, P, I32, I64, I32, F32, P, P]),
     "grace_natural_compress": (ST, [P, I64, P, U64, P, P]),
+    "grace_natural_compress_at": (ST, [P, I64, I64, P, U64, P, P]),
     "grace_cnat_compress": (ST, [P, I64, P, I32, U64, P, P]),
+    "grace_cnat_compress_at": (ST, [P, I64, I64, P, I32, U64, P, P]),
     "grace_natural_decompress": (ST, [P, I64, I32, I64, I32, I32, F32, P, P]),
     "grace_fp16_compress": (ST, [P, P, I64, P]),
     "grace_fp16_decompress": (ST, [P, P, I64, P]),

@@ -219,7 +219,9 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
     int nseg, int32_t nbuckets, float qf, const float* __restrict__ u, uint64_t seed,
     const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes,
-    float* __restrict__ fused_out = nullptr) {
+    float* __restrict__ fused_out = nullptr, uint32_t xoff = 0) {
+  // xoff: the bucket element of x[0] for the device generator (a shard of a larger bucket,
+  // grace_qsgd_compress_at): the draws are keyed by the bucket's element index
   __shared__ SegTables32 tab;
   // int8 codes leave as 16-B stores: each row stages its kQNB buckets' codes (128 B each) here and
   // every lane stores 16 contiguous bytes (a 4-B store per quad covered four 64-B pieces per wave
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode128_kernel(
 #ifdef GRACE_DIAG_NORNG   // diagnostic A/B build only: constant u
           uu[0] = uu[1] = uu[2] = uu[3] = 0.5f + 0.f * (float)key;
 #else
-          uniform01x4_k(key, (uint32_t)eq, uu);
+          uniform01x4_k(key, (uint32_t)eq + xoff, uu);
 #endif
         }
         CodeT c[4];
@@ -699,7 +701,7 @@ template <typename CodeT, int VARIANT>
 __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ bkt_off,
     int nseg, int64_t nbuckets, int bucket, float qf, const float* __restrict__ u, uint64_t seed,
-    const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes) {
+    const float* __restrict__ norms_in, float* __restrict__ norms_out, CodeT* __restrict__ codes, int64_t xoff = 0) {
   __shared__ SegTables tab;
   const SegView sv = stage_tables(tab, seg_off, bkt_off, nseg);
   const int l32 = threadIdx.x & 31;
@@ -754,7 +756,7 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
         const float scale = VARIANT == 0 ? (1.0f / norm[h]) * qf : qf / norm[h];
         float uu[4];
         if (u) load_quad(u, e, end[h], aligned[h], uu);
-        else uniform01x4(seed, (uint64_t)e, uu);
+        else uniform01x4(seed, (uint64_t)(e + xoff), uu);
         CodeT c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -786,7 +788,7 @@ __global__ __launch_bounds__(kQBlock) void qsgd_encode_kernel(
     const float scale = VARIANT == 0 ? (1.0f / norm) * qf : qf / norm;
     for (int64_t i = base + l32; i < end; i += 32) {
       const float v = x[i];
-      const float ui = u ? u[i] : uniform01(seed, (uint64_t)i);
+      const float ui = u ? u[i] : uniform01(seed, (uint64_t)(i + xoff));
       const float level = VARIANT == 0 ? scale * fabsf(v) : qf / norm * fabsf(v);
       codes[i] = qsgd_code<CodeT, VARIANT>(v, level, ui, norm);
     }
@@ -1613,7 +1615,8 @@ __device__ __forceinline__ void natural_rand4(uint64_t seed, int64_t e, int32_t 
 
 __global__ __launch_bounds__(kQBlock) void natural_encode_kernel(const float* __restrict__ x, int64_t n,
                                                                 const int32_t* __restrict__ ri, uint64_t seed,
-                                                                uint8_t* __restrict__ codes, int aligned) {
+                                                                uint8_t* __restrict__ codes, int aligned,
+                                                                int64_t xoff) {
   const int64_t nq = (n + 3) >> 2;
   for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
     const int64_t e = q << 2;
@@ -1630,7 +1633,7 @@ __global__ __launch_bounds__(kQBlock) void natural_encode_kernel(const float* __
         for (int j = 0; j < 4; ++j) r[j] = e + j < n ? ri[e + j] : 0;
       }
     } else {
-      natural_rand4(seed, e, r);
+      natural_rand4(seed, e + xoff, r);   // (xoff % 4 == 0: the bucket's quads)
     }
     uint32_t c[4];
 #pragma unroll
@@ -1668,7 +1671,7 @@ __device__ __forceinline__ uint32_t cnat_code(float v, float r) {
 __global__ __launch_bounds__(kQBlock) void cnat_encode_kernel(const float* __restrict__ x, int64_t n,
                                                              const float* __restrict__ rnd, int deterministic,
                                                              uint64_t seed, uint8_t* __restrict__ codes,
-                                                             int aligned) {
+                                                             int aligned, int64_t xoff) {
   const int64_t nq = (n + 3) >> 2;
   for (int64_t q = (int64_t)blockIdx.x * kQBlock + threadIdx.x; q < nq; q += (int64_t)gridDim.x * kQBlock) {
     const int64_t e = q << 2;
@@ -1681,7 +1684,7 @@ __global__ __launch_bounds__(kQBlock) void cnat_encode_kernel(const float* __res
     } else if (rnd) {
       load_quad(rnd, e, n, fast, r);
     } else {
-      uniform01x4(seed, (uint64_t)e, r);   // one hash per quad (device generator)
+      uniform01x4(seed, (uint64_t)(e + xoff), r);   // one hash per quad (device generator)
     }
     uint32_t c[4];
 #pragma unroll
@@ -1965,19 +1968,19 @@ grace_status_t grace_qsgd_step_w1(const float* x, const int64_t* seg_off, const 
 
 int32_t grace_qsgd_seg_max(void) { return kSegLds; }
 
-grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const int64_t* bkt_off,
-                                   int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
-                                   int32_t variant, const float* u, uint64_t seed, const float* norms_in,
-                                   float* norms_out, void* codes, void* stream) {
+grace_status_t grace_qsgd_compress_at(const float* x, int64_t xoff, const int64_t* seg_off, const int64_t* bkt_off,
+                                      int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
+                                      int32_t variant, const float* u, uint64_t seed, const float* norms_in,
+                                      float* norms_out, void* codes, void* stream) {
   GRACE_REQUIRE(x && seg_off && bkt_off && nseg >= 1 && nbuckets >= 0 && bucket_size >= 1 &&
-                    quantum_num >= 1 && norms_out && codes,
+                    quantum_num >= 1 && norms_out && codes && xoff >= 0 && xoff < ((int64_t)1 << 31),
                 "grace_qsgd_compress: bad arguments");
   if (nbuckets == 0) return GRACE_OK;
   GRACE_REQUIRE(variant == 0 || (variant == 1 && quantum_num < 128), "grace_qsgd_compress: bad variant");
   const unsigned grid = stream_grid(nbuckets, kQNB * kQBlock / 32, kQGridCap);
   hipStream_t st = as_stream(stream);
   if (bucket_size == 128 && nseg <= kSegLds && nbuckets < (int64_t(1) << 24)) {   // n < 2^31
-    const bool pipe = GRACE_QENC_PIPE && !u && !norms_in;
+    const bool pipe = GRACE_QENC_PIPE && !u && !norms_in && xoff == 0;
     const unsigned grid16 = pipe ? qenc_pipe_grid(nbuckets) : stream_grid(nbuckets, kQNB * kQBlock / 16, kQEncGridCap);
 #define GRACE_QENC128(CT, V)                                                                         \
   do { if (pipe)                                                                                          \
@@ -1987,7 +1990,8 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
   else                                                                                               \
     qsgd_encode128_kernel<CT, V><<<grid16, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, (int32_t)nbuckets, \
                                                           (float)quantum_num, u, seed, norms_in,      \
-                                                          norms_out, reinterpret_cast<CT*>(codes)); } while (0)
+                                                          norms_out, reinterpret_cast<CT*>(codes),    \
+                                                          nullptr, (uint32_t)xoff); } while (0)
     if (variant == 1) GRACE_QENC128(int8_t, 1);
     else if (quantum_num < 128) GRACE_QENC128(int8_t, 0);
     else GRACE_QENC128(__half, 0);
@@ -1998,18 +2002,26 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
   if (variant == 1) {
     qsgd_encode_kernel<int8_t, 1><<<grid, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, nbuckets, bucket_size,
                                                            (float)quantum_num, u, seed, norms_in, norms_out,
-                                                           reinterpret_cast<int8_t*>(codes));
+                                                           reinterpret_cast<int8_t*>(codes), xoff);
   } else if (quantum_num < 128) {
     qsgd_encode_kernel<int8_t, 0><<<grid, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, nbuckets, bucket_size,
                                                            (float)quantum_num, u, seed, norms_in, norms_out,
-                                                           reinterpret_cast<int8_t*>(codes));
+                                                           reinterpret_cast<int8_t*>(codes), xoff);
   } else {
     qsgd_encode_kernel<__half, 0><<<grid, kQBlock, 0, st>>>(x, seg_off, bkt_off, nseg, nbuckets, bucket_size,
                                                            (float)quantum_num, u, seed, norms_in, norms_out,
-                                                           reinterpret_cast<__half*>(codes));
+                                                           reinterpret_cast<__half*>(codes), xoff);
   }
   GRACE_CHECK_LAUNCH("grace_qsgd_compress");
   return GRACE_OK;
+}
+
+grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const int64_t* bkt_off,
+                                   int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
+                                   int32_t variant, const float* u, uint64_t seed, const float* norms_in,
+                                   float* norms_out, void* codes, void* stream) {
+  return grace_qsgd_compress_at(x, 0, seg_off, bkt_off, nseg, nbuckets, quantum_num, bucket_size, variant, u, seed,
+                                norms_in, norms_out, codes, stream);
 }
 
 size_t grace_qsgd_global_workspace_bytes(void) { return sizeof(double) * kQgBlocks; }
@@ -2205,28 +2217,38 @@ grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scala
   return GRACE_OK;
 }
 
-grace_status_t grace_natural_compress(const float* x, int64_t n, const int32_t* rand_int, uint64_t seed,
-                                      uint8_t* codes, void* stream) {
-  GRACE_REQUIRE(x && codes && n >= 0, "grace_natural_compress: bad arguments");
+grace_status_t grace_natural_compress_at(const float* x, int64_t xoff, int64_t n, const int32_t* rand_int,
+                                         uint64_t seed, uint8_t* codes, void* stream) {
+  GRACE_REQUIRE(x && codes && n >= 0 && xoff >= 0 && (xoff & 3) == 0, "grace_natural_compress: bad arguments");
   if (n == 0) return GRACE_OK;
   const int al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(rand_int)) & 15) == 0 &&
                  (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
   natural_encode_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      x, n, rand_int, seed, codes, al);
+      x, n, rand_int, seed, codes, al, xoff);
   GRACE_CHECK_LAUNCH("grace_natural_compress");
+  return GRACE_OK;
+}
+
+grace_status_t grace_natural_compress(const float* x, int64_t n, const int32_t* rand_int, uint64_t seed,
+                                      uint8_t* codes, void* stream) {
+  return grace_natural_compress_at(x, 0, n, rand_int, seed, codes, stream);
+}
+
+grace_status_t grace_cnat_compress_at(const float* x, int64_t xoff, int64_t n, const float* rand,
+                                      int32_t deterministic, uint64_t seed, uint8_t* codes, void* stream) {
+  GRACE_REQUIRE(x && codes && n >= 0 && xoff >= 0 && (xoff & 3) == 0, "grace_cnat_compress: bad arguments");
+  if (n == 0) return GRACE_OK;
+  const int al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(rand)) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
+  cnat_encode_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
+      x, n, rand, deterministic, seed, codes, al, xoff);
+  GRACE_CHECK_LAUNCH("grace_cnat_compress");
   return GRACE_OK;
 }
 
 grace_status_t grace_cnat_compress(const float* x, int64_t n, const float* rand, int32_t deterministic,
                                    uint64_t seed, uint8_t* codes, void* stream) {
-  GRACE_REQUIRE(x && codes && n >= 0, "grace_cnat_compress: bad arguments");
-  if (n == 0) return GRACE_OK;
-  const int al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(rand)) & 15) == 0 &&
-                 (reinterpret_cast<uintptr_t>(codes) & 3) == 0;
-  cnat_encode_kernel<<<stream_grid((n + 3) / 4, kQBlock, 4096), kQBlock, 0, as_stream(stream)>>>(
-      x, n, rand, deterministic, seed, codes, al);
-  GRACE_CHECK_LAUNCH("grace_cnat_compress");
-  return GRACE_OK;
+  return grace_cnat_compress_at(x, 0, n, rand, deterministic, seed, codes, stream);
 }
 
 grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, int32_t world, int64_t n,

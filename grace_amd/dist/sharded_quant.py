@@ -1,0 +1,189 @@
+"""Sharded element-wise and bucketed quantisers: ONE bucket of tensors split over the ranks and
+compressed exactly as the single-GPU codec compresses the whole bucket (SURVEY.md §8e, row
+"sign / QSGD / natural: none before encode").
+
+Codecs (the single-GPU codec each restates, and what a rank's shard must keep whole):
+- ``"sign"``    SignSGDCompressor encode / decode (signsgd.py:10-22): u8 (x >= 0), decoded 2s - 1;
+- ``"fp16"``    FP16Compressor (fp16.py): round-to-nearest-even cast and back;
+- ``"natural"`` NaturalCompressor (natural.py:12-39), cupy flavour, device generator or injected
+                randint stream;
+- ``"cnat"``    NaturalCompressor_CUDA (cnat_cuda.cu:68-134), device generator, injected uniforms or
+                the deterministic threshold;
+- ``"qsgd"``    QSGDCompressor (qsgd.py:12-49): per tensor, buckets of ``bucket_size`` with their own
+                norm, codes int8 (q < 128) or fp16.
+None of them needs anything from another rank before encoding -- a QSGD bucket's norm is local to
+the bucket -- so a step is: encode this rank's shard (the device generator keyed by the BUCKET's
+element index, so the codes equal the whole-bucket call's: ``grace_*_compress_at``), then
+``dense="replicated"``: ONE all-gather of the codes (and QSGD's bucket norms, in the same padded
+record) and the decode of the whole bucket on every rank; ``dense="shard"``: the decode of this
+rank's range only, no collective at all.
+
+Partition: QSGD by whole buckets (each tensor's buckets counted from its start, in equal contiguous
+blocks per rank, as sharded TernGrad's work units); the element-wise codecs by 128-element blocks of
+the flat bucket (so every shard starts on a quad of the device generator).  ``partition(sizes)``
+gives every rank's [start, end) and ``step()`` takes exactly that shard.  No host synchronisation in
+a step.  ``kernels`` defaults to the native HIP set; the CPU tests inject an oracle-backed emulator.
+"""
+import torch
+import torch.distributed as dist
+
+from grace_amd import ops
+
+CODECS = ("sign", "fp16", "natural", "cnat", "qsgd")
+_BLOCK = 128   # element-wise codecs: partition granule (a multiple of the generator's quad)
+
+
+class NativeQuantKernels:
+    """The HIP codec calls behind each step (GPU tensors only)."""
+
+    def encode(self, codec, x, xoff, sizes, u, seed, q, bucket, variant, deterministic):
+        """-> (codes, norms or None) of the shard x (its segment table `sizes`)."""
+        if codec == "sign":
+            return ops.sign_encode(x), None
+        if codec == "fp16":
+            return ops.fp16_compress(x), None
+        if codec == "natural":
+            return ops.natural_compress(x, rand_int=u, seed=seed, xoff=xoff), None
+        if codec == "cnat":
+            return ops.cnat_compress(x, rand=u, deterministic=deterministic, seed=seed, xoff=xoff), None
+        return ops.qsgd_compress(x, q, bucket, sizes=sizes, variant=variant, u=u, seed=seed, xoff=xoff)
+
+    def decode(self, codec, codes, norms, sizes, n, q, bucket, variant):
+        if codec == "sign":
+            return ops.sign_decode(codes)
+        if codec == "fp16":
+            return ops.fp16_decompress(codes)
+        if codec in ("natural", "cnat"):
+            return ops.natural_decompress(codes, n, 0 if codec == "natural" else 1)
+        return ops.qsgd_decompress(codes, norms, q, bucket, n, sizes=sizes, variant=variant)
+
+    def code_dtype(self, codec, q):
+        if codec == "fp16" or (codec == "qsgd" and q >= 128):
+            return torch.float16
+        return torch.int8 if codec == "qsgd" else torch.uint8
+
+
+class _Plan:
+    """The partition of one segment table over `world` ranks."""
+
+    def __init__(self, codec, sizes, world, bucket):
+        self.sizes = tuple(int(s) for s in sizes)
+        if any(s < 1 for s in self.sizes):
+            raise ValueError("ShardedQuant: empty tensor in the segment table")
+        seg = [0]
+        for s in self.sizes:
+            seg.append(seg[-1] + s)
+        self.n = seg[-1]
+        self.seg = seg
+        if codec == "qsgd":
+            starts = []                   # global element start of every bucket
+            for i, s in enumerate(self.sizes):
+                starts += [seg[i] + j * bucket for j in range((s + bucket - 1) // bucket)]
+        else:
+            starts = list(range(0, self.n, _BLOCK))
+        self.nunits = len(starts)
+        starts.append(self.n)
+        U = (self.nunits + world - 1) // world
+        self.units = [(min(r * U, self.nunits), min((r + 1) * U, self.nunits)) for r in range(world)]
+        self.ranges = [(starts[u0], starts[u1]) for u0, u1 in self.units]
+        self.max_len = max(hi - lo for lo, hi in self.ranges)
+        self.max_units = max(u1 - u0 for u0, u1 in self.units)
+        # per rank: the parts of the tensors its range holds (QSGD's segment table of the shard)
+        self.parts = []
+        for lo, hi in self.ranges:
+            self.parts.append([min(hi, seg[i + 1]) - max(lo, seg[i]) for i in range(len(self.sizes))
+                               if seg[i] < hi and seg[i + 1] > lo])
+
+
+class ShardedQuant:
+    """A sign / fp16 / natural / cnat / QSGD bucket whose elements are sharded across `group`."""
+
+    def __init__(self, codec, group=None, dense="replicated", quantum_num=127, bucket_size=128, variant=0,
+                 deterministic=False, kernels=None, seed=0):
+        if codec not in CODECS:
+            raise ValueError(f"codec must be one of {CODECS}")
+        if dense not in ("replicated", "shard"):
+            raise ValueError("dense must be 'replicated' or 'shard'")
+        self.codec = codec
+        self.group = group
+        self.dense = dense
+        self.q = int(quantum_num)
+        self.bucket = int(bucket_size)
+        self.variant = int(variant)
+        self.deterministic = bool(deterministic)
+        self.seed = seed
+        self.k_ops = kernels or NativeQuantKernels()
+        self._plans = {}
+        self.last_codes = None     # this rank's codes (its element range)
+        self.last_norms = None     # QSGD: this rank's bucket norms
+
+    def _world(self):
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group), dist.get_rank(self.group)
+        return 1, 0
+
+    def _plan(self, sizes, world):
+        key = (tuple(int(s) for s in sizes), world)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = self._plans[key] = _Plan(self.codec, key[0], world, self.bucket)
+        return plan
+
+    def partition(self, sizes, world=None):
+        """Every rank's [start, end) element range of the flat bucket."""
+        return list(self._plan(sizes, world or self._world()[0]).ranges)
+
+    def step(self, shard, sizes=None, u=None, seed=None):
+        """This rank's shard (exactly partition(sizes)[rank], a tensor of its own) -> the decoded
+        bucket (dense="replicated") or this rank's decoded range (dense="shard").  u: optional
+        injected random stream for THIS shard's elements (natural: int32 randint draws; cnat / QSGD:
+        f32 uniforms)."""
+        K = self.k_ops
+        world, rank = self._world()
+        x = shard.reshape(-1)
+        if sizes is None:
+            if world != 1:
+                raise ValueError("ShardedQuant: the bucket's segment sizes are needed at world > 1")
+            sizes = [x.numel()]
+        plan = self._plan(sizes, world)
+        lo, hi = plan.ranges[rank]
+        if x.numel() != hi - lo:
+            raise ValueError(f"ShardedQuant: rank {rank} holds {x.numel()} elements, its range is {hi - lo} "
+                             "(use partition(sizes))")
+        seed = self.seed if seed is None else seed
+        parts = plan.parts[rank]
+        if hi > lo:
+            codes, norms = K.encode(self.codec, x, lo, parts, u, seed, self.q, self.bucket, self.variant,
+                                    self.deterministic)
+        else:
+            codes = torch.empty(0, dtype=K.code_dtype(self.codec, self.q), device=x.device)
+            norms = torch.empty(0, dtype=torch.float32, device=x.device) if self.codec == "qsgd" else None
+        self.last_codes, self.last_norms = codes, norms
+        if self.dense == "shard" or world == 1:
+            if hi == lo:
+                return torch.empty(0, dtype=torch.float32, device=x.device)
+            return K.decode(self.codec, codes, norms, parts, hi - lo, self.q, self.bucket, self.variant)
+        # ONE all-gather of fixed-size records: [codes (padded to the longest range) | norms (QSGD,
+        # padded to the most buckets)] as bytes
+        csz = codes.element_size()
+        cb = (plan.max_len * csz + 15) // 16 * 16       # 16-B aligned norms and records
+        nb = (plan.max_units * 4 + 15) // 16 * 16 if self.codec == "qsgd" else 0
+        rec = torch.zeros(cb + nb, dtype=torch.uint8, device=x.device)
+        rec[:codes.numel() * csz].copy_(codes.view(torch.uint8).reshape(-1))
+        if nb:
+            rec[cb:cb + norms.numel() * 4].copy_(norms.view(torch.uint8))
+        gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=x.device)
+        dist.all_gather_into_tensor(gathered, rec, group=self.group)
+        g = gathered.view(world, -1)
+        full = torch.empty(plan.n * csz, dtype=torch.uint8, device=x.device)
+        for w, (a, b) in enumerate(plan.ranges):   # the padded records, back to one flat code buffer
+            if b > a:
+                full[a * csz:b * csz].copy_(g[w, :(b - a) * csz])
+        full = full.view(codes.dtype)
+        allnorms = None
+        if self.codec == "qsgd":
+            allnorms = torch.empty(plan.nunits, dtype=torch.float32, device=x.device)
+            for w, (u0, u1) in enumerate(plan.units):
+                if u1 > u0:
+                    allnorms[u0:u1].copy_(g[w, cb:cb + (u1 - u0) * 4].view(torch.float32))
+        return K.decode(self.codec, full, allnorms, list(plan.sizes), plan.n, self.q, self.bucket, self.variant)

@@ -600,14 +600,16 @@ def _opt(t):
 
 
 # ----------------------------------------------------------------------------- QSGD
-def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, seed=0, norms_in=None):
-    """x: flat f32 device buffer (one tensor, or `sizes` segments back to back)."""
+def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, seed=0, norms_in=None, xoff=0):
+    """x: flat f32 device buffer (one tensor, or `sizes` segments back to back).  xoff: the element
+    of a larger bucket x[0] is (a shard starting on a bucket boundary): the device generator draws
+    by that bucket's element index (grace_qsgd_compress_at)."""
     x = dev_f32(x)
     sizes = [x.numel()] if sizes is None else sizes
     seg_off, bkt_off, nb = seg_tables(sizes, bucket_size, x.device)
     codes = torch.empty(x.numel(), dtype=torch.int8 if quantum_num < 128 else torch.float16, device=x.device)
     norms = torch.empty(nb, dtype=F32, device=x.device)
-    _lib.call("grace_qsgd_compress", _p(x), _p(seg_off), _p(bkt_off), len(sizes), nb, int(quantum_num),
+    _lib.call("grace_qsgd_compress_at", _p(x), int(xoff), _p(seg_off), _p(bkt_off), len(sizes), nb, int(quantum_num),
               int(bucket_size), int(variant), _opt(u), int(seed) & (2 ** 64 - 1), _opt(norms_in), _p(norms),
               _p(codes), _stream())
     return codes, norms
@@ -700,18 +702,20 @@ def terngrad_decompress(codes, scalars, n, sizes=None, world=1, aggregate=False,
 
 
 # ----------------------------------------------------------------------------- natural / fp16
-def natural_compress(x, rand_int=None, seed=0):
+def natural_compress(x, rand_int=None, seed=0, xoff=0):
+    """xoff (a multiple of 4): the element of a larger bucket x[0] is, for the device generator."""
     x = dev_f32(x)
     codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
-    _lib.call("grace_natural_compress", _p(x), x.numel(), _opt(rand_int), int(seed) & (2 ** 64 - 1),
+    _lib.call("grace_natural_compress_at", _p(x), int(xoff), x.numel(), _opt(rand_int), int(seed) & (2 ** 64 - 1),
               _p(codes), _stream())
     return codes
 
 
-def cnat_compress(x, rand=None, deterministic=False, seed=0):
+def cnat_compress(x, rand=None, deterministic=False, seed=0, xoff=0):
+    """xoff (a multiple of 4): the element of a larger bucket x[0] is, for the device generator."""
     x = dev_f32(x)
     codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
-    _lib.call("grace_cnat_compress", _p(x), x.numel(), _opt(rand), 1 if deterministic else 0,
+    _lib.call("grace_cnat_compress_at", _p(x), int(xoff), x.numel(), _opt(rand), 1 if deterministic else 0,
               int(seed) & (2 ** 64 - 1), _p(codes), _stream())
     return codes
 

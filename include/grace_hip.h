@@ -242,6 +242,14 @@ grace_status_t grace_qsgd_compress(const float* x, const int64_t* seg_off, const
                                    int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
                                    int32_t variant, const float* u, uint64_t seed, const float* norms_in,
                                    float* norms_out, void* codes, void* stream);
+/* The same on a shard of a larger bucket (grace_amd/dist/sharded_quant.py): x[0] is the bucket's
+ * element xoff (0 <= xoff < 2^31) and the shard starts on a bucket boundary of its first segment;
+ * the device generator draws by the bucket's element index, so the codes equal the whole-bucket
+ * call's codes for the shard's elements. */
+grace_status_t grace_qsgd_compress_at(const float* x, int64_t xoff, const int64_t* seg_off, const int64_t* bkt_off,
+                                      int32_t nseg, int64_t nbuckets, int32_t quantum_num, int32_t bucket_size,
+                                      int32_t variant, const float* u, uint64_t seed, const float* norms_in,
+                                      float* norms_out, void* codes, void* stream);
 /* (norm / q) * code (qsgd.py:44-49).  world > 1 with rank-major payload strides: decode +
  * aggregate in rank order, aggregate != 0 adds the Python-sum 0 (allgather.py:40-45); divisor
  * applies the average. */
@@ -302,6 +310,12 @@ grace_status_t grace_natural_compress(const float* x, int64_t n, const int32_t* 
                                       uint8_t* codes, void* stream);
 grace_status_t grace_cnat_compress(const float* x, int64_t n, const float* rand, int32_t deterministic,
                                    uint64_t seed, uint8_t* codes, void* stream);
+/* the same on a shard of a larger bucket: x[0] is its element xoff (a multiple of 4) for the device
+ * generator (grace_amd/dist/sharded_quant.py) */
+grace_status_t grace_natural_compress_at(const float* x, int64_t xoff, int64_t n, const int32_t* rand_int,
+                                         uint64_t seed, uint8_t* codes, void* stream);
+grace_status_t grace_cnat_compress_at(const float* x, int64_t xoff, int64_t n, const float* rand,
+                                      int32_t deterministic, uint64_t seed, uint8_t* codes, void* stream);
 /* flavour 0 = natural.py:35-39 decode, 1 = cnat_cuda.cu:125-134 decode */
 grace_status_t grace_natural_decompress(const uint8_t* codes, int64_t stride, int32_t world, int64_t n,
                                         int32_t flavour, int32_t aggregate, float divisor, float* out,

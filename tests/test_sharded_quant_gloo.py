@@ -1,0 +1,150 @@
+"""Sharded sign / fp16 / natural / cnat / QSGD (grace_amd/dist/sharded_quant.py) on CPU with gloo,
+W = 2 and 3.  The device calls are replaced by the oracle restatements (signsgd.py:10-22, fp16.py,
+natural.py:12-39, cnat_cuda.cu:68-134, qsgd.py:12-49 per tensor) with injected random streams; the
+partition, the padded record all-gather and the per-rank segment tables are the product's.  The
+sharded result must equal the reference restatement applied to the whole bucket (QSGD: tensor by
+tensor, every bucket counted from its tensor's start).  The native GPU version is
+tests/test_gpu_sharded_quant.py."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import grace_oracle as O
+
+F32 = np.float32
+Q, BUCKET = 127, 128
+SIZES = [500, 128, 1, 1234, 96, 257, 3000, 5]
+
+
+class OracleQuantKernels:
+    """numpy restatement of the codec calls (test infrastructure)."""
+
+    def code_dtype(self, codec, q):
+        if codec == "fp16" or (codec == "qsgd" and q >= 128):
+            return torch.float16
+        return torch.int8 if codec == "qsgd" else torch.uint8
+
+    def encode(self, codec, x, xoff, sizes, u, seed, q, bucket, variant, deterministic):
+        xv = x.numpy()
+        if codec == "sign":
+            return torch.from_numpy(O.sign_encode(xv)), None
+        if codec == "fp16":
+            return torch.from_numpy(O.fp16_compress(xv)), None
+        if codec == "natural":
+            return torch.from_numpy(O.natural_compress(xv, u.numpy())), None
+        if codec == "cnat":
+            return torch.from_numpy(O.cnat_compress(xv, None if deterministic else u.numpy())), None
+        codes, norms, a = [], [], 0
+        for s in sizes:   # QSGD tensor by tensor (the shard's parts start on bucket boundaries)
+            c, nm = O.qsgd_compress(xv[a:a + s], u.numpy()[a:a + s], q, bucket)
+            codes.append(c)
+            norms.append(nm)
+            a += s
+        return torch.from_numpy(np.concatenate(codes)), torch.from_numpy(np.concatenate(norms).astype(F32))
+
+    def decode(self, codec, codes, norms, sizes, n, q, bucket, variant):
+        c = codes.numpy()
+        if codec == "sign":
+            return torch.from_numpy(O.sign_decode(c))
+        if codec == "fp16":
+            return torch.from_numpy(O.fp16_decode(c))
+        if codec == "natural":
+            return torch.from_numpy(O.natural_decode(c))
+        if codec == "cnat":
+            return torch.from_numpy(O.cnat_decode(c))
+        out, a, b = [], 0, 0
+        nm = norms.numpy()
+        for s in sizes:
+            nb = -(-s // bucket)
+            out.append(O.qsgd_decode(c[a:a + s], nm[b:b + nb], q, bucket, s))
+            a += s
+            b += nb
+        return torch.from_numpy(np.concatenate(out))
+
+
+def _data(seed):
+    rng = np.random.default_rng(seed)
+    flat = np.concatenate([(rng.standard_normal(n) * (0.01 * (1 + i % 3))).astype(F32) for i, n in enumerate(SIZES)])
+    flat[7] = F32(-0.0)
+    u = rng.random(flat.size).astype(F32)
+    ri = rng.integers(0, 2 ** 23 - 1, flat.size).astype(np.int32)
+    return flat, u, ri
+
+
+def _stream(codec, u, ri):
+    return ri if codec == "natural" else u
+
+
+def _worker(rank, world, path, outdir, codec, dense, det):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    from grace_amd.dist.sharded_quant import ShardedQuant
+    eng = ShardedQuant(codec, dense=dense, quantum_num=Q, bucket_size=BUCKET, deterministic=det,
+                       kernels=OracleQuantKernels())
+    flat, u, ri = _data(5)
+    lo, hi = eng.partition(SIZES)[rank]
+    s = _stream(codec, u, ri)
+    out = eng.step(torch.from_numpy(flat[lo:hi].copy()), SIZES, u=torch.from_numpy(s[lo:hi].copy()))
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), out=out.numpy(), lo=np.array([lo, hi]))
+    dist.destroy_process_group()
+
+
+def _expected(codec, det):
+    flat, u, ri = _data(5)
+    K = OracleQuantKernels()
+    s = torch.from_numpy(_stream(codec, u, ri))
+    codes, norms = K.encode(codec, torch.from_numpy(flat), 0, SIZES, s, 0, Q, BUCKET, 0, det)
+    return K.decode(codec, codes, norms, SIZES, flat.size, Q, BUCKET, 0).numpy(), flat
+
+
+def _bits(a, b):
+    return np.array_equal(np.asarray(a, F32).view(np.uint32), np.asarray(b, F32).view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("codec,det", [("sign", False), ("fp16", False), ("natural", False), ("cnat", False),
+                                       ("cnat", True), ("qsgd", False)])
+@pytest.mark.parametrize("dense", ["replicated", "shard"])
+def test_sharded_quant_matches_whole_bucket(world, codec, det, dense):
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, codec, dense, det), nprocs=world, join=True)
+        outs = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                outs.append({k: z[k] for k in z.files})
+    exp, flat = _expected(codec, det)
+    if dense == "shard":
+        assert _bits(np.concatenate([o["out"] for o in outs]), exp)
+    else:
+        for o in outs:
+            assert _bits(o["out"], exp)
+    # the partition tiles the bucket in rank order; QSGD shards start on a bucket of their tensor
+    los = [tuple(o["lo"]) for o in outs]
+    assert los[0][0] == 0 and los[-1][1] == flat.size and all(los[i][1] == los[i + 1][0] for i in range(world - 1))
+    seg = np.cumsum([0] + SIZES)
+    for a, _ in los:
+        if codec == "qsgd":
+            t = np.searchsorted(seg, a, side="right") - 1
+            assert (a - seg[t]) % BUCKET == 0
+        else:
+            assert a % 128 == 0
+
+
+def test_sharded_quant_world1_is_the_codec():
+    from grace_amd.dist.sharded_quant import ShardedQuant
+    flat, u, _ = _data(6)
+    eng = ShardedQuant("qsgd", kernels=OracleQuantKernels())
+    out = eng.step(torch.from_numpy(flat), SIZES, u=torch.from_numpy(u)).numpy()
+    exp = []
+    a = 0
+    for s in SIZES:
+        c, nm = O.qsgd_compress(flat[a:a + s], u[a:a + s], Q, BUCKET)
+        exp.append(O.qsgd_decode(c, nm, Q, BUCKET, s))
+        a += s
+    assert _bits(out, np.concatenate(exp))
+    with pytest.raises(ValueError):
+        ShardedQuant("topk")
