@@ -140,6 +140,8 @@ SIGNATURES = {
     "grace_randomk_indices": (ST, [U64, I64, I64, P, P]),
     "grace_gather": (ST, [P, P, I64, P, P]),
     "grace_randomk_step_w1": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, P]),
+    "grace_randomk_shard_step": (ST, [P, P, I32, F32, F32, I64, I64, P, I64, P, P, P]),
+    "grace_randomk_decode": (ST, [P, P, I64, P, I64, P]),
     "grace_randomk_step_w1_dense_workspace_bytes": (SZ, [I64, I64]),
     "grace_randomk_group_bytes": (SZ, [I64, I64]),
     "grace_randomk_step_w1_dense": (ST, [P, P, I32, F32, F32, I64, P, I64, P, P, P, P, SZ, P]),

@@ -46,6 +46,7 @@ __global__ __launch_bounds__(kSBlock) void randomk_pass_kernel(const float* __re
                                                               float* __restrict__ out) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int64_t stride = (int64_t)gridDim.x * kSBlock;
+  // out may be null (the sharded step's replicated mode decodes the gathered payload instead)
   const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(r) |
                      reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   const int64_t nq = vec ? n >> 2 : 0;
@@ -65,12 +66,38 @@ __global__ __launch_bounds__(kSBlock) void randomk_pass_kernel(const float* __re
       if (HAS_RES) t = f4{beta * rv[u].x + gamma * gv[u].x, beta * rv[u].y + gamma * gv[u].y,
                           beta * rv[u].z + gamma * gv[u].z, beta * rv[u].w + gamma * gv[u].w};
       __builtin_nontemporal_store(t, reinterpret_cast<f4*>(r) + q0 + u * stride);
-      __builtin_nontemporal_store(z, reinterpret_cast<f4*>(out) + q0 + u * stride);
+      if (out) __builtin_nontemporal_store(z, reinterpret_cast<f4*>(out) + q0 + u * stride);
     }
   }
   for (int64_t i = nq * 4 + (int64_t)blockIdx.x * kSBlock + threadIdx.x; i < n; i += stride) {
     r[i] = HAS_RES ? beta * r[i] + gamma * g[i] : g[i];
-    out[i] = 0.f;
+    if (out) out[i] = 0.f;
+  }
+}
+
+// Sharded random-k (grace_amd/dist/sharded_randomk.py): this rank holds the bucket's elements
+// [lo, lo + m); idx are the k GLOBAL indices every rank draws alike.  The gather takes t for the
+// drawn indices this rank holds and +0 for the others (every index has exactly one owner, so the
+// ranks' payloads sum to the whole bucket's payload, -0 excepted, which the step's 0 + d makes +0
+// anyway); the scatter zeroes r' at this rank's drawn positions and writes 0 + t to its dense slice.
+__global__ __launch_bounds__(kSBlock) void randomk_shard_gather_kernel(const float* __restrict__ t,
+                                                                      const int64_t* __restrict__ idx, int64_t k,
+                                                                      int64_t lo, int64_t m, float* __restrict__ vals) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock) {
+    const int64_t i = idx[j] - lo;
+    vals[j] = (i >= 0 && i < m) ? t[i] : 0.f;
+  }
+}
+__global__ __launch_bounds__(kSBlock) void randomk_shard_scatter_kernel(const int64_t* __restrict__ idx,
+                                                                       const float* __restrict__ vals, int64_t k,
+                                                                       int64_t lo, int64_t m, float* __restrict__ r,
+                                                                       float* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * kSBlock + threadIdx.x; j < k; j += (int64_t)gridDim.x * kSBlock) {
+    const int64_t i = idx[j] - lo;
+    if (i < 0 || i >= m) continue;
+    const float v = vals[j];
+    if (out) out[i] = 0.f + v;
+    if (r) r[i] = v - v;
   }
 }
 
@@ -663,6 +690,35 @@ grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t ha
   GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
   randomk_scatter_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(idx, vals, k, residual, out);
   GRACE_CHECK_LAUNCH("grace_randomk_step_w1");
+  return GRACE_OK;
+}
+
+grace_status_t grace_randomk_shard_step(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
+                                       int64_t lo, int64_t m, const int64_t* idx, int64_t k, float* vals, float* out,
+                                       void* stream) {
+  GRACE_REQUIRE(g && residual && vals && lo >= 0 && m >= 1 && k >= 0 && (k == 0 || idx),
+                "grace_randomk_shard_step: bad arguments");
+  hipStream_t s = as_stream(stream);
+  const unsigned grid = stream_grid((m + 3) / 4, kSBlock * kRQ, 4096);
+  if (has_residual) randomk_pass_kernel<true><<<grid, kSBlock, 0, s>>>(g, residual, beta, gamma, m, out);
+  else randomk_pass_kernel<false><<<grid, kSBlock, 0, s>>>(g, residual, beta, gamma, m, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_shard_step");
+  if (k == 0) return GRACE_OK;
+  randomk_shard_gather_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(residual, idx, k, lo, m, vals);
+  GRACE_CHECK_LAUNCH("grace_randomk_shard_step");
+  randomk_shard_scatter_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, s>>>(idx, vals, k, lo, m, residual, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_shard_step");
+  return GRACE_OK;
+}
+
+grace_status_t grace_randomk_decode(const float* vals, const int64_t* idx, int64_t k, float* out, int64_t n,
+                                    void* stream) {
+  GRACE_REQUIRE(out && n >= 1 && k >= 0 && (k == 0 || (vals && idx)), "grace_randomk_decode: bad arguments");
+  grace_status_t st = grace_fill(out, 0.f, n, stream);
+  if (st != GRACE_OK || k == 0) return st;
+  randomk_shard_scatter_kernel<<<stream_grid(k, kSBlock, 2048), kSBlock, 0, as_stream(stream)>>>(idx, vals, k, 0, n,
+                                                                                                  nullptr, out);
+  GRACE_CHECK_LAUNCH("grace_randomk_decode");
   return GRACE_OK;
 }
 

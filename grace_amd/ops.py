@@ -815,6 +815,26 @@ def randomk_step_w1(g, residual, has_residual, beta, gamma, idx):
     return vals, out
 
 
+def randomk_shard_step(g, residual, has_residual, beta, gamma, lo, idx, out=None):
+    """Sharded random-k (grace_randomk_shard_step): this rank's shard g (global elements
+    [lo, lo + g.numel())), the global indices idx; returns vals (t where this rank holds the index,
+    +0 elsewhere).  residual updated in place; out (optional): this rank's slice of the result."""
+    g = dev_f32(g)
+    idx = require_dev(idx, "indices")
+    vals = torch.empty(idx.numel(), dtype=F32, device=g.device)
+    _lib.call("grace_randomk_shard_step", _p(g), _p(residual), 1 if has_residual else 0, float(beta), float(gamma),
+              int(lo), g.numel(), _p(idx), idx.numel(), _p(vals), _p(out), _stream())
+    return vals
+
+
+def randomk_decode(vals, idx, n):
+    """zeros(n) with 0 + vals[j] at idx[j] (grace_randomk_decode): the world-1 step's result."""
+    vals, idx = require_dev(vals), require_dev(idx, "indices")
+    out = torch.empty(int(n), dtype=F32, device=vals.device)
+    _lib.call("grace_randomk_decode", _p(vals), _p(idx), idx.numel(), _p(out), int(n), _stream())
+    return out
+
+
 def randomk_step_w1_dense(g, residual, has_residual, beta, gamma, idx, out=None, grp=None, prev_grp=None):
     """The world-1 step's out (and r' in `residual`) in one streaming pass after grouping the indices
     by chunk (grace_randomk_step_w1_dense); no payload.  grp: a per-name uint8 buffer of

@@ -393,6 +393,18 @@ grace_status_t grace_gather(const float* x, const int64_t* idx, int64_t k, float
 grace_status_t grace_randomk_step_w1(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
                                      int64_t n, const int64_t* idx, int64_t k, float* vals, float* out,
                                      void* stream);
+/* Sharded random-k + residual (grace_amd/dist/sharded_randomk.py): this rank holds the bucket's
+ * elements [lo, lo + m) (g, residual and out point there); idx[k] are the bucket's GLOBAL indices,
+ * the same on every rank.  residual <- t with this rank's drawn positions t - t; vals[j] = t at
+ * idx[j] if this rank holds it, else +0 (the ranks' vals sum to the whole bucket's payload);
+ * out (may be NULL): this rank's slice of the world-1 step's result, 0 + t at its drawn positions. */
+grace_status_t grace_randomk_shard_step(const float* g, float* residual, int32_t has_residual, float beta, float gamma,
+                                       int64_t lo, int64_t m, const int64_t* idx, int64_t k, float* vals, float* out,
+                                       void* stream);
+/* The world-1 step's result from the whole bucket's payload: out = zeros(n), out[idx[j]] = 0 + vals[j]
+ * (randomk.py:39-40 decompress, allgather.py:44 sum from 0). */
+grace_status_t grace_randomk_decode(const float* vals, const int64_t* idx, int64_t k, float* out, int64_t n,
+                                    void* stream);
 /* The same world-1 step without materialising the payload (only `out` is the step's result at
  * world 1): the indices are grouped by 8192-element chunk, then ONE streaming pass writes r' and
  * out (16 B per element, no random gathers / scatters); bit-identical out and r'.  n < 2^31 and
