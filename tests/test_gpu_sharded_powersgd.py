@@ -1,0 +1,78 @@
+"""Sharded PowerSGD (grace_amd/dist/sharded_powersgd.py) with the NATIVE kernels: 2 and 3 processes
+share cuda:0 over gloo.  Each rank holds a block of rows; the result is compared with the
+single-GPU ``PowerSGDCompressor(4, one_pass=False)`` on the whole matrix (the same q draws, the same
+orthogonalisation input): P is gathered whole, so every rank's P must equal the single-GPU P bit for
+bit; Q = Σ M_iᵀ P_i sums in another order, so P Qᵀ agrees within f32 tolerance (SURVEY §8a row a17:
+rel <= 1e-5·sqrt(m)).  With error feedback (memory=True) over two steps the second step's input is
+M + r, r = M - P Qᵀ of the first (memory/powersgd.py:16-37)."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+NAME = "layer4.conv"
+
+
+def _mat(n, m, step):
+    return np.random.default_rng(200 + step).standard_normal((n, m)).astype(F32)
+
+
+def _worker(rank, world, path, outdir, n, m, dense, memory):
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from grace_amd.dist.sharded_powersgd import ShardedPowerSGD
+    eng = ShardedPowerSGD(4, dense=dense, memory=memory)
+    lo, hi = eng.partition(n, world)[rank]
+    res = {"lo": np.array([lo, hi])}
+    for s in range(2):
+        out = eng.step(torch.from_numpy(_mat(n, m, s)[lo:hi].copy()).cuda(), NAME, n)
+        res[f"out{s}"] = out.cpu().numpy()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+def _single(n, m, memory):
+    from grace_amd import ops
+    from grace_amd.dist.compressor.powersgd import PowerSGDCompressor
+    comp = PowerSGDCompressor(rank=4, one_pass=False)
+    outs, r = [], None
+    for s in range(2):
+        t = torch.from_numpy(_mat(n, m, s)).cuda()
+        if memory and r is not None:
+            t = t + r
+        _, ctx = comp.compress(t, NAME)
+        out = comp.decompress([], ctx)
+        if memory:
+            r = t - out
+        outs.append(out.cpu().numpy())
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("n,m,dense,memory", [(1000, 2048, "replicated", False), (1000, 2048, "shard", True),
+                                              (4096, 4096, "replicated", True)])
+def test_sharded_powersgd_matches_single_gpu(world, n, m, dense, memory):
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, n, m, dense, memory), nprocs=world, join=True)
+        outs = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                outs.append({k: z[k] for k in z.files})
+    exp = _single(n, m, memory)
+    tol = 1e-5 * np.sqrt(m)
+    for s in range(2):
+        got = [np.concatenate([o[f"out{s}"] for o in outs])] if dense == "shard" else [o[f"out{s}"] for o in outs]
+        for gi in got:
+            assert gi.shape == exp[s].shape
+            scale = float(np.abs(exp[s]).max())
+            err = float(np.abs(gi - exp[s]).max())
+            assert err <= tol * scale, (s, err, scale)
+        if dense == "replicated":   # every rank forms the identical result
+            for o in outs[1:]:
+                assert np.array_equal(o[f"out{s}"], outs[0][f"out{s}"])

@@ -32,7 +32,7 @@ for s in "$@"; do
           GRACE_HIP_LIB=$lib run wn_${v:-decpipe5}_$i 180 python3 tools/exp_wn_local.py
         done
       done ;;
-    quanttests) run quanttests 900 python3 -u -m pytest tests/test_gpu_sharded_randomk.py tests/test_gpu_sharded_quant.py tests/test_gpu_sparse.py \
+    quanttests) run quanttests 900 python3 -u -m pytest tests/test_gpu_sharded_powersgd.py tests/test_gpu_sharded_randomk.py \
         -q -x --timeout 300 --timeout-method thread ;;
     sparsetests) run sparsetests 600 python3 -u -m pytest tests/test_gpu_sparse.py tests/test_gpu_world2.py \
         tests/test_gpu_w8.py -q -x --timeout 300 --timeout-method thread ;;
