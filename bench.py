@@ -196,7 +196,7 @@ def pmc_traffic(workload, alg_bytes):
     WRITE_SIZE passes (tools/prof_r02.sh -> tools/pmc_all.py), with the ratio to the algorithmic
     bytes; None when that workload was not profiled."""
     wl = None
-    for tag in ("r04", "r03", "r02"):   # the newest committed passes that cover the workload
+    for tag in ("r05", "r04", "r03", "r02"):   # the newest committed passes that cover the workload
         try:
             with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_secondary.json")) as f:
                 wl = json.load(f)["workloads"][workload]
