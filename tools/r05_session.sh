@@ -48,6 +48,14 @@ for s in "$@"; do
           -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
       python3 tools/pmc_sq_summary.py $O/sq_head > $O/sq_head_summary.json; echo "sq summary rc=$?" ;;
     bench) run bench 300 python3 bench.py ;;
+    prof) # the headline, single stream, no in-bench probes (tools/prof_steady.py keeps the timed launches)
+          GRACE_BENCH_NO_PROBE=1 run prof_topk 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_topk -o run \
+            -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
+          python3 tools/prof_steady.py $O/prof_topk --last 20 --out $O/prof_topk_steady.json; echo "steady rc=$?" ;;
+    profwl) for wl in ${PROF_WL:-powersgd terngrad qsgd sign}; do
+              run "prof_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run \
+                -- python3 bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline
+            done ;;
     pytest) run pytest_gpu 1100 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
     secondary)
       : > $O/secondary.jsonl
