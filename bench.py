@@ -145,13 +145,19 @@ def main():
         # BASELINE configs[4] (one 256 MiB bucket sharded over the ranks, top-k 0.1 %) rides in the
         # same JSON line, so the driver's 1 -> 8 GPU record covers it next to the DP replicas
         line["sharded"] = nested_sharded(line, args, world, rank, dev)
+        # SURVEY §8e's other sharded codecs at the same N: configs[2]'s ResNet-50 set as ONE bucket
+        # split over the ranks (sharded TernGrad: one all-gather of unit partials + one of the codes;
+        # sharded QSGD: one all-gather of codes + norms), same guard
+        for key, codec in (("sharded_terngrad", "terngrad"), ("sharded_qsgd", "qsgd")):
+            line[key] = nested_sharded(line, args, world, rank, dev, key=key,
+                                       fn=lambda a, w, r, d, c=codec: bench_sharded_codec(a, w, r, d, c))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def nested_sharded(line, args, world, rank, dev):
+def nested_sharded(line, args, world, rank, dev, key="sharded", fn=None):
     """The configs[4] record inside the DP-replica line, guarded so that it can never cost the DP
     record: an exception on a rank is agreed through one all_reduce and recorded as {"error": ...};
     a rank that hangs (a collective some rank never reaches) is bounded by a watchdog that prints
@@ -161,7 +167,7 @@ def nested_sharded(line, args, world, rank, dev):
 
     def expire():
         if rank == 0:
-            line["sharded"] = {"error": f"timeout: the sharded leg did not finish within {limit:.0f} s"}
+            line[key] = {"error": f"timeout: the {key} leg did not finish within {limit:.0f} s"}
             print(json.dumps(line), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
@@ -174,7 +180,7 @@ def nested_sharded(line, args, world, rank, dev):
     try:
         if os.environ.get("GRACE_BENCH_INJECT_SHARDED_FAILURE", "") in ("all", str(rank)):
             raise RuntimeError(f"injected failure on rank {rank}")
-        sh = bench_topk_sharded(args, world, rank, dev)
+        sh = (fn or bench_topk_sharded)(args, world, rank, dev)
     except Exception as e:          # recorded, not raised: the DP-replica record stays
         err = f"{type(e).__name__}: {e}"[:400]
     flag = torch.tensor([1.0 if err else 0.0], device=dev)
@@ -182,8 +188,45 @@ def nested_sharded(line, args, world, rank, dev):
     dog.cancel()
     if float(flag.item()) > 0:
         return {"error": err or "failed on another rank"}
-    return {key: sh[key] for key in ("metric", "value", "unit", "ms_per_step", "scaling", "config", "roofline",
-                                     "shard_decode")}
+    return {k: sh[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "config", "roofline",
+                               "shard_decode") if k in sh}
+
+
+def bench_sharded_codec(args, world, rank, dev, codec):
+    """configs[2]'s 161 ResNet-50 tensors as ONE bucket whose elements are split over the
+    ranks (grace_amd/dist/sharded_terngrad.py, sharded_quant.py), the decoded bucket replicated on
+    every rank; strong scaling (the bucket is fixed).  Bytes per GPU: the shard's encode (TernGrad:
+    two reads of x and the codes, 9 B per element; QSGD: 5 B) plus the replicated decode of the
+    whole bucket (1 B of codes read, 4 B written per element)."""
+    sizes = [int(torch.Size(s).numel()) for s in resnet50_shapes()]
+    n = sum(sizes)
+    if codec == "terngrad":
+        from grace_amd.dist.sharded_terngrad import ShardedTernGrad
+        eng = ShardedTernGrad(seed=7)
+        enc_b = 9.0
+    else:
+        from grace_amd.dist.sharded_quant import ShardedQuant
+        eng = ShardedQuant("qsgd", quantum_num=127, bucket_size=128, seed=7)
+        enc_b = 5.0
+    lo, hi = eng.partition(sizes)[rank]
+    gen = torch.Generator(device=dev)
+    shards = []
+    for j in range(args.buffers):
+        gen.manual_seed(500 * rank + j + 1)
+        shards.append(torch.randn(hi - lo, device=dev, generator=gen) * 0.01)
+    elapsed = timed(lambda i: eng.step(shards[i % args.buffers], sizes), args.steps, args.warmup, world, dev)
+    t = elapsed / args.steps
+    m = max(b - a for a, b in eng.partition(sizes))
+    per_gpu = enc_b * m + 5.0 * n
+    return {"metric": f"grad-codec GB/s (device-resident encode+decode), {codec} over the ResNet-50 set sharded",
+            "value": round(4.0 * n / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 4),
+            "scaling": "strong",
+            "config": {"workload": f"Sharded{'TernGrad' if codec == 'terngrad' else 'Quant(qsgd 127, bucket 128)'}: "
+                                   f"161 ResNet-50 tensors ({n} elements) as one bucket over {world} rank(s), "
+                                   "replicated dense decode (BASELINE configs[2], SURVEY §8e)",
+                       "numel": n, "shard_max": m, "parallelism": f"{world} contiguous unit-aligned shards"},
+            "roofline": {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_gpu": per_gpu}}
 
 
 # GRACE_BENCH_NO_PROBE=1: skip the in-bench HBM probes (profiling passes, whose per-dispatch
