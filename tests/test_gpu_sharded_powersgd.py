@@ -55,8 +55,10 @@ def _single(n, m, memory):
 
 
 @pytest.mark.parametrize("world", [2, 3])
+# (2, 64, ...): a 2-row matrix (rank min(n, m, 4) = 2); over 3 processes the last rank holds no row
 @pytest.mark.parametrize("n,m,dense,memory", [(1000, 2048, "replicated", False), (1000, 2048, "shard", True),
-                                              (4096, 4096, "replicated", True)])
+                                              (4096, 4096, "replicated", True), (2, 64, "replicated", True),
+                                              (2, 64, "shard", False)])
 def test_sharded_powersgd_matches_single_gpu(world, n, m, dense, memory):
     with tempfile.TemporaryDirectory() as tmp:
         mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, n, m, dense, memory), nprocs=world, join=True)

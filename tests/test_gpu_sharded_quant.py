@@ -21,9 +21,9 @@ Q, BUCKET = 127, 128
 SIZES = [64, 16384, 100003, 1, 2048, 16385, 40000, 7, 65536, 3001]
 
 
-def _data(seed):
+def _data(seed, sizes=SIZES):
     rng = np.random.default_rng(seed)
-    flat = np.concatenate([(rng.standard_normal(n) * (0.01 * (1 + i % 3))).astype(F32) for i, n in enumerate(SIZES)])
+    flat = np.concatenate([(rng.standard_normal(n) * (0.01 * (1 + i % 3))).astype(F32) for i, n in enumerate(sizes)])
     flat[11] = F32(-0.0)
     u = rng.random(flat.size).astype(F32)
     ri = rng.integers(0, 2 ** 23 - 1, flat.size).astype(np.int32)
@@ -36,24 +36,24 @@ def _stream(codec, use_u, u, ri):
     return ri if codec == "natural" else u
 
 
-def _worker(rank, world, path, outdir, codec, dense, use_u, det, q):
+def _worker(rank, world, path, outdir, codec, dense, use_u, det, q, sizes=SIZES):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from grace_amd.dist.sharded_quant import ShardedQuant
     eng = ShardedQuant(codec, dense=dense, quantum_num=q, bucket_size=BUCKET, deterministic=det, seed=13)
-    flat, u, ri = _data(4)
-    lo, hi = eng.partition(SIZES)[rank]
+    flat, u, ri = _data(4, sizes)
+    lo, hi = eng.partition(sizes)[rank]
     s = _stream(codec, use_u, u, ri)
     res = {"lo": np.array([lo, hi])}
     for step in range(2):   # two steps: the plan is reused
         x = torch.from_numpy(flat[lo:hi] * F32(step + 1)).cuda()
-        out = eng.step(x, SIZES, u=torch.from_numpy(s[lo:hi].copy()).cuda() if s is not None else None)
+        out = eng.step(x, sizes, u=torch.from_numpy(s[lo:hi].copy()).cuda() if s is not None else None)
         res[f"out{step}"] = out.cpu().numpy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
 
-def _single(codec, x, s, det, q):
+def _single(codec, x, s, det, q, sizes=SIZES):
     from grace_amd import ops
     n = x.numel()
     if codec == "sign":
@@ -64,8 +64,8 @@ def _single(codec, x, s, det, q):
         return ops.natural_decompress(ops.natural_compress(x, rand_int=s, seed=13), n, 0)
     if codec == "cnat":
         return ops.natural_decompress(ops.cnat_compress(x, rand=s, deterministic=det, seed=13), n, 1)
-    codes, norms = ops.qsgd_compress(x, q, BUCKET, sizes=SIZES, u=s, seed=13)
-    return ops.qsgd_decompress(codes, norms, q, BUCKET, n, sizes=SIZES)
+    codes, norms = ops.qsgd_compress(x, q, BUCKET, sizes=sizes, u=s, seed=13)
+    return ops.qsgd_decompress(codes, norms, q, BUCKET, n, sizes=sizes)
 
 
 def _bits(a, b):
@@ -101,3 +101,30 @@ def test_sharded_quant_native_matches_single_gpu(world, codec, use_u, det, q, de
             for o in outs:
                 assert _bits(o[f"out{step}"], exp), (step, codec)
     assert int(outs[0]["lo"][0]) == 0 and int(outs[-1]["lo"][1]) == flat.size
+
+
+@pytest.mark.parametrize("codec", ["sign", "qsgd"])
+@pytest.mark.parametrize("dense", ["replicated", "shard"])
+def test_sharded_quant_native_rank_without_elements(codec, dense):
+    """A bucket of fewer partition units than ranks (one 128-element block; two QSGD buckets) over 3
+    processes: the last rank's shard is empty, it still joins the all-gather, and every rank's result
+    equals the single-GPU codec's."""
+    sizes = [100] if codec == "sign" else [130]
+    world = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, codec, dense, False, False, Q, sizes),
+                 nprocs=world, join=True)
+        outs = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                outs.append({k: z[k] for k in z.files})
+    assert int(outs[-1]["lo"][0]) == int(outs[-1]["lo"][1])
+    flat, _, _ = _data(4, sizes)
+    for step in range(2):
+        x = torch.from_numpy(flat * F32(step + 1)).cuda()
+        exp = _single(codec, x, None, False, Q, sizes).cpu().numpy()
+        if dense == "shard":
+            assert _bits(np.concatenate([o[f"out{step}"] for o in outs]), exp), step
+        else:
+            for o in outs:
+                assert _bits(o[f"out{step}"], exp), step

@@ -17,19 +17,19 @@ F32 = np.float32
 N, RATIO, NAME = (1 << 22) + 3, 0.01, "bucket0"
 
 
-def _grad(step):
-    return np.random.default_rng(90 + step).standard_normal(N).astype(F32)
+def _grad(step, n=N):
+    return np.random.default_rng(90 + step).standard_normal(n).astype(F32)
 
 
-def _worker(rank, world, path, outdir, dense, rng):
+def _worker(rank, world, path, outdir, dense, rng, n=N):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from grace_amd.dist.sharded_randomk import ShardedRandomK
     eng = ShardedRandomK(RATIO, dense=dense, rng=rng)
-    lo, hi = eng.partition(N, world)[rank]
+    lo, hi = eng.partition(n, world)[rank]
     res = {"lo": np.array([lo, hi])}
     for s in range(3):
-        out = eng.step(torch.from_numpy(_grad(s)[lo:hi].copy()).cuda(), NAME, N)
+        out = eng.step(torch.from_numpy(_grad(s, n)[lo:hi].copy()).cuda(), NAME, n)
         res[f"out{s}"] = out.cpu().numpy()
         res[f"res{s}"] = eng.residuals[NAME].cpu().numpy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
@@ -40,11 +40,14 @@ def _bits(a, b):
     return np.array_equal(np.asarray(a, F32).view(np.uint32), np.asarray(b, F32).view(np.uint32))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,n", [(2, N), (3, N), (3, 6)])
 @pytest.mark.parametrize("dense,rng", [("replicated", "device"), ("shard", "device"), ("replicated", "torch_cpu")])
-def test_sharded_randomk_native_matches_single_gpu(world, dense, rng):
+def test_sharded_randomk_native_matches_single_gpu(world, n, dense, rng):
+    """(3, 6): 4-element blocks over 3 ranks, the last rank holds no element."""
+    if n != N and rng == "torch_cpu":
+        pytest.skip("the empty-rank case runs with the device generator")
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense, rng), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense, rng, n), nprocs=world, join=True)
         outs = []
         for r in range(world):
             with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
@@ -54,7 +57,7 @@ def test_sharded_randomk_native_matches_single_gpu(world, dense, rng):
     from grace_amd.dist.memory.residual import ResidualMemory
     comm = Allgather(RandomKCompressor(RATIO, rng=rng), ResidualMemory(), 1)
     for s in range(3):
-        exp = comm.step(torch.from_numpy(_grad(s)).cuda(), NAME).cpu().numpy()
+        exp = comm.step(torch.from_numpy(_grad(s, n)).cuda(), NAME).cpu().numpy()
         r = comm.memory.residuals[NAME].cpu().numpy()
         assert _bits(np.concatenate([o[f"res{s}"] for o in outs]), r), s
         if dense == "shard":

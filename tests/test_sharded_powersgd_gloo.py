@@ -44,28 +44,28 @@ class OraclePowerSGDKernels:
         return b + a
 
 
-def _mat(step):
-    return np.random.default_rng(300 + step).standard_normal((N, M)).astype(F32)
+def _mat(step, n=N):
+    return np.random.default_rng(300 + step).standard_normal((n, M)).astype(F32)
 
 
-def _worker(rank, world, path, outdir, dense):
+def _worker(rank, world, path, outdir, dense, n=N):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded_powersgd import ShardedPowerSGD
     eng = ShardedPowerSGD(4, dense=dense, memory=True, kernels=OraclePowerSGDKernels())
-    lo, hi = eng.partition(N, world)[rank]
+    lo, hi = eng.partition(n, world)[rank]
     res = {}
     for s in range(2):
-        res[f"out{s}"] = eng.step(torch.from_numpy(_mat(s)[lo:hi].copy()), NAME, N).numpy()
+        res[f"out{s}"] = eng.step(torch.from_numpy(_mat(s, n)[lo:hi].copy()), NAME, n).numpy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
 
-def _oracle():
+def _oracle(n=N):
     from grace_amd import ops
     outs, r = [], None
     for s in range(2):
-        t = _mat(s) if r is None else (_mat(s) + r).astype(F32)
-        q = _q(ops.step_seed("powersgd-q", NAME, s + 1), M, 4).numpy()
+        t = _mat(s, n) if r is None else (_mat(s, n) + r).astype(F32)
+        q = _q(ops.step_seed("powersgd-q", NAME, s + 1), M, min(n, M, 4)).numpy()   # powersgd.py:36
         p, qq = O.powersgd_compress(t, q)
         d = O.powersgd_decode(p, qq)
         r = (t - d).astype(F32)
@@ -73,16 +73,18 @@ def _oracle():
     return outs
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,n", [(2, N), (3, N), (3, 2)])
 @pytest.mark.parametrize("dense", ["replicated", "shard"])
-def test_sharded_powersgd_matches_oracle(world, dense):
+def test_sharded_powersgd_matches_oracle(world, n, dense):
+    """(3, 2): a 2-row matrix over 3 ranks -- rank 2 holds no row, still joins the P all-gather and
+    the Q all-reduce, and the rank is min(n, m, 4) = 2 (powersgd.py:36)."""
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense, n), nprocs=world, join=True)
         outs = []
         for r in range(world):
             with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
                 outs.append({k: z[k] for k in z.files})
-    exp = _oracle()
+    exp = _oracle(n)
     for s in range(2):
         got = [np.concatenate([o[f"out{s}"] for o in outs])] if dense == "shard" else [o[f"out{s}"] for o in outs]
         for g in got:

@@ -67,9 +67,9 @@ class OracleQuantKernels:
         return torch.from_numpy(np.concatenate(out))
 
 
-def _data(seed):
+def _data(seed, sizes=SIZES):
     rng = np.random.default_rng(seed)
-    flat = np.concatenate([(rng.standard_normal(n) * (0.01 * (1 + i % 3))).astype(F32) for i, n in enumerate(SIZES)])
+    flat = np.concatenate([(rng.standard_normal(n) * (0.01 * (1 + i % 3))).astype(F32) for i, n in enumerate(sizes)])
     flat[7] = F32(-0.0)
     u = rng.random(flat.size).astype(F32)
     ri = rng.integers(0, 2 ** 23 - 1, flat.size).astype(np.int32)
@@ -80,25 +80,25 @@ def _stream(codec, u, ri):
     return ri if codec == "natural" else u
 
 
-def _worker(rank, world, path, outdir, codec, dense, det):
+def _worker(rank, world, path, outdir, codec, dense, det, sizes=SIZES):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded_quant import ShardedQuant
     eng = ShardedQuant(codec, dense=dense, quantum_num=Q, bucket_size=BUCKET, deterministic=det,
                        kernels=OracleQuantKernels())
-    flat, u, ri = _data(5)
-    lo, hi = eng.partition(SIZES)[rank]
+    flat, u, ri = _data(5, sizes)
+    lo, hi = eng.partition(sizes)[rank]
     s = _stream(codec, u, ri)
-    out = eng.step(torch.from_numpy(flat[lo:hi].copy()), SIZES, u=torch.from_numpy(s[lo:hi].copy()))
+    out = eng.step(torch.from_numpy(flat[lo:hi].copy()), sizes, u=torch.from_numpy(s[lo:hi].copy()))
     np.savez(os.path.join(outdir, f"r{rank}.npz"), out=out.numpy(), lo=np.array([lo, hi]))
     dist.destroy_process_group()
 
 
-def _expected(codec, det):
-    flat, u, ri = _data(5)
+def _expected(codec, det, sizes=SIZES):
+    flat, u, ri = _data(5, sizes)
     K = OracleQuantKernels()
     s = torch.from_numpy(_stream(codec, u, ri))
-    codes, norms = K.encode(codec, torch.from_numpy(flat), 0, SIZES, s, 0, Q, BUCKET, 0, det)
-    return K.decode(codec, codes, norms, SIZES, flat.size, Q, BUCKET, 0).numpy(), flat
+    codes, norms = K.encode(codec, torch.from_numpy(flat), 0, sizes, s, 0, Q, BUCKET, 0, det)
+    return K.decode(codec, codes, norms, sizes, flat.size, Q, BUCKET, 0).numpy(), flat
 
 
 def _bits(a, b):
@@ -132,6 +132,30 @@ def test_sharded_quant_matches_whole_bucket(world, codec, det, dense):
             assert (a - seg[t]) % BUCKET == 0
         else:
             assert a % 128 == 0
+
+
+@pytest.mark.parametrize("codec", ["sign", "qsgd"])
+@pytest.mark.parametrize("dense", ["replicated", "shard"])
+def test_sharded_quant_ranks_without_elements(codec, dense):
+    """A bucket smaller than one partition unit per rank (one 128-element block, two 128-element
+    QSGD buckets over 3 ranks): the ranks past the units hold empty shards, still join the one
+    all-gather and decode the whole bucket (or an empty slice)."""
+    sizes = [100] if codec == "sign" else [130]
+    world = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, codec, dense, False, sizes), nprocs=world,
+                 join=True)
+        outs = []
+        for r in range(world):
+            with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
+                outs.append({k: z[k] for k in z.files})
+    exp, flat = _expected(codec, False, sizes)
+    assert any(o["lo"][0] == o["lo"][1] for o in outs)   # some rank really is empty
+    if dense == "shard":
+        assert _bits(np.concatenate([o["out"] for o in outs]), exp)
+    else:
+        for o in outs:
+            assert _bits(o["out"], exp)
 
 
 def test_sharded_quant_world1_is_the_codec():

@@ -46,32 +46,32 @@ class OracleRandomKKernels:
         return torch.from_numpy(o)
 
 
-def _grad(step):
-    return np.random.default_rng(50 + step).standard_normal(N).astype(F32)
+def _grad(step, n=N):
+    return np.random.default_rng(50 + step).standard_normal(n).astype(F32)
 
 
-def _worker(rank, world, path, outdir, dense):
+def _worker(rank, world, path, outdir, dense, n=N):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded_randomk import ShardedRandomK
     eng = ShardedRandomK(RATIO, dense=dense, rng="torch_cpu", kernels=OracleRandomKKernels())
-    lo, hi = eng.partition(N, world)[rank]
+    lo, hi = eng.partition(n, world)[rank]
     res = {}
     for s in range(3):
-        out = eng.step(torch.from_numpy(_grad(s)[lo:hi].copy()), NAME, N)
+        out = eng.step(torch.from_numpy(_grad(s, n)[lo:hi].copy()), NAME, n)
         res[f"out{s}"] = out.numpy()
         res[f"res{s}"] = eng.residuals[NAME].numpy().copy()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), lo=np.array([lo, hi]), **res)
     dist.destroy_process_group()
 
 
-def _oracle():
+def _oracle(n=N):
     r = None
     outs, ress = [], []
     for s in range(3):
-        g = _grad(s)
+        g = _grad(s, n)
         t = g.copy() if r is None else O.residual_compensate(g, r)
-        idx, _ = O.randomk_indices(NAME, s, N, RATIO)
-        dec = O.randomk_decode(t[idx], idx, N)
+        idx, _ = O.randomk_indices(NAME, s, n, RATIO)
+        dec = O.randomk_decode(t[idx], idx, n)
         r = O.residual_update(t, dec)
         outs.append(O.python_sum([dec]))
         ress.append(r)
@@ -82,16 +82,18 @@ def _bits(a, b):
     return np.array_equal(np.asarray(a, F32).view(np.uint32), np.asarray(b, F32).view(np.uint32))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,n", [(2, N), (3, N), (3, 6)])
 @pytest.mark.parametrize("dense", ["replicated", "shard"])
-def test_sharded_randomk_matches_oracle_sequence(world, dense):
+def test_sharded_randomk_matches_oracle_sequence(world, n, dense):
+    """(3, 6): 4-element blocks over 3 ranks -- the last rank holds no element and still joins the
+    all-reduce (replicated) or returns an empty slice (shard)."""
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, dense, n), nprocs=world, join=True)
         outs = []
         for r in range(world):
             with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
                 outs.append({k: z[k] for k in z.files})
-    exp_out, exp_res = _oracle()
+    exp_out, exp_res = _oracle(n)
     for s in range(3):
         assert _bits(np.concatenate([o[f"res{s}"] for o in outs]), exp_res[s]), s
         if dense == "shard":
@@ -99,4 +101,4 @@ def test_sharded_randomk_matches_oracle_sequence(world, dense):
         else:
             for o in outs:
                 assert _bits(o[f"out{s}"], exp_out[s]), s
-    assert outs[0]["lo"][0] == 0 and outs[-1]["lo"][1] == N
+    assert outs[0]["lo"][0] == 0 and outs[-1]["lo"][1] == n
