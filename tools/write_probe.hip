@@ -7,6 +7,7 @@
 //   4 one 32 KiB tile per block, 8 x 16 B per lane (the W > 1 decode's write shape), non-temporal
 //   5 the same, plain
 //   6 hipMemsetD32Async (the runtime's fill); 7-11 other tile / block shapes
+//   12-14 wave-contiguous tiles (each wave's stores one contiguous span); 15-19 the tile shapes read
 // Build: hipcc --offload-arch=gfx950 -O3 tools/write_probe.hip -o tools/write_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -32,6 +33,27 @@ __global__ __launch_bounds__(BS) void fill_tile(f4* o, float v) {
     else base[u * BS + threadIdx.x] = f4{v, v, v, v};
   }
 }
+// wave-contiguous: wave w of the block writes its own contiguous 64 x PER x 16 B piece of the tile
+// (store u of lane l at w * 64 * PER + 64 u + l), so each wave's stores burst into one span
+template <int PER, int BS = 256>
+__global__ __launch_bounds__(BS) void fill_tile_wc(f4* o, float v) {
+  f4* base = o + (long)blockIdx.x * BS * PER + (threadIdx.x >> 6) * 64 * PER + (threadIdx.x & 63);
+#pragma unroll
+  for (int u = 0; u < PER; ++u) __builtin_nontemporal_store(f4{v, v, v, v}, base + 64 * u);
+}
+// read probes: the same two tile layouts read (non-temporal loads), a per-thread sum kept live
+template <int PER, bool WC, int BS = 256>
+__global__ __launch_bounds__(BS) void read_tile(const f4* x, float* sink) {
+  const f4* base = WC ? x + (long)blockIdx.x * BS * PER + (threadIdx.x >> 6) * 64 * PER + (threadIdx.x & 63)
+                      : x + (long)blockIdx.x * BS * PER + threadIdx.x;
+  f4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) v[u] = __builtin_nontemporal_load(base + (WC ? 64 : BS) * u);
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  if (acc == 12345.678f) sink[0] = acc;
+}
 
 int main() {
   const long n = 1L << 26, n4 = n / 4;
@@ -45,8 +67,13 @@ int main() {
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const char* names[] = {"stride nt", "stride plain", "tile16K nt", "tile16K plain", "tile32K nt", "tile32K plain",
                          "hipMemsetD32Async", "tile4K nt", "tile8K nt", "tile64K/1024 nt", "tile32K/512 nt",
-                         "tile16K/1024 nt"};
-  for (int v = 0; v < 12; ++v) {
+                         "tile16K/1024 nt", "tile32K wave-contig nt", "tile16K wave-contig nt",
+                         "tile8K wave-contig nt", "read tile32K interleaved", "read tile32K wave-contig",
+                         "read tile16K interleaved", "read tile16K wave-contig", "read tile4K"};
+  float* sink = nullptr;
+  if (hipMalloc(&sink, 64) != hipSuccess) { printf("alloc failed\n"); return 1; }
+  const int first = getenv("WP_FIRST") ? atoi(getenv("WP_FIRST")) : 0;
+  for (int v = first; v < 20; ++v) {
     std::vector<float> ts;
     for (int r = 0; r < 25; ++r) {
       f4* o = buf[r % 3];
@@ -64,6 +91,14 @@ int main() {
         case 9: fill_tile<true, 4, 1024><<<(unsigned)(n4 / 4096), 1024>>>(o, 0.f); break;
         case 10: fill_tile<true, 4, 512><<<(unsigned)(n4 / 2048), 512>>>(o, 0.f); break;
         case 11: fill_tile<true, 1, 1024><<<(unsigned)(n4 / 1024), 1024>>>(o, 0.f); break;
+        case 12: fill_tile_wc<8><<<(unsigned)(n4 / (256 * 8)), 256>>>(o, 0.f); break;
+        case 13: fill_tile_wc<4><<<(unsigned)(n4 / (256 * 4)), 256>>>(o, 0.f); break;
+        case 14: fill_tile_wc<2><<<(unsigned)(n4 / (256 * 2)), 256>>>(o, 0.f); break;
+        case 15: read_tile<8, false><<<(unsigned)(n4 / (256 * 8)), 256>>>(o, sink); break;
+        case 16: read_tile<8, true><<<(unsigned)(n4 / (256 * 8)), 256>>>(o, sink); break;
+        case 17: read_tile<4, false><<<(unsigned)(n4 / (256 * 4)), 256>>>(o, sink); break;
+        case 18: read_tile<4, true><<<(unsigned)(n4 / (256 * 4)), 256>>>(o, sink); break;
+        case 19: read_tile<1, false><<<(unsigned)(n4 / 256), 256>>>(o, sink); break;
       }
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
