@@ -221,7 +221,7 @@ def bench_sharded_codec(args, world, rank, dev, codec):
     return {"metric": f"grad-codec GB/s (device-resident encode+decode), {codec} over the ResNet-50 set sharded",
             "value": round(4.0 * n / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 4),
             "scaling": "strong",
-            "config": {"workload": f"Sharded{'TernGrad' if codec == 'terngrad' else 'Quant(qsgd 127, bucket 128)'}: "
+            "config": {"workload": f"Sharded{'TernGrad (2-bit packed codes on the wire)' if codec == 'terngrad' else 'Quant(qsgd 127, bucket 128)'}: "
                                    f"161 ResNet-50 tensors ({n} elements) as one bucket over {world} rank(s), "
                                    "replicated dense decode (BASELINE configs[2], SURVEY §8e)",
                        "numel": n, "shard_max": m, "parallelism": f"{world} contiguous unit-aligned shards"},

@@ -16,9 +16,13 @@ Per step on rank r (grace_terngrad_shard_*, grace_terngrad_scalars):
   3. shard_encode: this rank's codes (the device generator keyed by GLOBAL element index, so the
      codes equal the single-GPU ones for the same seed, or an injected u); grace_terngrad_scalars:
      every tensor's scalar, derived on every rank -- nothing but the slots travels before the codes;
-  4. dense="replicated": ONE all_gather of the codes (1 B per element) and the decode of the whole
-     bucket on every rank; dense="shard": the decode of this rank's elements only, no second
-     collective (reduce-scatter semantics).
+  4. dense="replicated": ONE all_gather of the codes and the decode of the whole bucket on every
+     rank; dense="shard": the decode of this rank's elements only, no second collective
+     (reduce-scatter semantics).
+Wire of step 4 (``wire``): "packed2" (default) moves the codes as code + 1 in the 2-bit planar byte
+layout of the reference's packing (grace_dl/tensorflow/compressor/packing.py:4-29, grace_tern_pack /
+grace_tern_unpack): a quarter of the int8 bytes over xGMI, unpacked straight into the flat code
+buffer; "int8" moves the codes as they are (1 B per element).  The decoded result is the same.
 Partition: the units in equal contiguous blocks (rank r: units [r U, (r + 1) U), U = ceil(units / W)),
 so the slot all-gather lands every unit at its global index; partition() gives every rank's element
 range and step() takes exactly that shard.  No host synchronisation in a step.
@@ -62,6 +66,17 @@ class NativeTernKernels:
     def decode(self, codes, scalars, sizes, n):
         return ops.terngrad_decompress(codes, scalars, n, sizes)
 
+    def pack_bytes(self, n):
+        return int(_lib.query("grace_pack2_bytes", int(n)))
+
+    def pack(self, codes, out):
+        """codes (int8 {-1, 0, 1}) -> out[:pack_bytes(codes.numel())], the 2-bit layout of code + 1"""
+        _lib.call("grace_tern_pack", codes.data_ptr(), codes.numel(), out.data_ptr(), ops._stream())
+
+    def unpack(self, packed, n, out):
+        """the first pack_bytes(n) bytes of packed -> n int8 codes into out"""
+        _lib.call("grace_tern_unpack", packed.data_ptr(), int(n), out.data_ptr(), ops._stream())
+
 
 class _Plan:
     """The unit partition of one segment table over `world` ranks."""
@@ -98,11 +113,14 @@ class _Plan:
 class ShardedTernGrad:
     """TernGrad over one bucket whose work units are sharded across the ranks of `group`."""
 
-    def __init__(self, group=None, dense="replicated", kernels=None, seed=0):
+    def __init__(self, group=None, dense="replicated", kernels=None, seed=0, wire="packed2"):
         if dense not in ("replicated", "shard"):
             raise ValueError("dense must be 'replicated' or 'shard'")
+        if wire not in ("packed2", "int8"):
+            raise ValueError("wire must be 'packed2' or 'int8'")
         self.group = group
         self.dense = dense
+        self.wire = wire
         self.seed = seed
         self.k_ops = kernels or NativeTernKernels()
         self._plans = {}
@@ -151,7 +169,8 @@ class ShardedTernGrad:
             # this rank's block (a copy: the collective's input must not alias its output)
             dist.all_gather_into_tensor(slots[:world * plan.U], slots[u0:u0 + plan.U].clone(), group=self.group)
         seed = self.seed if seed is None else seed
-        if self.dense == "replicated" and world > 1:
+        packed = self.wire == "packed2"
+        if self.dense == "replicated" and world > 1 and not packed:
             sendc = torch.empty(plan.max_len, dtype=torch.int8, device=dev)
             codes = sendc[:hi - lo]
         else:
@@ -167,9 +186,21 @@ class ShardedTernGrad:
             return K.decode(codes, scalars[s0:s1 + 1], own, hi - lo)
         if world == 1:
             return K.decode(codes, scalars, plan.sizes, plan.n)
+        full = torch.empty(plan.n, dtype=torch.int8, device=dev)
+        if packed:
+            # every rank's block padded to the longest range's packed size (16-B multiples)
+            pb = (K.pack_bytes(plan.max_len) + 15) // 16 * 16
+            send = torch.empty(pb, dtype=torch.uint8, device=dev)
+            if hi > lo:
+                K.pack(codes, send)
+            gathered = torch.empty(world * pb, dtype=torch.uint8, device=dev)
+            dist.all_gather_into_tensor(gathered, send, group=self.group)
+            for w, (a, b) in enumerate(plan.ranges):   # each block unpacked into its range
+                if b > a:
+                    K.unpack(gathered[w * pb:(w + 1) * pb], b - a, full[a:b])
+            return K.decode(full, scalars, plan.sizes, plan.n)
         gathered = torch.empty(world * plan.max_len, dtype=torch.int8, device=dev)
         dist.all_gather_into_tensor(gathered, sendc, group=self.group)
-        full = torch.empty(plan.n, dtype=torch.int8, device=dev)
         for w, (a, b) in enumerate(plan.ranges):   # the padded blocks, back to one flat code buffer
             if b > a:
                 full[a:b].copy_(gathered[w * plan.max_len:w * plan.max_len + (b - a)])

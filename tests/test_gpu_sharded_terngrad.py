@@ -32,8 +32,8 @@ def _worker(rank, world, path, outdir, mode):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from grace_amd.dist.sharded_terngrad import ShardedTernGrad
-    dense, use_u, use_clip = mode
-    eng = ShardedTernGrad(dense=dense, seed=11)
+    dense, use_u, use_clip, wire = mode
+    eng = ShardedTernGrad(dense=dense, seed=11, wire=wire)
     flat, u, clip = _data(3)
     lo, hi = eng.partition(SIZES)[rank]
     res = {"lo": np.array([lo, hi])}
@@ -53,8 +53,9 @@ def _bits(a, b):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("mode", [("replicated", False, False), ("replicated", True, True),
-                                  ("replicated", False, True), ("shard", True, False)])
+# (dense, injected u, injected clip, wire of the code all-gather)
+@pytest.mark.parametrize("mode", [("replicated", False, False, "packed2"), ("replicated", True, True, "packed2"),
+                                  ("replicated", False, True, "int8"), ("shard", True, False, "packed2")])
 def test_sharded_terngrad_native_matches_single_gpu(world, mode):
     from grace_amd import ops
     with tempfile.TemporaryDirectory() as tmp:
@@ -63,7 +64,7 @@ def test_sharded_terngrad_native_matches_single_gpu(world, mode):
         for r in range(world):
             with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
                 outs.append({k: z[k] for k in z.files})
-    dense, use_u, use_clip = mode
+    dense, use_u, use_clip, _ = mode
     flat, u, clip = _data(3)
     for step in range(2):
         x = torch.from_numpy(flat * F32(step + 1)).cuda()

@@ -88,16 +88,27 @@ class OracleTernKernels:
         sc = np.repeat(scalars.numpy().astype(F32), sizes)
         return torch.from_numpy((codes.numpy().astype(F32) * sc).astype(F32))
 
+    def pack_bytes(self, n):
+        return n // 4 + 1   # packing.py pads with range(0, 4 - n % 4)
+
+    def pack(self, codes, out):
+        p = O.pack2_encode(codes.numpy().astype(np.int64) + 1)
+        out[:p.size].copy_(torch.from_numpy(p))
+
+    def unpack(self, packed, n, out):
+        v = O.pack2_decode(packed.numpy()[:self.pack_bytes(n)], n) - 1
+        out.copy_(torch.from_numpy(v.astype(np.int8)))
+
 
 def _bucket(sizes, seed):
     rng = np.random.default_rng(seed)
     return [(rng.standard_normal(n) * (0.01 * (i + 1))).astype(F32) for i, n in enumerate(sizes)]
 
 
-def _worker(rank, world, path, outdir, sizes, dense, use_clip):
+def _worker(rank, world, path, outdir, sizes, dense, use_clip, wire="packed2"):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded_terngrad import ShardedTernGrad
-    eng = ShardedTernGrad(dense=dense, kernels=OracleTernKernels())
+    eng = ShardedTernGrad(dense=dense, kernels=OracleTernKernels(), wire=wire)
     flat = np.concatenate(_bucket(sizes, 7))
     u = np.random.default_rng(8).random(flat.size).astype(F32)
     clip = torch.from_numpy(np.array([0.015 * (i + 1) for i in range(len(sizes))], dtype=F32)) if use_clip else None
@@ -108,9 +119,10 @@ def _worker(rank, world, path, outdir, sizes, dense, use_clip):
     dist.destroy_process_group()
 
 
-def _run(world, sizes, dense, use_clip):
+def _run(world, sizes, dense, use_clip, wire="packed2"):
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, dense, use_clip), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, sizes, dense, use_clip, wire), nprocs=world,
+                 join=True)
         outs = []
         for r in range(world):
             with np.load(os.path.join(tmp, f"r{r}.npz")) as z:
@@ -138,8 +150,9 @@ SIZES = [500, 97, 1, 1234, 96, 98, 3000, 5]
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("use_clip", [True, False])
-def test_sharded_terngrad_matches_single_bucket(world, use_clip):
-    outs = _run(world, SIZES, "replicated", use_clip)
+@pytest.mark.parametrize("wire", ["packed2", "int8"])
+def test_sharded_terngrad_matches_single_bucket(world, use_clip, wire):
+    outs = _run(world, SIZES, "replicated", use_clip, wire)
     out1, codes1, sc1, flat, u = _single(SIZES, use_clip)
     assert _bits(np.concatenate([o["codes"] for o in outs]), codes1.astype(F32))
     for o in outs:
@@ -161,3 +174,28 @@ def test_sharded_terngrad_dense_shard_mode():
     outs = _run(2, SIZES, "shard", True)
     out1 = _single(SIZES, True)[0]
     assert _bits(np.concatenate([o["out"] for o in outs]), out1)
+
+
+@pytest.mark.parametrize("wire", ["packed2", "int8"])
+def test_sharded_terngrad_rank_without_units(wire):
+    """Two work units over 3 ranks: the last rank holds no element, still joins both all-gathers
+    (its packed block is padding only) and decodes the whole bucket."""
+    sizes = [150]
+    outs = _run(3, sizes, "replicated", True, wire)
+    out1 = _single(sizes, True)[0]
+    assert int(outs[-1]["lo"][0]) == int(outs[-1]["lo"][1])
+    for o in outs:
+        assert _bits(o["out"], out1)
+
+
+def test_pack2_wire_of_ternary_codes_round_trips():
+    """The emulator's wire (packing.py layout of code + 1) is lossless for every length mod 4."""
+    k = OracleTernKernels()
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 3, 4, 5, 97, 1000):
+        c = torch.from_numpy(rng.integers(-1, 2, n).astype(np.int8))
+        buf = torch.zeros(k.pack_bytes(n) + 16, dtype=torch.uint8)
+        k.pack(c, buf)
+        out = torch.empty(n, dtype=torch.int8)
+        k.unpack(buf, n, out)
+        assert torch.equal(out, c), n
