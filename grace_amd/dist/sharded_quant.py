@@ -16,7 +16,10 @@ the bucket -- so a step is: encode this rank's shard (the device generator keyed
 element index, so the codes equal the whole-bucket call's: ``grace_*_compress_at``), then
 ``dense="replicated"``: ONE all-gather of the codes (and QSGD's bucket norms, in the same padded
 record) and the decode of the whole bucket on every rank; ``dense="shard"``: the decode of this
-rank's range only, no collective at all.
+rank's range only, no collective at all.  sign with ``wire="bits"`` (its default): the codes are
+encoded straight into the 1-bit layout (grace_sign_encode_bits: word i bit j = x[32 i + j] >= 0),
+an eighth of the u8 codes' bytes cross the wire, and the gathered words decode as a majority of one
+(grace_sign_majority_bits, world 1: 2 b - 1) -- the same floats as the u8 path (``wire="u8"``).
 
 Partition: QSGD by whole buckets (each tensor's buckets counted from its start, in equal contiguous
 blocks per rank, as sharded TernGrad's work units); the element-wise codecs by 128-element blocks of
@@ -27,7 +30,7 @@ a step.  ``kernels`` defaults to the native HIP set; the CPU tests inject an ora
 import torch
 import torch.distributed as dist
 
-from grace_amd import ops
+from grace_amd import _lib, ops
 
 CODECS = ("sign", "fp16", "natural", "cnat", "qsgd")
 _BLOCK = 128   # element-wise codecs: partition granule (a multiple of the generator's quad)
@@ -56,6 +59,14 @@ class NativeQuantKernels:
         if codec in ("natural", "cnat"):
             return ops.natural_decompress(codes, n, 0 if codec == "natural" else 1)
         return ops.qsgd_decompress(codes, norms, q, bucket, n, sizes=sizes, variant=variant)
+
+    def encode_bits(self, x, words):
+        """sign codes of x straight into the 1-bit words (ceil(n / 32) int32)"""
+        _lib.call("grace_sign_encode_bits", x.data_ptr(), x.numel(), words.data_ptr(), ops._stream())
+
+    def decode_bits(self, words, n, out):
+        """n elements of 1-bit sign words -> out = 2 b - 1 (the majority of one payload)"""
+        _lib.call("grace_sign_majority_bits", words.data_ptr(), 0, 1, int(n), out.data_ptr(), ops._stream())
 
     def code_dtype(self, codec, q):
         if codec == "fp16" or (codec == "qsgd" and q >= 128):
@@ -99,9 +110,12 @@ class ShardedQuant:
     """A sign / fp16 / natural / cnat / QSGD bucket whose elements are sharded across `group`."""
 
     def __init__(self, codec, group=None, dense="replicated", quantum_num=127, bucket_size=128, variant=0,
-                 deterministic=False, kernels=None, seed=0):
+                 deterministic=False, kernels=None, seed=0, wire=None):
         if codec not in CODECS:
             raise ValueError(f"codec must be one of {CODECS}")
+        if wire not in (None, "bits", "u8") or (wire == "bits" and codec != "sign"):
+            raise ValueError("wire: 'bits' or 'u8' for sign (default 'bits'); the other codecs send their codes as they are")
+        self.bits = codec == "sign" and wire != "u8"
         if dense not in ("replicated", "shard"):
             raise ValueError("dense must be 'replicated' or 'shard'")
         self.codec = codec
@@ -114,7 +128,7 @@ class ShardedQuant:
         self.seed = seed
         self.k_ops = kernels or NativeQuantKernels()
         self._plans = {}
-        self.last_codes = None     # this rank's codes (its element range)
+        self.last_codes = None     # this rank's codes (its element range; sign with wire="bits": int32 words)
         self.last_norms = None     # QSGD: this rank's bucket norms
 
     def _world(self):
@@ -151,6 +165,8 @@ class ShardedQuant:
             raise ValueError(f"ShardedQuant: rank {rank} holds {x.numel()} elements, its range is {hi - lo} "
                              "(use partition(sizes))")
         seed = self.seed if seed is None else seed
+        if self.bits:
+            return self._step_bits(x, plan, world, rank, lo, hi)
         parts = plan.parts[rank]
         if hi > lo:
             codes, norms = K.encode(self.codec, x, lo, parts, u, seed, self.q, self.bucket, self.variant,
@@ -187,3 +203,34 @@ class ShardedQuant:
                 if u1 > u0:
                     allnorms[u0:u1].copy_(g[w, cb:cb + (u1 - u0) * 4].view(torch.float32))
         return K.decode(self.codec, full, allnorms, list(plan.sizes), plan.n, self.q, self.bucket, self.variant)
+
+    def _step_bits(self, x, plan, world, rank, lo, hi):
+        """sign over the 1-bit wire: rank r's words are its block of the bucket's bit stream (its
+        range starts on a 128-element block), padded to the longest range's words."""
+        K = self.k_ops
+        dev = x.device
+        nw = (hi - lo + 31) // 32
+        if self.dense == "shard" or world == 1:
+            out = torch.empty(hi - lo, dtype=torch.float32, device=dev)
+            words = torch.empty(nw, dtype=torch.int32, device=dev)
+            if hi > lo:
+                K.encode_bits(x, words)
+                K.decode_bits(words, hi - lo, out)
+            self.last_codes, self.last_norms = words, None
+            return out
+        per = ((plan.max_len + 31) // 32 + 3) // 4 * 4      # words per rank block, 16-B multiples
+        send = torch.zeros(per, dtype=torch.int32, device=dev)
+        if hi > lo:
+            K.encode_bits(x, send[:nw])
+        self.last_codes, self.last_norms = send[:nw], None
+        gathered = torch.empty(world * per, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(gathered, send, group=self.group)
+        out = torch.empty(plan.n, dtype=torch.float32, device=dev)
+        if all(b - a == per * 32 for a, b in plan.ranges[:-1]):
+            # every block but the last is whole: the gathered words are the bucket's bit stream
+            K.decode_bits(gathered, plan.n, out)
+        else:
+            for w, (a, b) in enumerate(plan.ranges):
+                if b > a:
+                    K.decode_bits(gathered[w * per:(w + 1) * per], b - a, out[a:b])
+        return out

@@ -40,7 +40,9 @@ def _worker(rank, world, path, outdir, codec, dense, use_u, det, q, sizes=SIZES)
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from grace_amd.dist.sharded_quant import ShardedQuant
-    eng = ShardedQuant(codec, dense=dense, quantum_num=q, bucket_size=BUCKET, deterministic=det, seed=13)
+    codec, _, wire = codec.partition(":")   # "sign:u8": the u8 wire instead of the 1-bit default
+    eng = ShardedQuant(codec, dense=dense, quantum_num=q, bucket_size=BUCKET, deterministic=det, seed=13,
+                       wire=wire or None)
     flat, u, ri = _data(4, sizes)
     lo, hi = eng.partition(sizes)[rank]
     s = _stream(codec, use_u, u, ri)
@@ -55,6 +57,7 @@ def _worker(rank, world, path, outdir, codec, dense, use_u, det, q, sizes=SIZES)
 
 def _single(codec, x, s, det, q, sizes=SIZES):
     from grace_amd import ops
+    codec = codec.partition(":")[0]
     n = x.numel()
     if codec == "sign":
         return ops.sign_decode(ops.sign_encode(x))
@@ -72,7 +75,7 @@ def _bits(a, b):
     return np.array_equal(np.asarray(a, F32).view(np.uint32), np.asarray(b, F32).view(np.uint32))
 
 
-CASES = [("sign", False, False, Q), ("fp16", False, False, Q), ("natural", False, False, Q),
+CASES = [("sign", False, False, Q), ("sign:u8", False, False, Q), ("fp16", False, False, Q), ("natural", False, False, Q),
          ("natural", True, False, Q), ("cnat", False, False, Q), ("cnat", True, False, Q), ("cnat", False, True, Q),
          ("qsgd", False, False, Q), ("qsgd", True, False, Q), ("qsgd", False, False, 255)]
 
@@ -81,7 +84,7 @@ CASES = [("sign", False, False, Q), ("fp16", False, False, Q), ("natural", False
 @pytest.mark.parametrize("codec,use_u,det,q", CASES)
 @pytest.mark.parametrize("dense", ["replicated", "shard"])
 def test_sharded_quant_native_matches_single_gpu(world, codec, use_u, det, q, dense):
-    if dense == "shard" and world == 3 and codec in ("sign", "fp16"):
+    if dense == "shard" and world == 3 and codec in ("sign", "sign:u8", "fp16"):
         pytest.skip("covered by world 2 (deterministic codecs)")
     with tempfile.TemporaryDirectory() as tmp:
         mp.spawn(_worker, args=(world, os.path.join(tmp, "rdv"), tmp, codec, dense, use_u, det, q), nprocs=world,

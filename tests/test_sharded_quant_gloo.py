@@ -47,6 +47,17 @@ class OracleQuantKernels:
             a += s
         return torch.from_numpy(np.concatenate(codes)), torch.from_numpy(np.concatenate(norms).astype(F32))
 
+    def encode_bits(self, x, words):
+        b = O.sign_encode(x.numpy()).astype(np.uint8)
+        by = np.zeros(4 * words.numel(), np.uint8)
+        pk = np.packbits(b, bitorder="little")
+        by[:pk.size] = pk
+        words.copy_(torch.from_numpy(by.view("<i4").copy()))
+
+    def decode_bits(self, words, n, out):
+        b = np.unpackbits(words.numpy().view(np.uint8), bitorder="little")[:n]
+        out.copy_(torch.from_numpy(O.sign_decode(b)))
+
     def decode(self, codec, codes, norms, sizes, n, q, bucket, variant):
         c = codes.numpy()
         if codec == "sign":
@@ -83,8 +94,9 @@ def _stream(codec, u, ri):
 def _worker(rank, world, path, outdir, codec, dense, det, sizes=SIZES):
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=rank, world_size=world)
     from grace_amd.dist.sharded_quant import ShardedQuant
+    codec, _, wire = codec.partition(":")   # "sign:u8": the u8 wire instead of the 1-bit default
     eng = ShardedQuant(codec, dense=dense, quantum_num=Q, bucket_size=BUCKET, deterministic=det,
-                       kernels=OracleQuantKernels())
+                       kernels=OracleQuantKernels(), wire=wire or None)
     flat, u, ri = _data(5, sizes)
     lo, hi = eng.partition(sizes)[rank]
     s = _stream(codec, u, ri)
@@ -94,6 +106,7 @@ def _worker(rank, world, path, outdir, codec, dense, det, sizes=SIZES):
 
 
 def _expected(codec, det, sizes=SIZES):
+    codec = codec.partition(":")[0]
     flat, u, ri = _data(5, sizes)
     K = OracleQuantKernels()
     s = torch.from_numpy(_stream(codec, u, ri))
@@ -106,7 +119,8 @@ def _bits(a, b):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("codec,det", [("sign", False), ("fp16", False), ("natural", False), ("cnat", False),
+@pytest.mark.parametrize("codec,det", [("sign", False), ("sign:u8", False), ("fp16", False), ("natural", False),
+                                       ("cnat", False),
                                        ("cnat", True), ("qsgd", False)])
 @pytest.mark.parametrize("dense", ["replicated", "shard"])
 def test_sharded_quant_matches_whole_bucket(world, codec, det, dense):
@@ -127,7 +141,7 @@ def test_sharded_quant_matches_whole_bucket(world, codec, det, dense):
     assert los[0][0] == 0 and los[-1][1] == flat.size and all(los[i][1] == los[i + 1][0] for i in range(world - 1))
     seg = np.cumsum([0] + SIZES)
     for a, _ in los:
-        if codec == "qsgd":
+        if codec.startswith("qsgd"):
             t = np.searchsorted(seg, a, side="right") - 1
             assert (a - seg[t]) % BUCKET == 0
         else:
