@@ -80,6 +80,8 @@ SIGNATURES = {
     "grace_dgc_select": (ST, [P, I64, P, I64, ctypes.c_double, P, P]),
     "grace_dgc_step_w1": (ST, [P, P, P, I64, P, P, P]),
     "grace_dgc_sample_comp": (ST, [P, P, P, I32, F32, I64, P, U64, I64, P, P]),
+    "grace_dgc_sample_kth_workspace_bytes": (SZ, []),
+    "grace_dgc_sample_kth": (ST, [P, I64, I64, P, P, P]),
     "grace_dgc_step_w1_fused_workspace_bytes": (SZ, [I64]),
     "grace_dgc_step_w1_fused": (ST, [P, P, P, I32, F32, I64, P, I64, ctypes.c_double, P, P, P, P, P]),
     "grace_sumsq_workspace_bytes": (SZ, []),

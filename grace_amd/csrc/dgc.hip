@@ -87,6 +87,15 @@ __device__ __forceinline__ void dgc_comp1(float gv, float& rv, float& av, int ha
 }
 __device__ __forceinline__ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// The device generator's sample index j: iid uniform over [0, n) (dgc.py:17-19 draws numel-range
+// uniforms).  (A stratified draw, one uniform index per stratum of n / ns elements, made the gather
+// SLOWER -- 54.9 vs 42.8 us for 671 K samples of g, r, a: the chip's in-flight gathers then crowd a
+// few MB of addresses instead of spreading over every bank; profiles/r05_dgc_ab.txt.)
+__device__ __forceinline__ int64_t dgc_sample_index(uint64_t seed, int64_t j, int64_t n) {
+  const uint64_t h = ((uint64_t)rand32(seed, (uint64_t)j) << 32) | rand32(seed ^ 0xD6E8FEB86659FD93ull, (uint64_t)j);
+  return (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
+}
+
 // ------------------------------------------------------------------------------------------------
 // sample: |t[idx_j]|, idx from the caller (parity: torch's CPU uniform_(0, numel).long()) or the
 // counter-based generator (uniform integer in [0, numel))
@@ -98,8 +107,7 @@ __global__ __launch_bounds__(kDBlock) void dgc_sample_kernel(const float* __rest
     if (sidx) {
       i = sidx[j];
     } else {
-      const uint64_t h = ((uint64_t)rand32(seed, (uint64_t)j) << 32) | rand32(seed ^ 0xD6E8FEB86659FD93ull, (uint64_t)j);
-      i = (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
+      i = dgc_sample_index(seed, j, n);
     }
     out[j] = fabsf(t[i]);
   }
@@ -118,14 +126,117 @@ __global__ __launch_bounds__(kDBlock) void dgc_sample_comp_kernel(const float* _
     if (sidx) {
       i = sidx[j];
     } else {
-      const uint64_t h = ((uint64_t)rand32(seed, (uint64_t)j) << 32) | rand32(seed ^ 0xD6E8FEB86659FD93ull, (uint64_t)j);
-      i = (int64_t)(((unsigned __int128)h * (uint64_t)n) >> 64);
+      i = dgc_sample_index(seed, j, n);
     }
     const float gv = g[i];
     float rv = has_state ? r[i] : 0.f, av = has_state ? a[i] : 0.f;
     dgc_comp1(gv, rv, av, has_state, momentum);
     out[j] = fabsf(av);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// thr0 without the sample's full top-k: torch.topk(samples, k_s)[0].min() (dgc.py:20-21) is the
+// k_s-th largest sampled magnitude, or NaN when the sample holds a NaN (topk ranks NaN above
+// everything and torch.min propagates it).  Radix select on the magnitude bits (order-preserving for
+// sign-clear floats) in three digits, one launch each: 11 bits (30..20), 11 bits (19..9), 9 bits
+// (8..0).  Every workgroup loads all of its elements first (one memory latency), histograms those
+// that share the digits chosen so far in LDS and adds its non-zero bins to a global histogram with
+// agent-scope atomics; after vmcnt(0) it takes a ticket, and the last to arrive reads the histogram
+// back (agent-scope loads: the other XCDs' adds are not in its L2), picks the digit holding the
+// remaining rank counting down from the top, and re-zeroes what it consumed (the state is left
+// zeroed).  No cache-wide fences.  (8 copies of the global histogram, blockIdx % 8, summed by the
+// last arriver: no faster -- profiles/r05_dgc_ab.txt.)
+constexpr int kKthBlock = 256;
+constexpr int kKthBins = 2048;
+constexpr int kKthPer = 16;      // elements per thread per round, all loads in flight together
+struct KthState {
+  uint32_t hist[kKthBins];
+  uint32_t prefix;   // the digits chosen so far, in place
+  uint32_t kleft;    // the rank still to find among the elements sharing them (1-based)
+  uint32_t nan;
+  uint32_t ticket;
+};
+
+template <int L>
+__global__ __launch_bounds__(kKthBlock) void dgc_kth_kernel(const float* __restrict__ x, int64_t ns, uint32_t ks,
+                                                            KthState* __restrict__ st, float* __restrict__ out) {
+  constexpr int kShift = L == 0 ? 20 : (L == 1 ? 9 : 0);
+  constexpr int kBins = L == 2 ? 512 : 2048;
+  constexpr int kHi = L == 0 ? 31 : (L == 1 ? 20 : 9);   // bits at and above this must match the prefix
+  __shared__ uint32_t h[kKthBins];
+  __shared__ uint32_t s_last, s_nan;
+  const int t = threadIdx.x;
+  for (int b = t; b < kBins; b += kKthBlock) h[b] = 0u;
+  if (t == 0) s_nan = 0u;
+  const uint32_t pre = L == 0 ? 0u : st->prefix;   // written by the previous launch's last arriver
+  __syncthreads();
+  uint32_t nan = 0;
+  for (int64_t base = (int64_t)blockIdx.x * (kKthBlock * kKthPer); base < ns;
+       base += (int64_t)gridDim.x * (kKthBlock * kKthPer)) {
+    uint32_t key[kKthPer];
+#pragma unroll
+    for (int u = 0; u < kKthPer; ++u) {
+      const int64_t j = base + u * kKthBlock + t;
+      key[u] = j < ns ? abs_key(x[j]) : 0xFFFFFFFFu;   // no magnitude has the sign bit
+    }
+#pragma unroll
+    for (int u = 0; u < kKthPer; ++u) {
+      if (key[u] == 0xFFFFFFFFu) continue;
+      if constexpr (L == 0) nan |= key[u] > 0x7F800000u;
+      if (L == 0 || (key[u] >> kHi) == (pre >> kHi)) atomicAdd(&h[(key[u] >> kShift) & (kBins - 1)], 1u);
+    }
+  }
+  if constexpr (L == 0) { if (nan) s_nan = 1u; }
+  __syncthreads();
+  for (int b = t; b < kBins; b += kKthBlock)
+    if (h[b]) __hip_atomic_fetch_add(&st->hist[b], h[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (L == 0 && t == 0 && s_nan) __hip_atomic_fetch_or(&st->nan, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this workgroup's adds have completed
+  __syncthreads();
+  if (t == 0) s_last = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int b = t; b < kBins; b += kKthBlock) {
+    h[b] = __hip_atomic_load(&st->hist[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h[b]) __hip_atomic_store(&st->hist[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (t >= kWave) return;
+  // wave 0: lane l owns bins [l per, (l + 1) per); suffix sums over the lanes find the lane holding
+  // the remaining rank, which then walks its bins from the top
+  constexpr int per = kBins / kWave;
+  const uint32_t kl = L == 0 ? ks : st->kleft;
+  uint32_t s = 0;
+  for (int b = 0; b < per; ++b) s += h[t * per + b];
+  uint32_t suf = s;
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t v = __shfl_down(suf, o, kWave);
+    if (t + o < kWave) suf += v;
+  }
+  const uint64_t reach = __ballot(suf >= kl);
+  const int owner = 63 - __builtin_clzll(reach);   // lanes 0..owner reach the rank (suffix sums fall with l)
+  if (t != owner) return;
+  uint32_t rem = kl - (suf - s);
+  int bin = per - 1;
+  for (; bin > 0; --bin) {
+    const uint32_t c = h[t * per + bin];
+    if (rem <= c) break;
+    rem -= c;
+  }
+  const uint32_t key = pre | ((uint32_t)(t * per + bin) << kShift);
+  if constexpr (L == 2) {
+    const uint32_t nn = __hip_atomic_load(&st->nan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[0] = nn ? u2f(0x7FC00000u) : u2f(key);
+    __hip_atomic_store(&st->nan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->prefix = 0u;
+    st->kleft = 0u;
+  } else {
+    st->prefix = key;
+    st->kleft = rem;
+  }
+  __hip_atomic_store(&st->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -822,6 +933,25 @@ grace_status_t grace_dgc_sample_comp(const float* g, const float* residual, cons
   return GRACE_OK;
 }
 
+size_t grace_dgc_sample_kth_workspace_bytes(void) { return al256(sizeof(KthState)); }
+
+grace_status_t grace_dgc_sample_kth(const float* sample_abs, int64_t ns, int64_t ks, void* ws, float* out,
+                                    void* stream) {
+  GRACE_REQUIRE(sample_abs && ws && out && ns >= 1 && ks >= 1 && ks <= ns && ns < ((int64_t)1 << 32),
+                "grace_dgc_sample_kth: bad arguments");
+  hipStream_t s = as_stream(stream);
+  KthState* st = reinterpret_cast<KthState*>(ws);
+  const int64_t nb = (ns + kKthPer * kKthBlock - 1) / (kKthPer * kKthBlock);
+  const unsigned grid = (unsigned)(nb < 1024 ? nb : 1024);
+  dgc_kth_kernel<0><<<grid, kKthBlock, 0, s>>>(sample_abs, ns, (uint32_t)ks, st, out);
+  GRACE_CHECK_LAUNCH("grace_dgc_sample_kth");
+  dgc_kth_kernel<1><<<grid, kKthBlock, 0, s>>>(sample_abs, ns, (uint32_t)ks, st, out);
+  GRACE_CHECK_LAUNCH("grace_dgc_sample_kth");
+  dgc_kth_kernel<2><<<grid, kKthBlock, 0, s>>>(sample_abs, ns, (uint32_t)ks, st, out);
+  GRACE_CHECK_LAUNCH("grace_dgc_sample_kth");
+  return GRACE_OK;
+}
+
 size_t grace_dgc_step_w1_fused_workspace_bytes(int64_t n) {
   return dgc_ws_bytes(n < 1 ? 1 : n) + 256 + sizeof(uint32_t) * (size_t)((n + kDChunkW1 - 1) / kDChunkW1);
 }
@@ -850,6 +980,9 @@ grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, co
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
   // gated fix-up (returns at once unless thr0 did not stand): the reference's full adjustment loop,
   // on grids small enough that the no-op launches cost little
+#ifdef GRACE_DGC_NO_FIXUP   // diagnostic A/B build only: what the five no-op launches cost (wrong when a fix is due)
+  return GRACE_OK;
+#endif
   dgc_table_kernel<true><<<1, 1024, 0, s>>>(top_vals, ks, w);   // the adjustment table, zeroed counts
   GRACE_CHECK_LAUNCH("grace_dgc_step_w1_fused");
   const unsigned sg = stream_grid((n + 3) / 4, kDBlock * kDQ, 1024);

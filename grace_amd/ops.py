@@ -6,6 +6,7 @@ allocates outputs and launches on ``torch.cuda.current_stream()``.
 """
 import functools
 import math
+import os
 
 import torch
 
@@ -1085,6 +1086,33 @@ def status_take(st):
 
 
 # ----------------------------------------------------------------------------- DGC
+# the sampled threshold thr0 = torch.topk(sample, ks)[0].min() (dgc.py:20-21) by the three-digit
+# radix select (grace_dgc_sample_kth) instead of the sample's full top-k; GRACE_DGC_SAMPLE_KTH=0
+# takes the top-k engine's values instead (A/B; the thresholds are identical)
+DGC_SAMPLE_KTH = os.environ.get("GRACE_DGC_SAMPLE_KTH", "1") != "0"
+
+
+def dgc_sample_kth(sample, ks):
+    """(1,) f32: the ks-th largest sampled magnitude, NaN if any sample is NaN -- what
+    torch.topk(sample, ks)[0].min() gives (grace_dgc_sample_kth)."""
+    sample = dev_f32(sample)
+    ns = sample.numel()
+    if not 1 <= ks <= ns:
+        raise ValueError(f"dgc_sample_kth: ks={ks} outside [1, {ns}]")
+    out = torch.empty(1, dtype=F32, device=sample.device)
+    ws = workspace("dgc_kth", _lib.query("grace_dgc_sample_kth_workspace_bytes"), sample.device)
+    _lib.call("grace_dgc_sample_kth", _p(sample), ns, int(ks), _p(ws), _p(out), _stream())
+    return out
+
+
+def _dgc_sample_top(sample, ks):
+    """(top values, their count) whose minimum is thr0: the k-th value alone, or the top-k's values"""
+    if DGC_SAMPLE_KTH:
+        return dgc_sample_kth(sample, ks), 1
+    _, top, _ = topk_compress(sample, ks)
+    return top, ks
+
+
 def dgc_compress(t, ratio, sample_idx=None, seed=0):
     """DgcCompressor.compress (dgc.py:12-43) of flat t: (values f32, indices int64, meta) where
     meta (16 B, device) holds the final threshold for dgc_mask_update.  sample_idx: int64 device
@@ -1095,9 +1123,9 @@ def dgc_compress(t, ratio, sample_idx=None, seed=0):
     ks = max(1, int(n * ratio * 0.01))
     sample = torch.empty(ns, dtype=F32, device=t.device)
     _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
-    _, top, _ = topk_compress(sample, min(ks, ns))
+    top, kt = _dgc_sample_top(sample, min(ks, ns))
     ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
-    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), kt, float(ratio), _p(ws), _stream())
     meta = ws[:16].clone()
     count = int(meta[8:12].view(torch.int32).item())          # host sync: the payload size
     vals = torch.empty(count, dtype=F32, device=t.device)
@@ -1117,9 +1145,9 @@ def dgc_threshold_dev(t, ratio, sample_idx=None, seed=0):
     ks = max(1, int(n * ratio * 0.01))
     sample = torch.empty(ns, dtype=F32, device=t.device)
     _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
-    _, top, _ = topk_compress(sample, min(ks, ns))
+    top, kt = _dgc_sample_top(sample, min(ks, ns))
     ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
-    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    _lib.call("grace_dgc_threshold", _p(t), n, _p(top), kt, float(ratio), _p(ws), _stream())
     return ws
 
 
@@ -1144,9 +1172,9 @@ def dgc_select(t, ratio, sample_idx=None, seed=0):
     ks = max(1, int(n * ratio * 0.01))
     sample = torch.empty(ns, dtype=F32, device=t.device)
     _lib.call("grace_dgc_sample", _p(t), n, _opt(sample_idx), int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
-    _, top, _ = topk_compress(sample, min(ks, ns))
+    top, kt = _dgc_sample_top(sample, min(ks, ns))
     ws = workspace("dgc", _lib.query("grace_dgc_workspace_bytes", n), t.device)
-    _lib.call("grace_dgc_select", _p(t), n, _p(top), min(ks, ns), float(ratio), _p(ws), _stream())
+    _lib.call("grace_dgc_select", _p(t), n, _p(top), kt, float(ratio), _p(ws), _stream())
     return ws
 
 
@@ -1169,11 +1197,11 @@ def dgc_step_w1_fused(g, residual, accum, has_state, momentum, ratio, sample_idx
     _lib.call("grace_dgc_sample_comp", _p(g), _p(residual) if has_state else None,
               _p(accum) if has_state else None, 1 if has_state else 0, float(momentum), n, _opt(sample_idx),
               int(seed) & (2 ** 64 - 1), ns, _p(sample), _stream())
-    _, top, _ = topk_compress(sample, min(ks, ns))
+    top, kt = _dgc_sample_top(sample, min(ks, ns))
     ws = workspace("dgc_w1", _lib.query("grace_dgc_step_w1_fused_workspace_bytes", n), g.device)
     r_new, a_new, out = torch.empty_like(g), torch.empty_like(g), torch.empty_like(g)
     _lib.call("grace_dgc_step_w1_fused", _p(g), _p(residual) if has_state else None,
-              _p(accum) if has_state else None, 1 if has_state else 0, float(momentum), n, _p(top), min(ks, ns),
+              _p(accum) if has_state else None, 1 if has_state else 0, float(momentum), n, _p(top), kt,
               float(ratio), _p(ws), _p(r_new), _p(a_new), _p(out), _stream())
     return out, r_new, a_new
 

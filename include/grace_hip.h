@@ -532,8 +532,8 @@ grace_status_t grace_shard_clear(float* out, int64_t out_base, int64_t out_len, 
 
 /* ---- DGC (grace_dl/dist/compressor/dgc.py:12-50, memory/dgc.py:15-39) -------------------------
  * compress: grace_dgc_sample (|t| at the sampled indices: sample_idx from the caller = torch's
- * CPU uniform_(0, numel).long() stream, or NULL = device generator) -> the k_s largest of the
- * sample (grace_topk_compress) -> grace_dgc_threshold (sampled threshold, the 10-step adjustment
+ * CPU uniform_(0, numel).long() stream, or NULL = device generator) -> thr0, the k_s-th largest of the
+ * sample (grace_dgc_sample_kth; or the k_s largest by grace_topk_compress) -> grace_dgc_threshold (sampled threshold, the 10-step adjustment
  * replayed on exact counts, ordered-compaction offsets; the selected count is at ws + 8, u32)
  * -> grace_dgc_write (values f32, indices int64, ascending).  The final threshold's bits are at
  * ws + 4 (u32); grace_dgc_mask_update reads them from the first 16 bytes of `meta`. */
@@ -580,6 +580,14 @@ grace_status_t grace_dgc_step_w1(const float* t, float* residual, float* accum, 
 grace_status_t grace_dgc_sample_comp(const float* g, const float* residual, const float* accum, int32_t has_state,
                                      float momentum, int64_t n, const int64_t* sample_idx, uint64_t seed, int64_t ns,
                                      float* sample_abs, void* stream);
+/* out[0] = the ks-th largest of sample_abs[0..ns) (magnitudes: the sign bit is ignored), NaN when
+ * any sample is NaN: torch.topk(samples, ks)[0].min() of dgc.py:20-21 without the full top-k, to
+ * pass to grace_dgc_threshold / _select / _step_w1_fused as top_vals with ks = 1.
+ * 1 <= ks <= ns < 2^32.  ws: grace_dgc_sample_kth_workspace_bytes, zeroed once at allocation (left
+ * zeroed by every call). */
+size_t grace_dgc_sample_kth_workspace_bytes(void);
+grace_status_t grace_dgc_sample_kth(const float* sample_abs, int64_t ns, int64_t ks, void* ws, float* out,
+                                    void* stream);
 size_t grace_dgc_step_w1_fused_workspace_bytes(int64_t n);
 grace_status_t grace_dgc_step_w1_fused(const float* g, const float* residual, const float* accum, int32_t has_state,
                                        float momentum, int64_t n, const float* top_vals, int64_t ks, double ratio,

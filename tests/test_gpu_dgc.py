@@ -173,3 +173,55 @@ def test_dgc_w1_speculative_pass_equals_multipass(case):
         assert same_bits(_np(out), _np(eo)), (case, s)
         assert same_bits(_np(r_new), _np(er)) and same_bits(_np(a_new), _np(ea)), (case, s)
         r, a = r_new, a_new
+
+
+@pytest.mark.parametrize("case", ["normal", "ties", "zeros", "inf", "nan", "tiny", "ks1", "ksall", "denorm"])
+def test_dgc_sample_kth_equals_topk_min(case):
+    """grace_dgc_sample_kth = torch.topk(sample, ks)[0].min() (dgc.py:20-21), bit for bit, NaN
+    included: the radix select every DGC path takes its sampled threshold from."""
+    gen = torch.Generator().manual_seed(11)
+    ns, ks = 671088, 6710
+    x = torch.randn(ns, generator=gen).abs()
+    if case == "ties":
+        x = torch.randint(0, 7, (ns,), generator=gen).float()
+    elif case == "zeros":
+        x = torch.zeros(ns)
+    elif case == "inf":
+        x[torch.randint(0, ns, (9000,), generator=gen)] = float("inf")
+    elif case == "nan":
+        x[12345] = float("nan")
+    elif case == "tiny":
+        ns, ks = 3, 2
+        x = torch.tensor([0.5, 2.0, 1.0])
+    elif case == "ks1":
+        ks = 1
+    elif case == "ksall":
+        ns = 5000
+        x, ks = x[:ns], 5000
+    elif case == "denorm":
+        x = (torch.rand(ns, generator=gen) * 1e-39).abs()
+    xd = _t(x.numpy())
+    for _ in range(2):   # the state is left zeroed: a second call gives the same answer
+        got = _np(ops.dgc_sample_kth(xd, ks))
+        want = torch.topk(x, ks)[0].min().reshape(1).numpy()
+        if np.isnan(want[0]):
+            assert np.isnan(got[0])
+        else:
+            assert same_bits(got, want), (case, got, want)
+
+
+def test_dgc_thresholds_same_with_either_sample_select():
+    """The three-digit select and the top-k engine's values give DGC the same threshold and payload
+    (ops.DGC_SAMPLE_KTH switched in one process)."""
+    gen = torch.Generator().manual_seed(5)
+    t = _t((torch.randn(1 << 22, generator=gen) * 0.01).numpy())
+    res = []
+    for kth in (True, False):
+        ops.DGC_SAMPLE_KTH = kth
+        try:
+            vals, idx, meta = ops.dgc_compress(t, 0.01, seed=3)
+        finally:
+            ops.DGC_SAMPLE_KTH = True
+        res.append((_np(vals), _np(idx), _np(meta.view(torch.int32))))
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
