@@ -4,7 +4,7 @@
 // The W payloads of a step land on every rank; decoding them with one random scatter per rank
 // read-modify-writes the 256 MiB output W times (~55 us per rank on MI355X).  Instead each rank
 // groups its own payload by 8192-element output chunk before the exchange (a counting sort by
-// chunk: LDS histograms, one scan, LDS-ranked scatter -- a full radix sort of the indices is not
+// chunk: LDS histograms, a scan of the counts, LDS-ranked scatter -- a full radix sort of the indices is not
 // needed and costs ~10x more), and the decode is one pass over the OUTPUT: a workgroup per chunk
 // finds every rank's sub-range of that chunk from a boundary table, accumulates the ranks in
 // order in LDS -- ((0 + d0) + d1) + ... exactly as Python's sum -- divides, and writes the chunk
@@ -40,17 +40,15 @@ constexpr int kGroupBlock = GRACE_GROUP_BLOCK;
 constexpr int kGroupPer = GRACE_GROUP_PER;             // entries per thread
 constexpr int kMaxGroupChunks = 32768;                 // LDS histogram bins (128 KB): n <= 2^28
 
-// pass 1: per-workgroup LDS histogram of chunk ids, flushed with one atomic per non-zero bin; the
-// last workgroup to finish (ticket; agent-scope atomics, no L2 fences) scans the counts in place
-// (the counts live in the caller's zeroed workspace; pass 2 leaves them zeroed again)
-__device__ void scan_counts_block(uint32_t* counts, int64_t nchunks);
-
+// pass 1: per-workgroup LDS histogram of chunk ids, flushed with one device atomic per non-zero bin
+// into the chunk counts (the caller's zeroed workspace) -- and nothing after it: no ticket, no scan.
+// pass 2 finds every chunk's start itself (each workgroup scans the counts, a kernel boundary
+// later), so the histogram pass ends as soon as its adds are issued.  (r05: the last arriver's scan
+// here was a ~4 us tail of vmcnt(0), ticket and one workgroup's scan on the grouping's chain.)
 template <typename IdxT>
 __global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const IdxT* __restrict__ idx, int64_t k,
-                                                                int64_t nchunks, uint32_t* __restrict__ counts,
-                                                                uint32_t* __restrict__ ticket) {
+                                                                int64_t nchunks, uint32_t* __restrict__ counts) {
   extern __shared__ uint32_t h[];
-  __shared__ uint32_t s_last;
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kGroupBlock * kGroupPer;
@@ -62,22 +60,15 @@ __global__ __launch_bounds__(kGroupBlock) void group_hist_kernel(const IdxT* __r
   __syncthreads();
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock)
     if (h[c]) atomicAdd(&counts[c], h[c]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (s_last) scan_counts_block(counts, nchunks);
 }
 
-// exclusive scan of the chunk counts in place by one workgroup (kScanPer counts per thread per
-// round); the counts were produced by device-scope atomics, so they are read with agent loads
+// exclusive scan of the chunk counts by one workgroup, kScanPer counts per thread per round: f(c,
+// exclusive start of chunk c, count of c) for every chunk; the counts come from device atomics of an
+// earlier launch, read with agent loads
 constexpr int kScanPer = 8;
-__device__ void scan_counts_block(uint32_t* counts, int64_t nchunks) {
+template <typename F>
+__device__ __forceinline__ void scan_counts(const uint32_t* counts, int64_t nchunks, uint32_t* s_w, F f) {
   constexpr int NT = kGroupBlock;
-  __shared__ uint32_t s_w[NT / kWave + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t run = 0;
   for (int64_t c0 = 0; c0 < nchunks; c0 += NT * kScanPer) {
@@ -105,7 +96,7 @@ __device__ void scan_counts_block(uint32_t* counts, int64_t nchunks) {
     uint32_t ex = run + s_w[w] + inc - sum;
 #pragma unroll
     for (int e = 0; e < kScanPer; ++e) {
-      if (cb + e < nchunks) counts[cb + e] = ex;
+      if (cb + e < nchunks) f(cb + e, ex, v[e]);
       ex += v[e];
     }
     run += s_w[NT / kWave];
@@ -113,34 +104,48 @@ __device__ void scan_counts_block(uint32_t* counts, int64_t nchunks) {
   }
 }
 
-// pass 2: each workgroup reserves its range of every chunk it touches (one atomic per non-zero
-// bin), ranks its entries within a bin with LDS atomics, and writes them grouped by chunk
+// pass 2: each workgroup reserves its range of every chunk it touches (one returning atomic per
+// non-zero bin on the chunk's cursor), adds the chunk starts from its own scan of the counts, ranks
+// its entries within a bin with LDS atomics, and writes them grouped by chunk.  Workgroup 0 writes
+// the chunk end offsets (the inclusive scan); the last workgroup to finish re-zeroes the counts and
+// cursors for the next grouping (the scratch lives in the caller's workspace, so no memset launch
+// precedes the histogram pass).
 template <typename IdxT>
 __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float* __restrict__ vals,
                                                                    const IdxT* __restrict__ idx, int64_t k,
-                                                                   int64_t nchunks, uint32_t* __restrict__ cursor,
+                                                                   int64_t nchunks, uint32_t* __restrict__ counts,
+                                                                   uint32_t* __restrict__ cursor,
                                                                    float* __restrict__ vals_out,
                                                                    uint16_t* __restrict__ off_out,
                                                                    uint32_t* __restrict__ ends_out,
                                                                    uint32_t* __restrict__ ticket) {
   extern __shared__ uint32_t h[];
-  for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
-  __syncthreads();
+  __shared__ uint32_t s_w[kGroupBlock / kWave + 1];
+  __shared__ uint32_t s_last;
   const int64_t base = (int64_t)blockIdx.x * kGroupBlock * kGroupPer;
   int32_t ii[kGroupPer];
   float vv[kGroupPer];
 #pragma unroll
-  for (int e = 0; e < kGroupPer; ++e) {
+  for (int e = 0; e < kGroupPer; ++e) {   // the entries' loads first: their latency overlaps the scan's
     const int64_t j = base + (int64_t)e * kGroupBlock + threadIdx.x;
     ii[e] = j < k ? (int32_t)idx[j] : -1;
     vv[e] = j < k && vals ? vals[j] : 0.f;
   }
+  for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) h[c] = 0u;
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < kGroupPer; ++e)
     if (ii[e] >= 0) atomicAdd(&h[ii[e] >> kPChunkLog], 1u);
   __syncthreads();
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock)
-    if (h[c]) h[c] = atomicAdd(&cursor[c], h[c]);     // this workgroup's first slot in chunk c
+    if (h[c]) h[c] = atomicAdd(&cursor[c], h[c]);     // this workgroup's first slot inside chunk c
+  __syncthreads();
+  // + the chunk's start: every bin a thread owns in the scan is its own to update
+  const bool w0 = blockIdx.x == 0;
+  scan_counts(counts, nchunks, s_w, [&](int64_t c, uint32_t start, uint32_t cnt) {
+    h[c] += start;
+    if (w0) ends_out[c] = start + cnt;
+  });
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kGroupPer; ++e) {
@@ -149,12 +154,10 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
     if (vals_out) vals_out[pos] = vv[e];
     off_out[pos] = (uint16_t)(ii[e] & (kPChunk - 1));   // the offset inside its chunk (13 bits)
   }
-  // the cursors (device atomics) now hold every chunk's end: the last workgroup to arrive copies
-  // them into the payload's end table and re-zeroes them for the next grouping (the scratch lives
-  // in the caller's workspace, so no memset launch precedes the histogram pass)
+  // every workgroup's cursor atomics and count reads are done once it arrives: the last one re-zeroes
+  // them for the next grouping
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
     s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(kGroupBlock) void group_scatter_kernel(const float*
   __syncthreads();
   if (!s_last) return;
   for (int64_t c = threadIdx.x; c < nchunks; c += kGroupBlock) {
-    ends_out[c] = __hip_atomic_load(cursor + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(counts + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(cursor + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -261,20 +264,21 @@ __global__ __launch_bounds__(kPBlock) void chunk_accumulate_kernel(const float* 
 
 // group entries by 8192-element chunk (u16 offsets, chunk end offsets); vals optional.  Shared by
 // grace_sort_payload and the world-1 random-k step (sparse.hip).
-// scratch: [2 tickets | 248 B | counts u32[kMaxGroupChunks]] (group_scratch_bytes), zeroed once and left
-// zeroed: counts -> exclusive offsets (hist pass) -> chunk ends (scatter cursors) -> ends_out
+// scratch: [ticket | 252 B | counts u32[kMaxGroupChunks] | cursors u32[kMaxGroupChunks]]
+// (group_scratch_bytes), zeroed once and left zeroed by every call
 template <typename IdxT>
 hipError_t group_by_chunk(const float* vals, const IdxT* idx, int64_t k, int64_t nchunks, float* vals_out,
                           uint16_t* off_out, uint32_t* ends_out, uint32_t* scratch, hipStream_t s) {
   if (k == 0) return hipMemsetAsync(ends_out, 0, sizeof(uint32_t) * nchunks, s);
   uint32_t* counts = scratch + 64;
+  uint32_t* cursor = counts + kMaxGroupChunks;
   const unsigned nb = (unsigned)((k + (int64_t)kGroupBlock * kGroupPer - 1) / ((int64_t)kGroupBlock * kGroupPer));
   const size_t lds = sizeof(uint32_t) * (size_t)nchunks;
-  group_hist_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts, scratch);
+  group_hist_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(idx, k, nchunks, counts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  group_scatter_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, vals_out, off_out, ends_out,
-                                                          scratch + 1);
+  group_scatter_kernel<IdxT><<<nb, kGroupBlock, lds, s>>>(vals, idx, k, nchunks, counts, cursor, vals_out, off_out,
+                                                          ends_out, scratch);
   return hipGetLastError();
 }
 template hipError_t group_by_chunk<int64_t>(const float*, const int64_t*, int64_t, int64_t, float*, uint16_t*,
@@ -283,7 +287,7 @@ template hipError_t group_by_chunk<int64_t>(const float*, const int64_t*, int64_
 // a larger call's counts land on a smaller call's data (the counts must stay zeroed)
 size_t group_scratch_bytes(int64_t nchunks) {
   (void)nchunks;
-  return 256 + sizeof(uint32_t) * (size_t)kMaxGroupChunks;
+  return 256 + 2 * sizeof(uint32_t) * (size_t)kMaxGroupChunks;
 }
 
 }  // namespace grace
@@ -294,7 +298,7 @@ extern "C" {
 
 size_t grace_sort_payload_workspace_bytes(int64_t k, int64_t n) {
   (void)k;
-  return group_scratch_bytes((n + kPChunk - 1) / kPChunk);   // tickets + chunk counts, left zeroed by every call
+  return group_scratch_bytes((n + kPChunk - 1) / kPChunk);   // ticket, chunk counts and cursors, left zeroed
 }
 
 // groups the payload by 8192-element output chunk (chunk-ascending; order within a chunk is
