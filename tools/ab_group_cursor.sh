@@ -1,7 +1,8 @@
 #!/bin/bash
 # Diagnostic: the grouping's scatter with its reservation atomics spread over 4 cursor copies
 # (libgrace_hip_curcopies.so: WRONG positions, timing only) vs the shipped one -- how much of the
-# scatter is the same-address chain of 164 workgroups' returning adds per chunk cursor.
+# scatter is the same-address chain of 164 workgroups' returning adds per chunk cursor.  (The build knob
+# GRACE_DIAG_CURSOR_COPIES was removed after this A/B: no gain, profiles/r05_group2_ab.txt.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out/r05
 : > gpurun_out/r05/ab_group_cursor.txt
