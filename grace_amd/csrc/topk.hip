@@ -159,6 +159,15 @@ constexpr int kBracketBins = 32768;                        // key >> 16: 1/64-oc
 #endif
 constexpr int kBracketRun = GRACE_SAMPLE_RUN;              // adjacent elements per sampling thread
 constexpr int kCoarseBins = 2048;                          // key >> 20: 1/8-octave bins
+// A/B knob: the bracket's search in every main-pass workgroup instead of the bracket's last sampler.
+// Measured slower (r05, tools/ab_main_search.sh, profiles/r05_main_search_ab.txt): headline step
+// 0.2330-0.2373 vs 0.2294-0.2314 ms, topk_main 204-209 vs 198-200 us -- 5462 workgroups x 2096
+// agent-scope histogram loads (46 MB at the memory side) and a search latency at every
+// workgroup's start cost more than the bracket's tail they remove.
+#ifndef GRACE_MAIN_SEARCH
+#define GRACE_MAIN_SEARCH 0
+#endif
+constexpr bool kMainSearch = GRACE_MAIN_SEARCH != 0;       // the bracket's search in the main pass
 constexpr int kHistStride = 1;
 
 // Workspace layout.  Every counter / histogram region is left zeroed by the step that used it
@@ -412,8 +421,9 @@ __device__ __forceinline__ uint32_t cand_bin(uint32_t key, uint32_t lo, uint32_t
 // the bracket from the fine bins (key >> 16) holding the three ranks: sure = key > hi (rounded up
 // to the top of its bin: fewer sure), candidates from the bottom of the low bin (more candidates),
 // the provisional threshold in the middle of its bin, clamped into the band
-__device__ __forceinline__ void bracket_publish(TopkCtl* ctl, const BracketRanks& b, int64_t S, uint32_t d_hi,
-                                                uint32_t d_lo, uint32_t d_mid) {
+struct BracketThr { uint32_t lo, hi, sh, mid; };
+__device__ __forceinline__ BracketThr bracket_thresholds(const BracketRanks& b, int64_t S, uint32_t d_hi,
+                                                        uint32_t d_lo, uint32_t d_mid) {
   uint32_t hi = (d_hi << 16) | 0xFFFFu;
   // top of the binned key range: hi, or with nothing sure the top of the sample maximum's bin
   // (r1[0] = 1 then); the keys above it share the top bin (binning clamps), so the 2048 bins
@@ -429,10 +439,74 @@ __device__ __forceinline__ void bracket_publish(TopkCtl* ctl, const BracketRanks
   while ((span >> sh) >= (uint64_t)kHistBins) ++sh;
   uint32_t mid = (d_mid << 16) | 0x8000u;
   mid = mid < lo ? lo : (mid > hi ? hi : mid);
-  ctl->thr_lo = lo;
-  ctl->thr_hi = hi;
-  ctl->shift = sh;
-  ctl->thr_mid = mid;
+  return BracketThr{lo, hi, sh, mid};
+}
+__device__ __forceinline__ void bracket_publish(TopkCtl* ctl, const BracketThr& t) {
+  ctl->thr_lo = t.lo;
+  ctl->thr_hi = t.hi;
+  ctl->shift = t.sh;
+  ctl->thr_mid = t.mid;
+}
+
+// The bracket's search, by one workgroup of NT threads once the sample histograms are complete:
+// thread t owns kCPT consecutive coarse bins from the top down, one block scan finds the coarse bins
+// of the three bracketing ranks, then one 16-lane group per rank scans that coarse bin's 16 fine
+// bins (descending) for the first lane whose running count reaches the rank.  Every thread returns
+// the same thresholds.  The histograms were filled by device atomics: agent-scope loads.
+template <int NT>
+__device__ __forceinline__ BracketThr bracket_search(const StepArgs& a, const TopkWs& w, uint32_t* s_w,
+                                                     uint32_t* s_fc, uint32_t* s_res) {
+  const int tid = threadIdx.x;
+  const int64_t S = a.sample_n;
+  const BracketRanks br = bracket_ranks(S, a.k, a.n);
+  const uint32_t(&r1)[3] = br.r1;
+  const uint32_t rk0 = br.r1[0], rk1 = br.r1[1], rk2 = br.r1[2];
+  constexpr int kCPT = kCoarseBins / NT;
+  static_assert(kCPT * NT == kCoarseBins && kCPT >= 1 && NT >= 64, "coarse bins tile the block");
+  const int top = kCoarseBins - 1 - kCPT * tid;
+  uint32_t hc[kCPT], hs = 0;
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    hc[c] = __hip_atomic_load(w.chist + top - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hs += hc[c];
+  }
+  if (tid < 6) s_fc[tid] = 0;
+  const uint32_t ex = block_excl_scan<NT>(hs, s_w, nullptr);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (ex < r1[q] && r1[q] <= ex + hs) {
+      uint32_t acc = ex;
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        if (r1[q] <= acc + hc[c]) {
+          s_fc[2 * q] = (uint32_t)(top - c);
+          s_fc[2 * q + 1] = acc;
+          break;
+        }
+        acc += hc[c];
+      }
+    }
+  __syncthreads();
+  if (tid < 64) {
+    const int q = tid >> 4, j = tid & 15;
+    const bool act = q < 3;
+    const uint32_t bin = act ? s_fc[2 * q] * 16 + (15 - j) : 0u;
+    uint32_t v = act ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const uint32_t u = __shfl_up(v, o, 16);
+      if (j >= o) v += u;
+    }
+    const int qc = act ? q : 0;
+    // (selects of SSA values: a dynamic index, or selects of r1's elements that the compiler folds
+    // back into one, keep r1 in scratch memory)
+    const uint32_t rq = qc == 0 ? rk0 : (qc == 1 ? rk1 : rk2);
+    const uint64_t bal = __ballot(act && s_fc[2 * qc + 1] + v >= rq);
+    const uint32_t hm = (uint32_t)(bal >> (16 * q)) & 0xFFFFu;
+    if (act && j == __ffs(hm) - 1) s_res[q] = bin;
+  }
+  __syncthreads();
+  return bracket_thresholds(br, S, s_res[0], s_res[1], s_res[2]);
 }
 
 // Single-GPU bracket: sample + select in ONE launch.  The sample workgroups count their keys into
@@ -539,6 +613,10 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   for (int b = tid; b < kCoarseBins; b += kBracketBlock)
     if (lc[b]) atomicAdd(&w.chist[b], lc[b]);
   STAMP(w.ctl, 2);
+  // kMainSearch: no last arriver here -- every main-pass workgroup runs the search itself, a kernel
+  // boundary later (the tail of waiting for the last sampler and one workgroup's search leaves the
+  // chain, as the payload grouping's histogram pass did)
+  if constexpr (kMainSearch) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) s_last = atomicAdd(&w.ctl->bticket, 1u) == nsamp - 1;
@@ -546,63 +624,11 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
   if (!s_last) return;
   STAMP_IF(true, w.ctl, 3);
   // sample ranks bracketing the k-th largest with ~6 sigma, and the sample's k-th estimate
-  const int64_t S = a.sample_n;
-  const BracketRanks br = bracket_ranks(S, a.k, a.n);
-  const uint32_t(&r1)[3] = br.r1;
-  const uint32_t rk0 = br.r1[0], rk1 = br.r1[1], rk2 = br.r1[2];
-  // coarse: thread t owns kCPT consecutive bins from top down (descending); one block scan finds
-  // the three coarse bins
-  constexpr int kCPT = kCoarseBins / kBracketBlock;
-  static_assert(kCPT * kBracketBlock == kCoarseBins && kCPT >= 1, "coarse bins tile the block");
-  const int top = kCoarseBins - 1 - kCPT * tid;
-  uint32_t hc[kCPT], hs = 0;
-#pragma unroll
-  for (int c = 0; c < kCPT; ++c) {
-    hc[c] = __hip_atomic_load(w.chist + top - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hs += hc[c];
-  }
-  if (tid < 6) s_fc[tid] = 0;
-  const uint32_t ex = block_excl_scan<kBracketBlock>(hs, s_w, nullptr);
-#pragma unroll
-  for (int q = 0; q < 3; ++q)
-    if (ex < r1[q] && r1[q] <= ex + hs) {
-      uint32_t acc = ex;
-#pragma unroll
-      for (int c = 0; c < kCPT; ++c) {
-        if (r1[q] <= acc + hc[c]) {
-          s_fc[2 * q] = (uint32_t)(top - c);
-          s_fc[2 * q + 1] = acc;
-          break;
-        }
-        acc += hc[c];
-      }
-    }
-  __syncthreads();
-  // fine: one 16-lane group per target rank, inclusive scan of the coarse bin's 16 fine bins
-  // (descending) and the first lane whose running count reaches the rank
-  if (tid < 64) {
-    const int q = tid >> 4, j = tid & 15;
-    const bool act = q < 3;
-    const uint32_t bin = act ? s_fc[2 * q] * 16 + (15 - j) : 0u;
-    uint32_t v = act ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const uint32_t u = __shfl_up(v, o, 16);
-      if (j >= o) v += u;
-    }
-    const int qc = act ? q : 0;
-    // (selects of SSA values: a dynamic index, or selects of r1's elements that the compiler folds
-    // back into one, keep r1 in scratch memory)
-    const uint32_t rq = qc == 0 ? rk0 : (qc == 1 ? rk1 : rk2);
-    const uint64_t bal = __ballot(act && s_fc[2 * qc + 1] + v >= rq);
-    const uint32_t hm = (uint32_t)(bal >> (16 * q)) & 0xFFFFu;
-    if (act && j == __ffs(hm) - 1) s_res[q] = bin;
-  }
-  __syncthreads();
+  const BracketThr thr = bracket_search<kBracketBlock>(a, w, s_w, s_fc, s_res);
   STAMP_IF(true, w.ctl, 4);
   if (tid == 0) {
     // the fused main pass writes candidates above the provisional threshold as selected
-    bracket_publish(w.ctl, br, S, s_res[0], s_res[1], s_res[2]);
+    bracket_publish(w.ctl, thr);
     w.ctl->bticket = 0u;
   }
   STAMP_IF(true, w.ctl, 5);
@@ -939,7 +965,15 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
   if constexpr (!SKEL) {
     for (int b = tid; b < kHistBins; b += kMainBlock) sm.hist[b] = 0;
   }
-  const uint32_t lo = w.ctl->thr_lo, hi = w.ctl->thr_hi, sh = w.ctl->shift, mid = w.ctl->thr_mid;
+  uint32_t lo, hi, sh, mid;
+  if constexpr (kMainSearch && !SKEL) {
+    __shared__ uint32_t s_w[kMainBlock / kWave + 1], s_fc[6], s_res[3];
+    const BracketThr t = bracket_search<kMainBlock>(a, w, s_w, s_fc, s_res);
+    lo = t.lo; hi = t.hi; sh = t.sh; mid = t.mid;
+    if (blockIdx.x == 0 && tid == 0) bracket_publish(w.ctl, t);   // for the finalize (next launch)
+  } else {
+    lo = w.ctl->thr_lo; hi = w.ctl->thr_hi; sh = w.ctl->shift; mid = w.ctl->thr_mid;
+  }
   constexpr int64_t kCh = (int64_t)kMainBlock * 4 * NV;
   const int64_t nchunks = (a.n + kCh - 1) / kCh;
   const bool unit = HAS_RES && a.beta == 1.f && a.gamma == 1.f;
@@ -2005,7 +2039,7 @@ __global__ __launch_bounds__(kSelBlock) void seg_prep_kernel(SegPlan p) {
   int d[3];
   uint32_t above[3];
   find_bins_desc<kSelBlock, kBracketBins, 3, true>(lds, br.r1, s_w, s_res, d, above);
-  if (tid == 0) bracket_publish(w.ctl, br, S, (uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2]);
+  if (tid == 0) bracket_publish(w.ctl, bracket_thresholds(br, S, (uint32_t)d[0], (uint32_t)d[1], (uint32_t)d[2]));
   STAMP_IF(true, w.ctl, 15);
 }
 
