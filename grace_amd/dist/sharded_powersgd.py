@@ -102,10 +102,9 @@ class ShardedPowerSGD:
             send[:hi - lo].copy_(Pi)
             gathered = torch.empty(world * per, r, dtype=torch.float32, device=dev)
             dist.all_gather_into_tensor(gathered, send, group=self.group)
-            P = torch.empty(int(n_rows), r, dtype=torch.float32, device=dev)
-            for w, (a, b) in enumerate(self.partition(int(n_rows), world)):
-                if b > a:
-                    P[a:b].copy_(gathered[w * per:w * per + (b - a)])
+            # the padded row blocks back to one P: one batched copy
+            P = torch.cat([gathered[w * per:w * per + (b - a)]
+                           for w, (a, b) in enumerate(self.partition(int(n_rows), world)) if b > a])
         else:
             P = Pi.contiguous()
         K.orthogonalize_(P)

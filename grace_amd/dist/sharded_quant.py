@@ -191,17 +191,12 @@ class ShardedQuant:
         gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=x.device)
         dist.all_gather_into_tensor(gathered, rec, group=self.group)
         g = gathered.view(world, -1)
-        full = torch.empty(plan.n * csz, dtype=torch.uint8, device=x.device)
-        for w, (a, b) in enumerate(plan.ranges):   # the padded records, back to one flat code buffer
-            if b > a:
-                full[a * csz:b * csz].copy_(g[w, :(b - a) * csz])
-        full = full.view(codes.dtype)
+        # the padded records back to one flat code buffer (and one norm buffer): one batched copy each
+        full = torch.cat([g[w, :(b - a) * csz] for w, (a, b) in enumerate(plan.ranges) if b > a]).view(codes.dtype)
         allnorms = None
         if self.codec == "qsgd":
-            allnorms = torch.empty(plan.nunits, dtype=torch.float32, device=x.device)
-            for w, (u0, u1) in enumerate(plan.units):
-                if u1 > u0:
-                    allnorms[u0:u1].copy_(g[w, cb:cb + (u1 - u0) * 4].view(torch.float32))
+            allnorms = torch.cat([g[w, cb:cb + (u1 - u0) * 4] for w, (u0, u1) in enumerate(plan.units)
+                                  if u1 > u0]).view(torch.float32)
         return K.decode(self.codec, full, allnorms, list(plan.sizes), plan.n, self.q, self.bucket, self.variant)
 
     def _step_bits(self, x, plan, world, rank, lo, hi):

@@ -186,8 +186,8 @@ class ShardedTernGrad:
             return K.decode(codes, scalars[s0:s1 + 1], own, hi - lo)
         if world == 1:
             return K.decode(codes, scalars, plan.sizes, plan.n)
-        full = torch.empty(plan.n, dtype=torch.int8, device=dev)
         if packed:
+            full = torch.empty(plan.n, dtype=torch.int8, device=dev)
             # every rank's block padded to the longest range's packed size (16-B multiples)
             pb = (K.pack_bytes(plan.max_len) + 15) // 16 * 16
             send = torch.empty(pb, dtype=torch.uint8, device=dev)
@@ -201,7 +201,7 @@ class ShardedTernGrad:
             return K.decode(full, scalars, plan.sizes, plan.n)
         gathered = torch.empty(world * plan.max_len, dtype=torch.int8, device=dev)
         dist.all_gather_into_tensor(gathered, sendc, group=self.group)
-        for w, (a, b) in enumerate(plan.ranges):   # the padded blocks, back to one flat code buffer
-            if b > a:
-                full[a:b].copy_(gathered[w * plan.max_len:w * plan.max_len + (b - a)])
+        # the padded blocks back to one flat code buffer: one batched copy
+        full = torch.cat([gathered[w * plan.max_len:w * plan.max_len + (b - a)]
+                          for w, (a, b) in enumerate(plan.ranges) if b > a])
         return K.decode(full, scalars, plan.sizes, plan.n)
