@@ -234,22 +234,28 @@ def bench_sharded_codec(args, world, rank, dev, codec):
 NO_PROBE = os.environ.get("GRACE_BENCH_NO_PROBE", "0") not in ("", "0")
 
 
-def pmc_traffic(workload, alg_bytes):
-    """HBM bytes per step of a secondary workload's kernels from the committed rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes (tools/prof_r02.sh -> tools/pmc_all.py), with the ratio to the algorithmic
-    bytes; None when that workload was not profiled."""
-    wl = None
-    for tag in ("r05", "r04", "r03", "r02"):   # the newest committed passes that cover the workload
-        try:
-            with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_secondary.json")) as f:
-                wl = json.load(f)["workloads"][workload]
-            break
-        except (OSError, ValueError, KeyError):
-            continue
-    if wl is None:
-        return None, None
+# the round whose PMC passes (tools/r06_session.sh pmc -> profiles/r06_pmc_secondary.json) this
+# tree's lines quote: older passes measured older kernels, and some of them another output mode
+PMC_TAG = "r06"
+
+
+def pmc_traffic(workload, alg_bytes, mode=None):
+    """HBM bytes per step of a secondary workload's kernels from this round's committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_all.py), with the ratio to the algorithmic bytes.  A
+    workload whose step has several output modes (the recycled or dense output of top-k, sharded
+    top-k and random-k) passes the mode that ran, and only a pass recorded in that same mode counts:
+    a pass of another mode moved other bytes (the no-memory line once quoted an r02
+    dense-output pass for the recycled step).  Returns (bytes, ratio, source) or (None, None, None)."""
+    path = os.path.join(ROOT, "profiles", f"{PMC_TAG}_pmc_secondary.json")
+    try:
+        with open(path) as f:
+            wl = json.load(f)["workloads"][workload]
+    except (OSError, ValueError, KeyError):
+        return None, None, None
+    if mode is not None and wl.get("mode") != mode:
+        return None, None, None
     t = wl["hbm_bytes_per_step"]
-    return t, round(t / alg_bytes, 3)
+    return t, round(t / alg_bytes, 3), os.path.relpath(path, ROOT)
 
 
 def gpu_clocks(dev):
@@ -583,10 +589,10 @@ def bench_topk_nomem(args, world, rank, dev):
     main_avg_ms = main_ms / max(launches, 1)
     main_bytes = (4 * n + 4 * k if recycled else 8 * n) if world == 1 else 4 * n
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic("topk_nomem", step_bytes)
+    traffic, ratio, tsrc = pmc_traffic("topk_nomem", step_bytes, mode="recycled" if recycled else "dense")
     line["roofline"] = {"bound": "hbm", "achieved": round(step_bytes / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(step_bytes / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio,
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
                         "step_algorithmic_bytes": step_bytes, "kernel": "topk_main",
                         "kernel_avg_us": round(main_avg_ms * 1e3, 2),
                         "kernel_frac": round(main_bytes / (main_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -712,10 +718,11 @@ def bench_topk_sharded(args, world, rank, dev):
         per_gpu = 12.0 * m + 8.0 * k + 16.0 * world * k + 8.0 * k
     else:
         per_gpu = survey
-    traffic, t_ratio = pmc_traffic("topk_sharded", per_gpu) if world == 1 else (None, None)
+    traffic, t_ratio, tsrc = (pmc_traffic("topk_sharded", per_gpu, mode="recycled" if recycled else "dense")
+                              if world == 1 else (None, None, None))
     line["roofline"] = {"bound": "hbm", "achieved": round(per_gpu / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(per_gpu / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": t_ratio,
+                        "traffic_over_algorithmic": t_ratio, "traffic_source": tsrc,
                         "algorithmic_bytes_per_gpu": per_gpu, "survey_bytes_per_gpu": survey,
                         "output": "recycled" if recycled else "dense zero-fill",
                         "recycled_steps": eng._recycler.hits}
@@ -769,10 +776,10 @@ def bench_ddp(args, world, rank, dev):
         k_sum = sum(min(p.numel(), max(1, int(p.numel() * 0.01))) for p in bucket.params)
     alg = (16 if world == 1 else 12) * total + 8 * k_sum
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic(args.workload, alg) if world == 1 else (None, None)
+    traffic, ratio, tsrc = pmc_traffic(args.workload, alg) if world == 1 else (None, None, None)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio,
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
                         "algorithmic_bytes_per_step": alg, "selected_per_step": k_sum,
                         "note": "16 B per element at world 1 (g, r read; r', dense out written) + 8 B per selected entry"}
     return line
@@ -798,12 +805,20 @@ def bench_sign(args, world, rank, dev):
     line["config"] = {"workload": f"Allgather(SignSGD, NoneMemory).step, {4 * n >> 20} MiB fp32", "numel": n,
                       "rotated_buffers": nbuf}
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic(args.workload, 10.0 * n)
-    line["roofline"] = {"bound": "hbm", "achieved": round(10.0 * n / t / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(10.0 * n / t / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "traffic_over_algorithmic": ratio,
-                        "note": "10n algorithmic bytes per step (SURVEY.md §8d config 1); the world-1 fused step "
-                                "never materialises the u8 codes, so it moves 8n"}
+    # the world-1 fused step never materialises the u8 codes: it reads x and writes the result, 8n.
+    # `frac` follows the bytes moved; SURVEY.md §8d's 10n (the codes written and read back) is kept
+    # beside it as frac_of_survey_bytes (a frac on 10n printed an `achieved` above the
+    # box's measured copy rate)
+    alg = 8.0 * n if world == 1 else 10.0 * n
+    traffic, ratio, tsrc = pmc_traffic(args.workload, alg)
+    line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
+                        "algorithmic_bytes_per_step": alg,
+                        "frac_of_survey_bytes": round(10.0 * n / t / 1e9 / HBM_PEAK_GBS, 4),
+                        "note": ("8n moved per step at world 1 (x read, the f32 result written; the fused step "
+                                 "never stores the u8 codes); frac_of_survey_bytes counts SURVEY.md §8d config 1's "
+                                 "10n" if world == 1 else "10n: the u8 codes written and read back")}
     return line
 
 
@@ -846,10 +861,10 @@ def bench_quant(args, world, rank, dev):
             else "compress+decompress")
     line["config"] = {"workload": f"{args.workload} {what}, 161 ResNet-50 tensors in one segmented "
                                   "launch per stage (BASELINE configs[2])", "numel": total, "tensors": len(sizes)}
-    traffic, ratio = pmc_traffic(args.workload, alg)
+    traffic, ratio, tsrc = pmc_traffic(args.workload, alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg}
     # the encoders' own ceiling: the same read-4-B / write-1-B mix streamed with no arithmetic
     if not NO_PROBE:
         enc_gbs, enc_v = measured_encode_gbs(dev, total)
@@ -881,10 +896,10 @@ def bench_cast(args, world, rank, dev):
                      metric=f"grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 {args.workload}")
     line["config"] = {"workload": f"Allgather({type(comp).__name__}, NoneMemory).step, 256 MiB fp32", "numel": n,
                       "rotated_buffers": nbuf}
-    traffic, ratio = pmc_traffic(args.workload, alg)
+    traffic, ratio, tsrc = pmc_traffic(args.workload, alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg,
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg,
                         "note": "8n at world 1 (fused step: x read once, the f32 result written once); "
                                 f"{8 + 2 * code_bytes}n with the codes materialised (world > 1)"}
     return line
@@ -917,10 +932,15 @@ def bench_sparse(args, world, rank, dev):
     line["config"] = {"workload": f"{desc} on a 256 MiB fp32 bucket (SURVEY.md 8a)", "numel": n}
     alg = 16.0 * n                       # g, r read; r', dense out written (payload bytes excluded)
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic(args.workload, alg)
+    rec = getattr(comp, "_recycler", None)
+    mode = None
+    if args.workload == "randomk":       # random-k's world-1 step recycles its dropped output
+        mode = "recycled" if rec is not None and rec.hits > 0 else "dense"
+        line["config"]["output"] = mode
+    traffic, ratio, tsrc = pmc_traffic(args.workload, alg, mode=mode)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg}
     return line
 
 
@@ -954,10 +974,10 @@ def bench_dgc(args, world, rank, dev):
         note = ("48n: compensate 20n, threshold histogram 4n, compaction 4n, mask update 16n, dense decode 4n "
                 "(the reference's passes, each fused to one kernel)")
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic("dgc", alg)
+    traffic, ratio, tsrc = pmc_traffic("dgc", alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg, "note": note}
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg, "note": note}
     return line
 
 
@@ -984,10 +1004,10 @@ def bench_sign_bits(args, world, rank, dev):
                       "numel": n}
     alg = 4.0 * n + n / 8 + n / 8 * world + 4.0 * n     # read x, write bits; read W bit payloads, write out
     t = elapsed / args.steps
-    traffic, ratio = pmc_traffic("sign_bits", alg)
+    traffic, ratio, tsrc = pmc_traffic("sign_bits", alg)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "algorithmic_bytes_per_step": alg}
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg}
     return line
 
 
@@ -1007,10 +1027,10 @@ def bench_powersgd(args, world, rank, dev):
                      metric="grad-codec GB/s (device-resident encode+decode), PowerSGD rank 4, 4096x4096")
     line["config"] = {"workload": "Allreduce(PowerSGD rank 4, NoneMemory).step, 4096x4096 fp32 (BASELINE configs[3])",
                       "numel": n * m, "rank": r}
-    traffic, ratio = pmc_traffic("powersgd", 12.0 * n * m)
+    traffic, ratio, tsrc = pmc_traffic("powersgd", 12.0 * n * m)
     line["roofline"] = {"bound": "hbm", "achieved": round(12 * n * m / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio,
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
                         "mfma_tflops": round(flops / t / 1e12, 3),
                         "mfma_util": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 5),
                         "note": "12n algorithmic bytes, 6nmr flops (SURVEY.md §8d config 4; AI = 2 flop/B)"}

@@ -183,7 +183,8 @@ struct TopkWs {
   int64_t cap;
   uint32_t* fb;        // parallel exact fallback scratch [kFbWords] (zero between uses)
   int32_t* hstatus;    // registered pinned host status word (grace_topk_status_word) or null
-  uint32_t spin_max;   // bound of every parallel-fallback wait, in polls (grace_topk_fallback_spin_limit)
+  uint32_t spin_max;   // bound of every parallel-fallback wait, in microseconds of wall time
+                       // (grace_topk_fallback_spin_limit; s_memrealtime runs at 100 MHz)
 };
 
 static inline int64_t topk_cap(int64_t n, int64_t k) {
@@ -197,7 +198,9 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr int kFbWordsHost = 64 + 3 * 2048 + 2 * 1024;
 // the host word every top-k launch reports a run-out to, and the bound of the fallback's waits
 static int32_t* g_topk_hstatus = nullptr;
-static uint32_t g_fb_spin_max = 1u << 22;
+// 2 s: the claimed-slice fallback always progresses, so only a true hang (a device so oversubscribed
+// that a claimed slice's workgroup makes no progress for seconds) may trip it
+static uint32_t g_fb_spin_max = 2000000u;
 
 static TopkWs carve(void* ws, int64_t n, int64_t k) {
   char* p = reinterpret_cast<char*>(ws);
@@ -699,11 +702,14 @@ constexpr int kStageWave = kStage / kMainWaves;            // each wave's own re
 
 struct MainShared {
   uint32_t hist[kHistBins];
-  int2 sure[kStage];
-  int2 cand[kStage];
-  uint32_t wcnt[kMainWaves];   // each wave's packed staged counts (sure | cand << 16), for the flush
+  // v3: ONE staged list of flagged elements, kListWave entries per wave (sure / candidate decided at
+  // the flush); v2 (A/B build): sure = list[0 .. kStage), candidates = list[kStage .. 2 kStage)
+  int2 list[2 * kStage];
+  uint32_t wcnt[kMainWaves];   // each wave's staged count (v2: packed sure | cand << 16), for the flush
   uint32_t gbase[2];           // the chunk's reservations in the global sure / candidate lists
+  uint32_t cnt[2];             // v3 flush: the chunk's sure / candidate counts, then their positions
 };
+constexpr int kListWave = 2 * kStage / kMainWaves;         // v3: each wave's region of the one list
 
 // wave-wide inclusive scan of one uint32 per lane: DPP row shifts within each 16-lane row, then
 // the row broadcasts (gfx9 row_bcast:15 / row_bcast:31) -- 6 VALU, no LDS, no loop
@@ -815,14 +821,14 @@ __device__ __forceinline__ uint32_t classify_group(const StepArgs& a, const Topk
           const int2 e = make_int2((int)i, (int)f2u(tv));
           if ((msure >> b) & 1u) {
             if (ps < (uint32_t)kStageWave) {
-              sm.sure[wb + ps] = e;
+              sm.list[wb + ps] = e;
             } else if (gs < (uint32_t)a.k) {
               a.vals[gs] = tv; a.idx[gs] = (int32_t)(e.x + a.idx_base); ++gs;
             }
             ++ps;
           } else {
             if (pc < (uint32_t)kStageWave) {
-              sm.cand[wb + pc] = e;
+              sm.list[kStage + wb + pc] = e;
             } else {
               atomicAdd(&sm.hist[cand_bin(abs_key(tv), lo, sh)], 1u);
               if (gcn < (uint32_t)w.cap) w.cand[gcn] = e;
@@ -837,6 +843,234 @@ __device__ __forceinline__ uint32_t classify_group(const StepArgs& a, const Topk
   return wfill + tot;
 }
 
+// ------------------------------------------------------------------------------------------------
+// v3 classification (r06).  The r05 SQ counters of the no-memory main pass (4 B read per element,
+// profiles/r06_nomem_sq_summary.json) showed 2640 VALU instructions per wave for 128 elements per
+// lane -- 20 per element, 35 us of the SIMDs' issue time against a 43 us read stream, half of them
+// in v2's walk over the 16 element positions of a group (one divergent block per position that any
+// lane flagged, ~10 of 16 with ~15 flagged elements per wave and group).  v3 keeps per element only
+// what every element needs: its dense outputs, if any, and ONE flag bit (key >= lo) shifted into a
+// per-lane 16-bit mask -- a compare and an add-with-carry.  The flagged elements (~1.5 %) are then
+// visited by a per-lane set-bit loop whose trip count is the wave's largest popcount (typically 2),
+// which classifies them exactly and stages them in the wave's region of ONE LDS list; the flush
+// splits sure entries from candidates.
+#ifndef GRACE_MAIN_V2
+#define GRACE_MAIN_V2 0
+#endif
+constexpr bool kMainV3 = GRACE_MAIN_V2 == 0;   // A/B knob: 1 builds the r05 classification
+
+// t[e >> 2].(e & 3) of a lane whose element e is known only at run time: a select tree on e's bits
+__device__ __forceinline__ float sel16(const float4 (&t)[4], uint32_t e) {
+  const float4 p = (e & 4u) ? t[1] : t[0];
+  const float4 q = (e & 4u) ? t[3] : t[2];
+  const float4 c = (e & 8u) ? q : p;
+  const float x = (e & 1u) ? c.y : c.x;
+  const float y = (e & 1u) ? c.w : c.z;
+  return (e & 2u) ? y : x;
+}
+
+// a flagged element past its wave's LDS region (massive ties inside the band): classified here and
+// appended with one global atomic (rare; the finalize sees list overflows as usual)
+__device__ __forceinline__ void spill_entry(const StepArgs& a, const TopkWs& w, MainShared& sm, int2 e, uint32_t key,
+                                            uint32_t lo, uint32_t hi, uint32_t sh) {
+  if (key > hi) {
+    const uint32_t gp = atomicAdd(&w.ctl->n_sure, 1u);
+    if (gp < (uint32_t)a.k) {
+      a.vals[gp] = u2f((uint32_t)e.y);
+      a.idx[gp] = (int32_t)(e.x + a.idx_base);
+    }
+  } else {
+    atomicAdd(&sm.hist[cand_bin(key, lo, sh)], 1u);
+    const uint32_t gp = atomicAdd(&w.ctl->n_cand, 1u);
+    if (gp < (uint32_t)w.cap) w.cand[gp] = e;
+  }
+}
+
+template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false>
+__device__ __forceinline__ uint32_t classify_group_v3(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                                      uint32_t hi, uint32_t sh, uint32_t mid, int64_t gbase,
+                                                      const float4 (&rc)[kGroup], const float4 (&gc)[kGroup],
+                                                      uint32_t wfill) {
+  static_assert(kGroup == 4, "sel16 picks from 4 float4 per lane");
+#ifdef GRACE_MAIN_STREAM_ONLY   // diagnostic A/B build only: the streaming ceiling of this layout
+  constexpr bool kSkel = true;
+#else
+  constexpr bool kSkel = SKEL;
+#endif
+  // the exact provisional decision (key > mid) per element, where a dense output depends on it
+  constexpr bool kDenseProv = kProv<MODE> && (kWritesR<MODE> || (kWritesOut<MODE> && !SPARSE));
+  const int64_t n = a.n;
+  const float lo_f = u2f(lo);
+  float4 t[kGroup];
+  uint32_t m = 0;   // element e = u * 4 + j flagged at bit 15 - e
+#pragma unroll
+  for (int u = 0; u < kGroup; ++u) {
+    if constexpr (HAS_RES && UNIT) {
+      t[u].x = rc[u].x + gc[u].x;
+      t[u].y = rc[u].y + gc[u].y;
+      t[u].z = rc[u].z + gc[u].z;
+      t[u].w = rc[u].w + gc[u].w;
+    } else if constexpr (HAS_RES) {
+      t[u].x = a.beta * rc[u].x + a.gamma * gc[u].x;
+      t[u].y = a.beta * rc[u].y + a.gamma * gc[u].y;
+      t[u].z = a.beta * rc[u].z + a.gamma * gc[u].z;
+      t[u].w = a.beta * rc[u].w + a.gamma * gc[u].w;
+    } else {
+      t[u] = gc[u];
+    }
+    const int64_t i0 = gbase + (int64_t)u * (kMainBlock * 4);
+    float4 rout = t[u], dout = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float tv = comp4(t[u], j);
+      bool f;
+      if constexpr (kDenseProv) {
+        // sure elements, and candidates above the provisional threshold, are written as selected
+        // (r' = t - t, out = 0 + t); the finalize fixes up the candidates it decides otherwise.
+        // lo <= mid <= hi (bracket_publish), so that set is key > mid
+        const uint32_t key = abs_key(tv);
+        const bool sel = !kSkel && key > mid;
+        set4(rout, j, sel ? tv - tv : tv);
+        if constexpr (kWritesOut<MODE> && !SPARSE) set4(dout, j, sel ? 0.f + tv : 0.f);
+        f = key >= lo;
+      } else {
+        // a superset test, made exact in the loop below: |t| >= lo, or NaN (unordered); a denormal
+        // flushed to 0 would compare as 0 on both sides
+        f = !(fabsf(tv) < lo_f);
+      }
+      if (!FAST) f = f && i0 + j < n;
+      if (kSkel) f = false;
+      m = m + m + (f ? 1u : 0u);
+    }
+    if constexpr (kWritesR<MODE>) st4<FAST>(a.r, i0, n, rout);
+    if constexpr (kWritesOut<MODE> && !SPARSE) st4<FAST>(a.out, i0, n, dout);
+  }
+  if constexpr (SKEL) return wfill;
+  const uint32_t cnt = __popc(m);
+  const uint32_t incl = wave_incl_scan_dpp(cnt);
+  const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+  uint32_t slot = wfill + incl - cnt;   // this lane's first slot in the wave's region
+  const uint32_t wb = (threadIdx.x >> 6) * kListWave;
+  uint32_t ovf = 0;                      // flagged elements past the region (bit 15 - e)
+  while (m) {
+    const uint32_t b = (uint32_t)__builtin_ctz(m);
+    m &= m - 1u;
+    const uint32_t e = 15u - b;
+    const float tv = sel16(t, e);
+    const uint32_t key = abs_key(tv);
+    const bool ok = key >= lo;             // exact (the float flag was a superset)
+    // (recycled output: the flush writes the provisional picks, so that no global store sits
+    // between a group's loads and their waits -- vmcnt counts stores too)
+    // a flag the exact test rejects leaves an empty entry
+    const int2 ent = ok ? make_int2((int)(gbase + (int64_t)(e >> 2) * (kMainBlock * 4) + (e & 3u)), (int)f2u(tv))
+                        : make_int2(-1, 0);
+    if (slot < (uint32_t)kListWave) sm.list[wb + slot] = ent;
+    else ovf |= (ok ? 1u : 0u) << b;
+    ++slot;
+  }
+  // rare: entries past the wave's region leave through global atomics, outside the loop above so
+  // that its memory operations stay store-only
+  if (__ballot(ovf != 0)) {
+    while (ovf) {
+      const uint32_t b = (uint32_t)__builtin_ctz(ovf);
+      ovf &= ovf - 1u;
+      const uint32_t e = 15u - b;
+      const float tv = sel16(t, e);
+      const int64_t i = gbase + (int64_t)(e >> 2) * (kMainBlock * 4) + (e & 3u);
+      const uint32_t key = abs_key(tv);
+      if constexpr (SPARSE && kWritesOut<MODE>) if (key > mid) a.out[i] = 0.f + tv;
+      spill_entry(a, w, sm, make_int2((int)i, (int)f2u(tv)), key, lo, hi, sh);
+    }
+  }
+  return wfill + tot;
+}
+
+// v3 flush: the waves' regions are concatenated; one pass counts sure / candidate entries with wave
+// ballots, one reservation per list and chunk, a second pass writes them (wave ballot ranks, one LDS
+// add per wave and list); candidates are counted into the LDS histogram there
+template <bool SPARSE_OUT>
+__device__ __forceinline__ void flush_staged_v3(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                                uint32_t hi, uint32_t sh, uint32_t mid, uint32_t wfill) {
+  const int tid = threadIdx.x;
+  if ((tid & 63) == 0) sm.wcnt[tid >> 6] = min(wfill, (uint32_t)kListWave);
+  if (tid == 0) sm.cnt[0] = 0u;
+  __syncthreads();
+  uint32_t off[kMainWaves + 1];
+  off[0] = 0;
+#pragma unroll
+  for (int v = 0; v < kMainWaves; ++v) off[v + 1] = off[v] + sm.wcnt[v];
+  const uint32_t ne = off[kMainWaves];
+  auto entry = [&](uint32_t j) {
+    int v = 0;
+#pragma unroll
+    for (int x = 1; x < kMainWaves; ++x) v += j >= off[x];
+    return sm.list[v * kListWave + (j - off[v])];
+  };
+  uint32_t ns_w = 0, nc_w = 0;   // this wave's counts (wave-uniform)
+  for (uint32_t j0 = 0; j0 < ne; j0 += kMainBlock) {
+    const uint32_t j = j0 + tid;
+    const int2 e = j < ne ? entry(j) : make_int2(-1, 0);
+    const bool sure = e.x >= 0 && abs_key(u2f((uint32_t)e.y)) > hi;
+    ns_w += (uint32_t)__popcll(__ballot(sure));
+    nc_w += (uint32_t)__popcll(__ballot(e.x >= 0 && !sure));
+  }
+  if ((tid & 63) == 0 && (ns_w | nc_w)) atomicAdd(&sm.cnt[0], ns_w | (nc_w << 16));
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t c = sm.cnt[0], ns = c & 0xFFFFu, nc = c >> 16;
+#ifdef GRACE_DIAG_NORESERVE   // timing-only A/B build (wrong results): no atomic return to wait for
+    sm.gbase[0] = (uint32_t)((blockIdx.x * 97u) % (uint32_t)(a.k > 2048 ? a.k - 2048 : 1));
+    sm.gbase[1] = (uint32_t)((blockIdx.x * 53u) % (uint32_t)(w.cap > 2048 ? w.cap - 2048 : 1));
+    (void)ns; (void)nc;
+#else
+    sm.gbase[0] = ns ? atomicAdd(&w.ctl->n_sure, ns) : 0u;
+    sm.gbase[1] = nc ? atomicAdd(&w.ctl->n_cand, nc) : 0u;
+#endif
+    sm.cnt[0] = 0u;
+    sm.cnt[1] = 0u;
+  }
+  __syncthreads();
+  for (uint32_t j0 = 0; j0 < ne; j0 += kMainBlock) {
+    const uint32_t j = j0 + tid;
+    const int2 e = j < ne ? entry(j) : make_int2(-1, 0);
+    const uint32_t key = abs_key(u2f((uint32_t)e.y));
+    const bool sure = e.x >= 0 && key > hi, cand = e.x >= 0 && !sure;
+    const uint64_t bs = __ballot(sure), bc = __ballot(cand);
+    uint32_t base_s = 0, base_c = 0;
+    if ((tid & 63) == 0) {
+      if (bs) base_s = atomicAdd(&sm.cnt[0], (uint32_t)__popcll(bs));
+      if (bc) base_c = atomicAdd(&sm.cnt[1], (uint32_t)__popcll(bc));
+    }
+    base_s = __builtin_amdgcn_readfirstlane(base_s);
+    base_c = __builtin_amdgcn_readfirstlane(base_c);
+    // recycled output: only the provisional picks (key > mid, mid >= lo) are written
+    if constexpr (SPARSE_OUT) if (e.x >= 0 && key > mid) a.out[e.x] = 0.f + u2f((uint32_t)e.y);
+    if (sure) {
+      const uint32_t gp = sm.gbase[0] + base_s + lane_rank(bs);
+      if (gp < (uint32_t)a.k) {
+        a.vals[gp] = u2f((uint32_t)e.y);
+        a.idx[gp] = (int32_t)(e.x + a.idx_base);
+      }
+    } else if (cand) {
+      atomicAdd(&sm.hist[cand_bin(key, lo, sh)], 1u);
+      const uint32_t gp = sm.gbase[1] + base_c + lane_rank(bc);
+      if (gp < (uint32_t)w.cap) w.cand[gp] = e;
+    }
+  }
+  __syncthreads();   // the list and wcnt are free for the next chunk
+}
+
+template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false>
+__device__ __forceinline__ uint32_t classify_group_sel(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                                       uint32_t hi, uint32_t sh, uint32_t mid, int64_t gbase,
+                                                       const float4 (&rc)[kGroup], const float4 (&gc)[kGroup],
+                                                       uint32_t wfill) {
+  if constexpr (kMainV3)
+    return classify_group_v3<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
+  else
+    return classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
+}
+
 template <bool HAS_RES, int MODE, bool FAST, bool SKEL = false, bool SPARSE = false, bool UNIT = false,
           int NV = kVecOf<HAS_RES, MODE>>
 __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkWs& w, MainShared& sm,
@@ -845,6 +1079,29 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
   static_assert(NG * kGroup == NV, "groups tile the chunk (group 2 / 3 / 6 lost 0-5 %, A/B)");
   const int64_t cbase = chunk * (kMainBlock * 4 * NV) + (int64_t)threadIdx.x * 4;
   uint32_t wfill = 0;
+  if constexpr (kMainV3 && FAST) {
+    // v3: the group loop fully unrolled over a static ring of R group buffers (R - 1 groups' loads
+    // in flight ahead of the one being classified).  Every load is unconditional at compile time:
+    // a load that a run-time condition may skip (the r05 ring's `q + R - 1 < NG`), or a rotating
+    // copy of the next group's buffer into the current one (v2), made hipcc wait vmcnt(0) -- for
+    // every load in flight -- once per group
+    constexpr int R = HAS_RES ? 2 : 3;   // buffers: 2 x (r, g) or 3 x g
+    constexpr int64_t S = (int64_t)kGroup * (kMainBlock * 4);
+    float4 rb[R][kGroup], gb[R][kGroup];
+#pragma unroll
+    for (int p = 0; p < R - 1; ++p)
+      if (p < NG) load_group<HAS_RES, FAST>(a, cbase + p * S, rb[p], gb[p]);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      // no instruction crosses a group boundary: the scheduler would otherwise hoist later groups'
+      // loads and spill (the unrolled ring at 128 VGPRs with 15-70 spilled)
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + R - 1 < NG) load_group<HAS_RES, FAST>(a, cbase + (q + R - 1) * S, rb[(q + R - 1) % R], gb[(q + R - 1) % R]);
+      wfill = classify_group_v3<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, cbase + q * S,
+                                                                         rb[q % R], gb[q % R], wfill);
+    }
+    return wfill;
+  }
   if constexpr (kMainRing) {
     // A static ring of R group buffers, R - 1 groups' loads in flight ahead of the one being
     // classified: the loop body is unrolled over the R slots, so no buffer is ever copied.  (The
@@ -864,7 +1121,7 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
         const int q = q0 + j;
         if (q < NG) {   // workgroup-uniform
           if (q + R - 1 < NG) load_group<HAS_RES, FAST>(a, cbase + (q + R - 1) * S, rb[(j + R - 1) % R], gb[(j + R - 1) % R]);
-          wfill = classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, cbase + q * S,
+          wfill = classify_group_sel<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, cbase + q * S,
                                                                           rb[j], gb[j], wfill);
         }
       }
@@ -883,7 +1140,7 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
     for (int q = 0; q < NG; ++q) {
       const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
       if (q + 2 < NG) load_group<false, FAST>(a, gbase + 2 * kGroup * (kMainBlock * 4), rc, g2);
-      wfill = classify_group<false, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
+      wfill = classify_group_sel<false, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
 #pragma unroll
       for (int u = 0; u < kGroup; ++u) { gc[u] = g1[u]; g1[u] = g2[u]; }
     }
@@ -896,7 +1153,7 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
     const int64_t gbase = cbase + (int64_t)q * kGroup * (kMainBlock * 4);
     float4 rn[kGroup], gn[kGroup];
     if (q + 1 < NG) load_group<HAS_RES, FAST>(a, gbase + kGroup * (kMainBlock * 4), rn, gn);
-    wfill = classify_group<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
+    wfill = classify_group_sel<HAS_RES, MODE, FAST, SKEL, SPARSE, UNIT>(a, w, sm, lo, hi, sh, mid, gbase, rc, gc, wfill);
 #pragma unroll
     for (int u = 0; u < kGroup; ++u) { rc[u] = rn[u]; gc[u] = gn[u]; }
   }
@@ -905,8 +1162,8 @@ __device__ __forceinline__ uint32_t main_chunk_v2(const StepArgs& a, const TopkW
 
 // the staged lists of one chunk leave with one global atomic per list: the waves' regions are
 // concatenated in wave order (v2: the staged candidates are counted into the LDS histogram here)
-__device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
-                                             uint32_t sh, uint32_t wfill) {
+__device__ __forceinline__ void flush_staged_v2(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                                uint32_t sh, uint32_t wfill) {
   const int tid = threadIdx.x;
   if ((tid & 63) == 0) sm.wcnt[tid >> 6] = wfill;
   __syncthreads();
@@ -937,7 +1194,7 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
       int v = 0;
 #pragma unroll
       for (int x = 1; x < kMainWaves; ++x) v += j >= os[x];
-      const int2 e = sm.sure[v * kStageWave + (j - os[v])];
+      const int2 e = sm.list[v * kStageWave + (j - os[v])];
       a.vals[gp] = u2f((uint32_t)e.y);
       a.idx[gp] = (int32_t)(e.x + a.idx_base);
     }
@@ -947,11 +1204,18 @@ __device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w,
     int v = 0;
 #pragma unroll
     for (int x = 1; x < kMainWaves; ++x) v += j >= oc[x];
-    const int2 e = sm.cand[v * kStageWave + (j - oc[v])];
+    const int2 e = sm.list[kStage + v * kStageWave + (j - oc[v])];
     atomicAdd(&sm.hist[cand_bin(abs_key(u2f((uint32_t)e.y)), lo, sh)], 1u);
     if (gp < (uint32_t)w.cap) w.cand[gp] = e;
   }
   __syncthreads();   // the lists and wcnt are free for the next chunk
+}
+
+template <bool SPARSE_OUT = false>
+__device__ __forceinline__ void flush_staged(const StepArgs& a, const TopkWs& w, MainShared& sm, uint32_t lo,
+                                             uint32_t hi, uint32_t sh, uint32_t mid, uint32_t wfill) {
+  if constexpr (kMainV3) flush_staged_v3<SPARSE_OUT>(a, w, sm, lo, hi, sh, mid, wfill);
+  else flush_staged_v2(a, w, sm, lo, sh, wfill);
 }
 
 // NV: float4 per lane per chunk
@@ -988,7 +1252,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void topk_main(StepArgs a, TopkWs w)
       wfill = main_chunk_v2<HAS_RES, MODE, VEC, SKEL, SPARSE, false, NV>(a, w, sm, lo, hi, sh, mid, chunk);
     else
       wfill = main_chunk_v2<HAS_RES, MODE, false, SKEL, SPARSE, false, NV>(a, w, sm, lo, hi, sh, mid, chunk);
-    if constexpr (!SKEL) flush_staged(a, w, sm, lo, sh, wfill);
+    if constexpr (!SKEL) flush_staged<SPARSE && kWritesOut<MODE>>(a, w, sm, lo, hi, sh, mid, wfill);
     (void)wfill;
   }
   if constexpr (SKEL) return;
@@ -1283,12 +1547,14 @@ __device__ __forceinline__ void fb_abort(const TopkWs& w) {
 template <int BLOCK>
 __device__ bool fb_wait(const TopkWs& w, int p, uint32_t nsl, FinShared<BLOCK>& fs) {
   if (threadIdx.x == 0) {
-    uint32_t ok = 1, spins = 0;
+    uint32_t ok = 1;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t lim = (uint64_t)w.spin_max * 100u;   // 100 MHz ticks
     for (;;) {
       asm volatile("" ::: "memory");
       if (ld_agent_u32(w.fb + kFbDone + p) >= nsl) break;
       if (ld_agent_u32(w.fb + kFbAbort)) { ok = 0; break; }
-      if (spins++ >= w.spin_max) { fb_abort(w); ok = 0; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 >= lim) { fb_abort(w); ok = 0; break; }
       __builtin_amdgcn_s_sleep(2);
     }
     fs.s_res[0] = ok;
@@ -2068,7 +2334,7 @@ __global__ __launch_bounds__(kMainBlock, 4) void seg_main_kernel(SegPlan p) {
   } else {
     wfill = main_chunk_v2<HAS_RES, MODE, false>(a, w, sm, lo, hi, sh, mid, chunk);
   }
-  flush_staged(a, w, sm, lo, sh, wfill);
+  flush_staged(a, w, sm, lo, hi, sh, mid, wfill);
   __syncthreads();
   for (int b = tid; b < kHistBins; b += kMainBlock) {
     const uint32_t h = sm.hist[b];

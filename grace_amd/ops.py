@@ -330,7 +330,10 @@ def _topk_status():
         v = int(_lib.query("grace_status_take", hit[0].data_ptr()))   # read-and-clear, host atomic
         if v & 2:
             raise TopKWaitError("grace_amd: a top-k exact-fallback wait ran out in an earlier call; its "
-                                "payload, residual and output were not valid")
+                                "payload, residual and output were not valid -- discard the residual / "
+                                "sharded state of the names stepped since the last check (e.g. "
+                                "memory.residuals.pop(name)), or run with TopKCompressor(check_sync=True) "
+                                "so the failing step itself raises")
     return hit[0]
 
 
@@ -342,7 +345,8 @@ def topk_check():
 
 
 def topk_fallback_spin_limit(limit=-1):
-    """Bound of the parallel exact fallback's waits in polls (tests force 0); returns the previous."""
+    """Bound of each parallel exact-fallback wait in microseconds of device wall time (default
+    2 s, so only a true hang trips it; tests force 0); returns the previous bound."""
     return int(_lib.query("grace_topk_fallback_spin_limit", int(limit)))
 
 

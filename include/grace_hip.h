@@ -63,8 +63,12 @@ int32_t grace_status_take(int32_t* host_word);
  * reports to: bit 2 = a wait of the parallel exact fallback ran out, so that launch's payload /
  * residual / output are NOT valid (the fallback aborted in every workgroup; its waits are only on
  * slices that running workgroups claimed, so this is never expected).  The device status word of
- * grace_read_status then reads 2.  grace_topk_fallback_spin_limit sets the bound of those waits in
- * polls (limit < 0: unchanged) and returns the previous bound; tests set 0 to force a run-out. */
+ * grace_read_status then reads 2.  grace_topk_fallback_spin_limit sets the bound of each of those
+ * waits in microseconds of device wall time (default 2,000,000 = 2 s: only a true hang trips it;
+ * limit < 0: unchanged) and returns the previous bound; tests set 0 to force a run-out.  The
+ * launch's own results are already invalid when the word reports it: a caller that needs the
+ * failing step itself to raise checks the word after that step's event (TopKCompressor
+ * check_sync=True); otherwise the next top-k call raises. */
 grace_status_t grace_topk_status_word(int32_t* host_word);
 int64_t grace_topk_fallback_spin_limit(int64_t limit);
 

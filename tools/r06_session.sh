@@ -1,0 +1,50 @@
+#!/bin/bash
+# r06 GPU measurement session: tools/r06_session.sh STEP...  (each step under its own timeout;
+# outputs under gpurun_out/r06/).  Steps:
+#   scatter    tools/scatter_probe (read + sparse-write granules, clear lists)
+#   nomemkt    kernel trace of the no-memory top-k bench (bench.py --workload topk_nomem)
+#   nomemsq    SQ + FETCH / WRITE counter passes of the no-memory top-k (tools/pmc_sq.sh)
+#   headsq     SQ counter passes of the headline (the bimodality record)
+#   prof       the headline, single stream, steady composition (tools/prof_steady.py)
+#   bench      the default bench line
+#   wl:NAME    one secondary bench line (bench.py --workload NAME)
+#   pytest     the whole -m gpu suite
+#   t:PATH     one GPU test file
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r06; mkdir -p $O
+export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
+run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1; local rc=$?
+        echo "$name rc=$rc"; tail -4 "$O/$name.log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+sqpasses() {   # $1 tag, rest: the program
+  local tag=$1; shift
+  local i=0
+  for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i + 1))
+    run ${tag}_$i 120 rocprofv3 --pmc $c --output-format csv -d $O/${tag}_$i -o pmc -- "$@"
+  done
+}
+for s in "$@"; do
+  case $s in
+    scatter) run scatter 120 ./tools/scatter_probe ;;
+    nomemkt) run nomem_kt 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sq_nomem_kt -o run \
+               -- python3 bench.py --workload topk_nomem --steps 20 --warmup 5 --no-cpu-baseline ;;
+    nomemsq) sqpasses sq_nomem python3 bench.py --workload topk_nomem --steps 5 --warmup 2 --no-cpu-baseline
+             python3 tools/pmc_sq_summary.py $O/sq_nomem > $O/sq_nomem_summary.json; echo "sq summary rc=$?" ;;
+    headsq) GRACE_BENCH_NO_PROBE=1 sqpasses sq_head python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-overlap
+            python3 tools/pmc_sq_summary.py $O/sq_head > $O/sq_head_summary.json; echo "sq summary rc=$?" ;;
+    prof) GRACE_BENCH_NO_PROBE=1 run prof_topk 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_topk -o run \
+            -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
+          python3 tools/prof_steady.py $O/prof_topk --last 20 --out $O/prof_topk_steady.json; echo "steady rc=$?" ;;
+    bench) run bench 300 python3 bench.py ;;
+    abv3) run ab_v3 300 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_main_v2.so grace_amd/lib/libgrace_hip.so ;;
+    topktests) run topktests 900 python3 -u -m pytest tests/test_gpu_topk.py tests/test_gpu_topk_recycle.py \
+        tests/test_gpu_topk_carry.py tests/test_gpu_harness.py tests/test_gpu_sparse.py -q -x --timeout 300 --timeout-method thread ;;
+    wl:*) w=${s#wl:}; run "bench_$w" 300 python3 bench.py --workload $w --steps 20 --no-cpu-baseline ;;
+    pytest) run pytest_gpu 1100 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    t:*) f=${s#t:}; b=$(basename $f .py); run "pytest_$b" 600 python3 -u -m pytest $f -q -x --timeout 300 --timeout-method thread ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
