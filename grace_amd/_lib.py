@@ -108,6 +108,7 @@ SIGNATURES = {
     "grace_qsgd_compress": (ST, [P, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
     "grace_qsgd_compress_at": (ST, [P, I64, P, P, I32, I64, I32, I32, I32, P, U64, P, P, P, P]),
     "grace_qsgd_decompress": (ST, [P, P, I64, I64, I32, P, P, I32, I64, I32, I32, I32, I32, F32, P, P]),
+    "grace_qsgd_decompress_records": (ST, [P, I64, I64, I32, I64, P, P, P, I32, I64, I32, I32, P, P]),
     "grace_qsgd_global_workspace_bytes": (SZ, []),
     "grace_qsgd_global_compress": (ST, [P, I64, I32, P, U64, P, P, P, P, P]),
     "grace_randomk_perm_indices": (ST, [U64, I64, I64, P, P]),
@@ -130,6 +131,7 @@ SIGNATURES = {
     "grace_terngrad_compress": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_step_w1": (ST, [P, P, P, I32, I64, P, P, U64, P, P, P, P]),
     "grace_terngrad_decompress": (ST, [P, P, I64, I64, I32, P, I32, I64, I32, F32, P, P]),
+    "grace_terngrad_decompress_records": (ST, [P, I64, I32, P, I32, P, P, I32, I64, P, P]),
     "grace_natural_compress": (ST, [P, I64, P, U64, P, P]),
     "grace_natural_compress_at": (ST, [P, I64, I64, P, U64, P, P]),
     "grace_cnat_compress": (ST, [P, I64, P, I32, U64, P, P]),

@@ -925,12 +925,24 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_kernel(
 // quads), kQNB buckets per row per iteration, every load issued before any is used.  The segment
 // walk and the scale norm_w / q (one division) are per bucket and lane-pair of quads instead of
 // per quad.  Same arithmetic as qsgd_decode_kernel.
+// Sharded records (grace_qsgd_decompress_records, sharded_quant.py): the codes and norms of the
+// bucket's buckets [w U, (w + 1) U) sit in rank w's gathered record -- codes from the record's
+// start (element rank_lo[w] first), norms from rec_norms floats further -- so bucket b reads
+// through rank w = b / U's record.  units == 0: the plain flat layout.
+struct QShardRec {
+  int64_t units;       // buckets per rank U (0: off)
+  int64_t rec_codes;   // record stride in codes
+  int64_t rec_norms;   // record stride in floats
+  int64_t norm_off;    // the norms' offset inside a record, in floats
+  const int64_t* lo;   // rank_lo[w]: the first element of rank w's range
+};
+
 template <typename CodeT, int VARIANT>
 __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
     const CodeT* __restrict__ codes, const float* __restrict__ norms, int64_t code_stride,
     int64_t norm_stride, int world, const int64_t* __restrict__ seg_off,
     const int64_t* __restrict__ bkt_off, int nseg, float qf, float divisor, int aggregate, int vec,
-    float* __restrict__ out) {
+    float* __restrict__ out, QShardRec sr = QShardRec{0, 0, 0, 0, nullptr}) {
   __shared__ SegTables32 tab;
   stage_tables32(tab, seg_off, bkt_off, nseg);
   const int l16 = threadIdx.x & 15;
@@ -943,6 +955,8 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
   for (int32_t b = b_first; b < bhi; b += kQNB * kRows) {
     int32_t bb[kQNB], e[kQNB][2], end[kQNB];
     bool ok[kQNB], full[kQNB][2];
+    const CodeT* cp[kQNB];   // codes / norms of bucket bb[h] (a rank's record with sharded records)
+    const float* np[kQNB];
 #pragma unroll
     for (int h = 0; h < kQNB; ++h) {
       bb[h] = b + h * kRows;
@@ -950,10 +964,20 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
       if (ok[h]) s = seg_advance32(tab.sub, nseg, s, bb[h]);
       const int32_t base = tab.seg[s] + (bb[h] - tab.sub[s]) * 128;
       end[h] = ok[h] ? min(base + 128, tab.seg[s + 1]) : base;
+      cp[h] = codes;
+      np[h] = norms;
+      bool al = true;
+      if (sr.units && ok[h]) {
+        const int64_t w = bb[h] / sr.units;
+        const int64_t lo = sr.lo[w];
+        cp[h] = codes + w * sr.rec_codes - lo;
+        np[h] = norms + w * sr.rec_norms + sr.norm_off - w * sr.units;
+        al = ((base - lo) & 3) == 0;   // the record's codes start at rank_lo[w]
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         e[h][q] = base + 4 * l16 + 64 * q;   // quads l16 and l16 + 16: each instruction covers 256 contiguous bytes per row
-        full[h][q] = ok[h] && vec && (base & 3) == 0 && e[h][q] + 3 < end[h];
+        full[h][q] = ok[h] && vec && al && (base & 3) == 0 && e[h][q] + 3 < end[h];
       }
     }
     float acc[kQNB][2][4] = {};
@@ -964,15 +988,15 @@ __global__ __launch_bounds__(kQBlock) void qsgd_decode_bkt_kernel(
       for (int h = 0; h < kQNB; ++h) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-          load_codes4(codes + (full[h][q] ? w * code_stride + e[h][q] : 0), true, c[h][q]);
-        nrm[h] = norms[w * norm_stride + (ok[h] ? bb[h] : 0)];
+          load_codes4(full[h][q] ? cp[h] + w * code_stride + e[h][q] : codes, true, c[h][q]);
+        nrm[h] = ok[h] ? np[h][w * norm_stride + bb[h]] : norms[0];
       }
 #pragma unroll
       for (int h = 0; h < kQNB; ++h) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
           if (ok[h] && !full[h][q]) {
-            const CodeT* p = codes + w * code_stride + e[h][q];
+            const CodeT* p = cp[h] + w * code_stride + e[h][q];
 #pragma unroll
             for (int j = 0; j < 4; ++j) c[h][q][j] = e[h][q] + j < end[h] ? load_code1(p + j) : 0.f;
           }
@@ -1582,6 +1606,67 @@ __global__ __launch_bounds__(kQBlock) void tern_decode_kernel(const int8_t* __re
   }
 }
 
+// Sharded TernGrad (grace_amd/dist/sharded_terngrad.py): the whole bucket decoded straight from the
+// gathered per-rank records.  Rank w's codes of its elements [rank_lo[w], rank_lo[w + 1]) sit in
+// its record at w * rec_bytes, as int8 or (packed) in the 2-bit planar layout of the reference's
+// packing (grace_dl/tensorflow/compressor/packing.py:4-29, code + 1: element i of an L-element
+// block in byte i % Q at bits 2 (i / Q), Q = grace_pack2_bytes(L)) -- no unpack pass, no copy into
+// a flat code buffer.  out = code * scalar, tern_decode_kernel's arithmetic at world 1.
+constexpr int kRecRanksMax = 64;
+
+__device__ __forceinline__ float tern_rec_code(const uint8_t* __restrict__ r, uint32_t i, uint32_t L, int packed) {
+  if (!packed) return (float)(int8_t)r[i];
+  const uint32_t Q = (L + (4u - L % 4u)) / 4u;
+  const uint32_t pl = i / Q;
+  return (float)((int)((r[i - pl * Q] >> (2u * pl)) & 3u) - 1);
+}
+
+__global__ __launch_bounds__(kQBlock) void tern_decode_records_kernel(const uint8_t* __restrict__ rec, int64_t rec_bytes,
+                                                                     int world, const int64_t* __restrict__ rank_lo,
+                                                                     int packed, const float* __restrict__ scalars,
+                                                                     const int64_t* __restrict__ seg_off, int nseg,
+                                                                     int64_t n, float* __restrict__ out) {
+  __shared__ SegTables tab;
+  __shared__ int64_t rlo[kRecRanksMax + 1];
+  for (int i = threadIdx.x; i <= world; i += blockDim.x) rlo[i] = rank_lo[i];
+  const SegView sv = stage_tables(tab, seg_off, nullptr, nseg);
+  __syncthreads();
+  int w = 0, s = 0;
+  for (int64_t e = 4 * ((int64_t)blockIdx.x * kQBlock + threadIdx.x); e < n; e += 4 * (int64_t)gridDim.x * kQBlock) {
+    while (w + 1 < world && rlo[w + 1] <= e) ++w;   // e grows: the rank and segment only advance
+    s = seg_advance(sv.seg, nseg, s, e);
+    const uint32_t i = (uint32_t)(e - rlo[w]), L = (uint32_t)(rlo[w + 1] - rlo[w]);
+    const uint8_t* r = rec + w * rec_bytes;
+    if (e + 3 < n && e + 3 < rlo[w + 1] && e + 3 < sv.seg[s + 1]) {
+      float c[4];
+      if (packed) {
+        const uint32_t Q = (L + (4u - L % 4u)) / 4u, pl = i / Q, j = i - pl * Q;
+        if (j + 3u < Q) {   // the quad's four codes in one plane: four adjacent bytes
+#pragma unroll
+          for (int t = 0; t < 4; ++t) c[t] = (float)((int)((r[j + t] >> (2u * pl)) & 3u) - 1);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) c[t] = tern_rec_code(r, i + t, L, 1);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) c[t] = (float)(int8_t)r[i + t];
+      }
+      const float sc = scalars[s];
+      __builtin_nontemporal_store(f4v{c[0] * sc, c[1] * sc, c[2] * sc, c[3] * sc}, reinterpret_cast<f4v*>(out + e));
+    } else {
+      // the quad crosses the bucket's end, a rank's range or a segment: element by element
+      for (int64_t x = e; x < e + 4 && x < n; ++x) {
+        int wx = 0;
+        while (wx + 1 < world && rlo[wx + 1] <= x) ++wx;
+        const int sx = find_seg(sv.seg, nseg, x);
+        out[x] = tern_rec_code(rec + wx * rec_bytes, (uint32_t)(x - rlo[wx]), (uint32_t)(rlo[wx + 1] - rlo[wx]), packed) *
+                 scalars[sx];
+      }
+    }
+  }
+}
+
 // ================================================================================================
 // Elementwise byte codecs (natural, cnat, fp16).  Every thread handles quads of 4 consecutive
 // elements: one 16-B load of x (and of an injected random stream), one 4-B code store (8-B for
@@ -2096,6 +2181,49 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
   }
 #undef GRACE_QDEC
   GRACE_CHECK_LAUNCH("grace_qsgd_decompress");
+  return GRACE_OK;
+}
+
+grace_status_t grace_qsgd_decompress_records(const void* records, int64_t rec_bytes, int64_t norm_off_bytes,
+                                             int32_t world, int64_t units_per_rank, const int64_t* rank_lo,
+                                             const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg, int64_t n,
+                                             int32_t quantum_num, int32_t variant, float* out, void* stream) {
+  const int64_t cbytes = variant == 0 && quantum_num >= 128 ? 2 : 1;
+  GRACE_REQUIRE(records && rank_lo && seg_off && bkt_off && out && world >= 1 && nseg >= 1 && n >= 0 &&
+                    units_per_rank >= 1 && nseg <= kSegLds && n < (int64_t(1) << 31) && rec_bytes % 16 == 0 &&
+                    norm_off_bytes % 16 == 0 && norm_off_bytes < rec_bytes && (uintptr_t)records % 16 == 0,
+                "grace_qsgd_decompress_records: bad arguments (16-B aligned records and norms, nseg <= 512)");
+  GRACE_REQUIRE(variant == 0 || (variant == 1 && quantum_num < 128), "grace_qsgd_decompress_records: bad variant");
+  if (n == 0) return GRACE_OK;
+  const char* rec = reinterpret_cast<const char*>(records);
+  const QShardRec sr{units_per_rank, rec_bytes / cbytes, rec_bytes / 4, norm_off_bytes / 4, rank_lo};
+  const float* norms = reinterpret_cast<const float*>(rec);
+  const unsigned bgrid = stream_grid((n + 127) / 128 + nseg, kQNB * kQBlock / 16, kQGridCap);
+  hipStream_t st = as_stream(stream);
+#define GRACE_QDECR(CT, V)                                                                           \
+  qsgd_decode_bkt_kernel<CT, V><<<bgrid, kQBlock, 0, st>>>(reinterpret_cast<const CT*>(rec), norms, 0, 0, 1, \
+                                                          seg_off, bkt_off, nseg, (float)quantum_num, 1.0f, 0, \
+                                                          1, out, sr)
+  if (variant == 1) GRACE_QDECR(int8_t, 1);
+  else if (quantum_num < 128) GRACE_QDECR(int8_t, 0);
+  else GRACE_QDECR(__half, 0);
+#undef GRACE_QDECR
+  GRACE_CHECK_LAUNCH("grace_qsgd_decompress_records");
+  return GRACE_OK;
+}
+
+grace_status_t grace_terngrad_decompress_records(const void* records, int64_t rec_bytes, int32_t world,
+                                                 const int64_t* rank_lo, int32_t packed, const float* scalars,
+                                                 const int64_t* seg_off, int32_t nseg, int64_t n, float* out,
+                                                 void* stream) {
+  GRACE_REQUIRE(records && rank_lo && scalars && seg_off && out && world >= 1 && world <= kRecRanksMax && nseg >= 1 &&
+                    n >= 0 && n < (int64_t(1) << 31) && rec_bytes >= 0 && (uintptr_t)out % 16 == 0,
+                "grace_terngrad_decompress_records: bad arguments (1 <= world <= 64, n < 2^31, 16-B aligned out)");
+  if (n == 0) return GRACE_OK;
+  tern_decode_records_kernel<<<stream_grid((n + 3) / 4, kQBlock, 8192), kQBlock, 0, as_stream(stream)>>>(
+      reinterpret_cast<const uint8_t*>(records), rec_bytes, world, rank_lo, packed ? 1 : 0, scalars, seg_off, nseg, n,
+      out);
+  GRACE_CHECK_LAUNCH("grace_terngrad_decompress_records");
   return GRACE_OK;
 }
 

@@ -1970,6 +1970,31 @@ __global__ __launch_bounds__(256) void topk_all(StepArgs a) {
     emit<MODE>(a, (uint32_t)i, i, compensate<HAS_RES>(a, i));
 }
 
+#ifndef GRACE_MAIN_VEC_NORES_BIG
+#define GRACE_MAIN_VEC_NORES_BIG 64
+#endif
+constexpr int kNoresBigVec = GRACE_MAIN_VEC_NORES_BIG;
+constexpr int64_t kNoresBigMinN = (int64_t)1024 * kMainBlock * 4 * kNoresBigVec;   // 2^26 at 64
+
+// the main pass at NV float4 per lane per chunk (one chunk per workgroup)
+template <bool HAS_RES, int MODE, int NV>
+static void launch_main(const StepArgs& a, const TopkWs& w, bool sparse, bool vec, hipStream_t s) {
+  constexpr int64_t kCh = (int64_t)kMainBlock * 4 * NV;
+  const unsigned nblk = (unsigned)((a.n + kCh - 1) / kCh);
+  if (sparse) {
+    if constexpr (kWritesOut<MODE>) {
+      if (vec)
+        launch_timed(topk_main<HAS_RES, MODE, true, false, true, NV>, dim3(nblk), dim3(kMainBlock), s, a, w);
+      else
+        launch_timed(topk_main<HAS_RES, MODE, false, false, true, NV>, dim3(nblk), dim3(kMainBlock), s, a, w);
+    }
+  } else if (vec) {
+    launch_timed(topk_main<HAS_RES, MODE, true, false, false, NV>, dim3(nblk), dim3(kMainBlock), s, a, w);
+  } else {
+    launch_timed(topk_main<HAS_RES, MODE, false, false, false, NV>, dim3(nblk), dim3(kMainBlock), s, a, w);
+  }
+}
+
 template <bool HAS_RES, int MODE>
 static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s) {
   if (!a.r_in) a.r_in = a.r;
@@ -2007,19 +2032,18 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   topk_bracket<HAS_RES><<<(unsigned)((a.sample_n / kBracketRun + kBracketBlock - 1) / kBracketBlock) + nclr,
                           kBracketBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
-  const unsigned nblk = (unsigned)((a.n + kChunkOf<HAS_RES, MODE> - 1) / kChunkOf<HAS_RES, MODE>);
-  if (sparse) {
-    if constexpr (kWritesOut<MODE>) {
-      if (vec)
-        launch_timed(topk_main<HAS_RES, MODE, true, false, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
-      else
-        launch_timed(topk_main<HAS_RES, MODE, false, false, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
-    }
-  } else if (vec) {
-    launch_timed(topk_main<HAS_RES, MODE, true>, dim3(nblk), dim3(kMainBlock), s, a, w);
-  } else {
-    launch_timed(topk_main<HAS_RES, MODE, false>, dim3(nblk), dim3(kMainBlock), s, a, w);
+  bool big = false;
+  if constexpr (!HAS_RES && kMainV3) {
+    // 4 / 8 B per element (no residual stream): large buckets take chunks of kNoresBigVec float4 per
+    // lane, so that the grid is ONE balanced generation (2^26 elements: 1024 workgroups, 4 per CU;
+    // 32 float4 gave 2048 for 1536 resident slots).  r06 A/B (tools/ab_v3.py, 256 MiB, 1 %): main
+    // pass with the recycled output, 32 / 40 / 48 / 64 / 80 / 96 / 128 float4 -> 72.2 / 67.4 / 67.3 /
+    // 59.2-60.6 / 69.2 / 72.7 / 58.5 us (820 and 683 workgroups leave CUs unevenly loaded).  Only for
+    // k <= n / 50: a wave's LDS region holds 512 flagged elements, ~1.45 % of 16384 at k = 1 %.
+    big = a.n >= kNoresBigMinN && a.k <= a.n / 50;
+    if (big) launch_main<HAS_RES, MODE, kNoresBigVec>(a, w, sparse, vec, s);
   }
+  if (!big) launch_main<HAS_RES, MODE, kVecOf<HAS_RES, MODE>>(a, w, sparse, vec, s);
   GRACE_CHECK_LAUNCH("topk_main");
   // finalize workgroups by the candidate capacity -- one routing round (kSelBlock * kFinPer
   // candidates) each for the band the bracket can produce -- and by the bucket (at most 2^19

@@ -27,9 +27,9 @@ from grace_amd import ops
 class NativePowerSGDKernels:
     """The HIP calls behind each step (GPU tensors only)."""
 
-    def p_draw(self, M, r, seed):
+    def p_draw(self, M, r, seed, out=None):
         ops.dev_f32(M, "rows")   # a GPU f32 tensor, or GraceDeviceError
-        return ops.powersgd_p_draw(M, r, seed)
+        return ops.powersgd_p_draw(M, r, seed, out=out)
 
     def orthogonalize_(self, P):
         return ops.orthogonalize_(P)
@@ -94,19 +94,20 @@ class ShardedPowerSGD:
                 # t = M + r (memory/powersgd.py:16-25: tensor += residual), into a fresh buffer
                 Mi = K.add(res, Mi)
         seed = ops.step_seed("powersgd-q", name, step)
-        Pi = K.p_draw(Mi, r, seed) if hi > lo else torch.empty(0, r, dtype=torch.float32, device=dev)
-        # the whole P on every rank: one all-gather of the row blocks (padded to the largest)
+        # the whole P on every rank: one all-gather of the row blocks.  Every block is `per` rows
+        # except the last non-empty one, so the first n_rows gathered rows ARE P: P_i is drawn
+        # straight into this rank's send block and nothing is copied back (the padding rows after
+        # the last block are never read)
         per = max(b - a for a, b in self.partition(int(n_rows), world))
         if world > 1:
-            send = torch.zeros(per, r, dtype=torch.float32, device=dev)
-            send[:hi - lo].copy_(Pi)
+            send = torch.empty(per, r, dtype=torch.float32, device=dev)
+            if hi > lo:
+                K.p_draw(Mi, r, seed, out=send[:hi - lo])
             gathered = torch.empty(world * per, r, dtype=torch.float32, device=dev)
             dist.all_gather_into_tensor(gathered, send, group=self.group)
-            # the padded row blocks back to one P: one batched copy
-            P = torch.cat([gathered[w * per:w * per + (b - a)]
-                           for w, (a, b) in enumerate(self.partition(int(n_rows), world)) if b > a])
+            P = gathered[:int(n_rows)]
         else:
-            P = Pi.contiguous()
+            P = K.p_draw(Mi, r, seed) if hi > lo else torch.empty(0, r, dtype=torch.float32, device=dev)
         K.orthogonalize_(P)
         Pi = P[lo:hi]
         Q = K.qt(Mi, Pi) if hi > lo else torch.zeros(m, r, dtype=torch.float32, device=dev)

@@ -51,6 +51,26 @@ class NativeQuantKernels:
             return ops.cnat_compress(x, rand=u, deterministic=deterministic, seed=seed, xoff=xoff), None
         return ops.qsgd_compress(x, q, bucket, sizes=sizes, variant=variant, u=u, seed=seed, xoff=xoff)
 
+    def encode_into(self, codec, x, xoff, sizes, u, seed, q, bucket, variant, deterministic, codes, norms):
+        """encode straight into `codes` (and QSGD's `norms`): views of this rank's send record"""
+        if codec == "sign":
+            ops.sign_encode(x, out=codes)
+        elif codec == "fp16":
+            ops.fp16_compress(x, out=codes)
+        elif codec == "natural":
+            ops.natural_compress(x, rand_int=u, seed=seed, xoff=xoff, out=codes)
+        elif codec == "cnat":
+            ops.cnat_compress(x, rand=u, deterministic=deterministic, seed=seed, xoff=xoff, out=codes)
+        else:
+            ops.qsgd_compress(x, q, bucket, sizes=sizes, variant=variant, u=u, seed=seed, xoff=xoff,
+                              codes_out=codes, norms_out=norms)
+
+    def decode_records(self, records, rec_bytes, norm_off, plan, rank_lo, q, variant):
+        """QSGD (bucket 128): the whole bucket from the W gathered records in ONE launch
+        (grace_qsgd_decompress_records), no copy into flat code / norm buffers"""
+        return ops.qsgd_decompress_records(records, rec_bytes, norm_off, len(plan.ranges), plan.max_units, rank_lo,
+                                           q, plan.n, sizes=list(plan.sizes), variant=variant)
+
     def decode(self, codec, codes, norms, sizes, n, q, bucket, variant):
         if codec == "sign":
             return ops.sign_decode(codes)
@@ -167,6 +187,8 @@ class ShardedQuant:
         seed = self.seed if seed is None else seed
         if self.bits:
             return self._step_bits(x, plan, world, rank, lo, hi)
+        if self.dense == "replicated" and world > 1:
+            return self._step_records(x, plan, world, rank, lo, hi, u, seed)
         parts = plan.parts[rank]
         if hi > lo:
             codes, norms = K.encode(self.codec, x, lo, parts, u, seed, self.q, self.bucket, self.variant,
@@ -175,28 +197,55 @@ class ShardedQuant:
             codes = torch.empty(0, dtype=K.code_dtype(self.codec, self.q), device=x.device)
             norms = torch.empty(0, dtype=torch.float32, device=x.device) if self.codec == "qsgd" else None
         self.last_codes, self.last_norms = codes, norms
-        if self.dense == "shard" or world == 1:
-            if hi == lo:
-                return torch.empty(0, dtype=torch.float32, device=x.device)
-            return K.decode(self.codec, codes, norms, parts, hi - lo, self.q, self.bucket, self.variant)
-        # ONE all-gather of fixed-size records: [codes (padded to the longest range) | norms (QSGD,
-        # padded to the most buckets)] as bytes
-        csz = codes.element_size()
+        if hi == lo:
+            return torch.empty(0, dtype=torch.float32, device=x.device)
+        return K.decode(self.codec, codes, norms, parts, hi - lo, self.q, self.bucket, self.variant)
+
+    def _step_records(self, x, plan, world, rank, lo, hi, u, seed):
+        """dense="replicated" at world > 1: the encoder writes this rank's codes (and QSGD's bucket
+        norms) straight into its fixed-size send record, ONE all-gather moves the W records, and the
+        decoder reads them through the record stride: no zero-fill, no copies.  Element-wise codecs:
+        rank r's range is [r U 128, (r + 1) U 128) and the record is exactly U 128 codes (a 16-B
+        multiple), so the gathered records ARE the bucket's codes in order.  QSGD: [codes (padded to
+        the longest range) | norms (padded to the most buckets)], decoded in one launch through the
+        records (grace_qsgd_decompress_records; bucket_size 128, other sizes copy the records back to
+        flat buffers first)."""
+        K = self.k_ops
+        dev = x.device
+        dt = K.code_dtype(self.codec, self.q)
+        csz = torch.empty(0, dtype=dt).element_size()
+        if self.codec != "qsgd":
+            rec = torch.empty(plan.max_len, dtype=dt, device=dev)
+            codes = rec[:hi - lo]
+            if hi > lo:
+                K.encode_into(self.codec, x, lo, plan.parts[rank], u, seed, self.q, self.bucket, self.variant,
+                              self.deterministic, codes, None)
+            self.last_codes, self.last_norms = codes, None
+            gathered = torch.empty(world * plan.max_len, dtype=dt, device=dev)
+            dist.all_gather_into_tensor(gathered, rec, group=self.group)
+            return K.decode(self.codec, gathered[:plan.n], None, list(plan.sizes), plan.n, self.q, self.bucket,
+                            self.variant)
         cb = (plan.max_len * csz + 15) // 16 * 16       # 16-B aligned norms and records
-        nb = (plan.max_units * 4 + 15) // 16 * 16 if self.codec == "qsgd" else 0
-        rec = torch.zeros(cb + nb, dtype=torch.uint8, device=x.device)
-        rec[:codes.numel() * csz].copy_(codes.view(torch.uint8).reshape(-1))
-        if nb:
-            rec[cb:cb + norms.numel() * 4].copy_(norms.view(torch.uint8))
-        gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=x.device)
+        nb = (plan.max_units * 4 + 15) // 16 * 16
+        rec = torch.empty(cb + nb, dtype=torch.uint8, device=dev)
+        u0, u1 = plan.units[rank]
+        codes = rec[:(hi - lo) * csz].view(dt)
+        norms = rec[cb:cb + (u1 - u0) * 4].view(torch.float32)
+        if hi > lo:
+            K.encode_into(self.codec, x, lo, plan.parts[rank], u, seed, self.q, self.bucket, self.variant,
+                          self.deterministic, codes, norms)
+        self.last_codes, self.last_norms = codes, norms
+        gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=dev)
         dist.all_gather_into_tensor(gathered, rec, group=self.group)
+        if self.bucket == 128:
+            key = ("lo", plan.sizes, world, str(dev))
+            rank_lo = self._plans.get(key)
+            if rank_lo is None:
+                rank_lo = self._plans[key] = torch.tensor([a for a, _ in plan.ranges], dtype=torch.int64, device=dev)
+            return K.decode_records(gathered, rec.numel(), cb, plan, rank_lo, self.q, self.variant)
         g = gathered.view(world, -1)
-        # the padded records back to one flat code buffer (and one norm buffer): one batched copy each
-        full = torch.cat([g[w, :(b - a) * csz] for w, (a, b) in enumerate(plan.ranges) if b > a]).view(codes.dtype)
-        allnorms = None
-        if self.codec == "qsgd":
-            allnorms = torch.cat([g[w, cb:cb + (u1 - u0) * 4] for w, (u0, u1) in enumerate(plan.units)
-                                  if u1 > u0]).view(torch.float32)
+        full = torch.cat([g[w, :(b - a) * csz] for w, (a, b) in enumerate(plan.ranges) if b > a]).view(dt)
+        allnorms = torch.cat([g[w, cb:cb + (b - a) * 4] for w, (a, b) in enumerate(plan.units) if b > a]).view(torch.float32)
         return K.decode(self.codec, full, allnorms, list(plan.sizes), plan.n, self.q, self.bucket, self.variant)
 
     def _step_bits(self, x, plan, world, rank, lo, hi):

@@ -17,8 +17,9 @@ Per step on rank r (grace_terngrad_shard_*, grace_terngrad_scalars):
      codes equal the single-GPU ones for the same seed, or an injected u); grace_terngrad_scalars:
      every tensor's scalar, derived on every rank -- nothing but the slots travels before the codes;
   4. dense="replicated": ONE all_gather of the codes and the decode of the whole bucket on every
-     rank; dense="shard": the decode of this rank's elements only, no second collective
-     (reduce-scatter semantics).
+     rank straight from the gathered per-rank records (grace_terngrad_decompress_records: no unpack
+     pass, no copy into a flat code buffer); dense="shard": the decode of this rank's elements only,
+     no second collective (reduce-scatter semantics).
 Wire of step 4 (``wire``): "packed2" (default) moves the codes as code + 1 in the 2-bit planar byte
 layout of the reference's packing (grace_dl/tensorflow/compressor/packing.py:4-29, grace_tern_pack /
 grace_tern_unpack): a quarter of the int8 bytes over xGMI, unpacked straight into the flat code
@@ -65,6 +66,10 @@ class NativeTernKernels:
 
     def decode(self, codes, scalars, sizes, n):
         return ops.terngrad_decompress(codes, scalars, n, sizes)
+
+    def decode_records(self, records, rec_bytes, world, rank_lo, packed, scalars, sizes, n):
+        """the whole bucket straight from the W gathered records, one launch (no unpack, no copy)"""
+        return ops.terngrad_decompress_records(records, rec_bytes, world, rank_lo, packed, scalars, n, sizes)
 
     def pack_bytes(self, n):
         return int(_lib.query("grace_pack2_bytes", int(n)))
@@ -186,22 +191,22 @@ class ShardedTernGrad:
             return K.decode(codes, scalars[s0:s1 + 1], own, hi - lo)
         if world == 1:
             return K.decode(codes, scalars, plan.sizes, plan.n)
+        # every rank's element range boundaries, for the decode through the records
+        lkey = ("lo", plan.sizes, world, str(dev))
+        rank_lo = self._slots.get(lkey)
+        if rank_lo is None:
+            rank_lo = self._slots[lkey] = torch.tensor([a for a, _ in plan.ranges] + [plan.n], dtype=torch.int64,
+                                                       device=dev)
         if packed:
-            full = torch.empty(plan.n, dtype=torch.int8, device=dev)
-            # every rank's block padded to the longest range's packed size (16-B multiples)
+            # every rank's block padded to the longest range's packed size (16-B multiples); the
+            # padding is never read
             pb = (K.pack_bytes(plan.max_len) + 15) // 16 * 16
             send = torch.empty(pb, dtype=torch.uint8, device=dev)
             if hi > lo:
                 K.pack(codes, send)
             gathered = torch.empty(world * pb, dtype=torch.uint8, device=dev)
             dist.all_gather_into_tensor(gathered, send, group=self.group)
-            for w, (a, b) in enumerate(plan.ranges):   # each block unpacked into its range
-                if b > a:
-                    K.unpack(gathered[w * pb:(w + 1) * pb], b - a, full[a:b])
-            return K.decode(full, scalars, plan.sizes, plan.n)
+            return K.decode_records(gathered, pb, world, rank_lo, True, scalars, plan.sizes, plan.n)
         gathered = torch.empty(world * plan.max_len, dtype=torch.int8, device=dev)
         dist.all_gather_into_tensor(gathered, sendc, group=self.group)
-        # the padded blocks back to one flat code buffer: one batched copy
-        full = torch.cat([gathered[w * plan.max_len:w * plan.max_len + (b - a)]
-                          for w, (a, b) in enumerate(plan.ranges) if b > a])
-        return K.decode(full, scalars, plan.sizes, plan.n)
+        return K.decode_records(gathered, plan.max_len, world, rank_lo, False, scalars, plan.sizes, plan.n)

@@ -232,9 +232,18 @@ def sum_rank_order(tensors):
 
 
 # ----------------------------------------------------------------------------- sign family
-def sign_encode(x):
+def _out_buf(out, n, dtype, device, what):
+    """a caller-provided output (a view into a send record) or a new tensor"""
+    if out is None:
+        return torch.empty(n, dtype=dtype, device=device)
+    if out.dtype != dtype or out.numel() != n or not out.is_contiguous() or out.device != device:
+        raise ValueError(f"{what}: out must be a contiguous {dtype} tensor of {n} elements on {device}")
+    return out
+
+
+def sign_encode(x, out=None):
     x = dev_f32(x)
-    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    codes = _out_buf(out, x.numel(), torch.uint8, x.device, "sign_encode")
     _lib.call("grace_sign_encode", _p(x), _p(codes), x.numel(), _stream())
     return codes
 
@@ -605,15 +614,18 @@ def _opt(t):
 
 
 # ----------------------------------------------------------------------------- QSGD
-def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, seed=0, norms_in=None, xoff=0):
+def qsgd_compress(x, quantum_num, bucket_size, sizes=None, variant=0, u=None, seed=0, norms_in=None, xoff=0,
+                  codes_out=None, norms_out=None):
     """x: flat f32 device buffer (one tensor, or `sizes` segments back to back).  xoff: the element
     of a larger bucket x[0] is (a shard starting on a bucket boundary): the device generator draws
-    by that bucket's element index (grace_qsgd_compress_at)."""
+    by that bucket's element index (grace_qsgd_compress_at).  codes_out / norms_out: write there
+    (views into a send record) instead of new tensors."""
     x = dev_f32(x)
     sizes = [x.numel()] if sizes is None else sizes
     seg_off, bkt_off, nb = seg_tables(sizes, bucket_size, x.device)
-    codes = torch.empty(x.numel(), dtype=torch.int8 if quantum_num < 128 else torch.float16, device=x.device)
-    norms = torch.empty(nb, dtype=F32, device=x.device)
+    codes = _out_buf(codes_out, x.numel(), torch.int8 if quantum_num < 128 else torch.float16, x.device,
+                     "qsgd_compress")
+    norms = _out_buf(norms_out, nb, F32, x.device, "qsgd_compress norms")
     _lib.call("grace_qsgd_compress_at", _p(x), int(xoff), _p(seg_off), _p(bkt_off), len(sizes), nb, int(quantum_num),
               int(bucket_size), int(variant), _opt(u), int(seed) & (2 ** 64 - 1), _opt(norms_in), _p(norms),
               _p(codes), _stream())
@@ -645,6 +657,21 @@ def qsgd_decompress(codes, norms, quantum_num, bucket_size, n, sizes=None, varia
     _lib.call("grace_qsgd_decompress", _p(codes), _p(norms), n, nb, int(world), _p(seg_off), _p(bkt_off),
               len(sizes), n, int(quantum_num), int(bucket_size), int(variant), 1 if aggregate else 0,
               float(divisor), _p(out), _stream())
+    return out
+
+
+def qsgd_decompress_records(records, rec_bytes, norm_off, world, units_per_rank, rank_lo, quantum_num, n, sizes=None,
+                            variant=0):
+    """Sharded QSGD's replicated decode (bucket 128) straight from the W gathered per-rank records
+    (grace_qsgd_decompress_records): rank w's codes from byte w * rec_bytes, its bucket norms from
+    byte w * rec_bytes + norm_off; rank_lo: device int64[W], each rank's first element."""
+    records = require_dev(records)
+    sizes = [n] if sizes is None else sizes
+    seg_off, bkt_off, _ = seg_tables(sizes, 128, records.device)
+    out = torch.empty(n, dtype=F32, device=records.device)
+    _lib.call("grace_qsgd_decompress_records", _p(records), int(rec_bytes), int(norm_off), int(world),
+              int(units_per_rank), _p(rank_lo), _p(seg_off), _p(bkt_off), len(sizes), int(n), int(quantum_num),
+              int(variant), _p(out), _stream())
     return out
 
 
@@ -695,6 +722,20 @@ def terngrad_step_w1(x, sizes=None, clip=None, u=None, seed=0):
     return out
 
 
+def terngrad_decompress_records(records, rec_bytes, world, rank_lo, packed, scalars, n, sizes=None):
+    """Sharded TernGrad's replicated decode straight from the W gathered per-rank records
+    (grace_terngrad_decompress_records): int8 codes, or 2-bit planar packed (packed=True);
+    rank_lo: device int64[W + 1], each rank's element range boundaries."""
+    records, scalars = require_dev(records), require_dev(scalars)
+    sizes = [n] if sizes is None else sizes
+    unit = _lib.query("grace_terngrad_unit")
+    seg_off, _, _ = seg_tables(sizes, unit, records.device)
+    out = torch.empty(n, dtype=F32, device=records.device)
+    _lib.call("grace_terngrad_decompress_records", _p(records), int(rec_bytes), int(world), _p(rank_lo),
+              1 if packed else 0, _p(scalars), _p(seg_off), len(sizes), int(n), _p(out), _stream())
+    return out
+
+
 def terngrad_decompress(codes, scalars, n, sizes=None, world=1, aggregate=False, divisor=1.0):
     codes, scalars = require_dev(codes), require_dev(scalars)
     sizes = [n] if sizes is None else sizes
@@ -707,19 +748,19 @@ def terngrad_decompress(codes, scalars, n, sizes=None, world=1, aggregate=False,
 
 
 # ----------------------------------------------------------------------------- natural / fp16
-def natural_compress(x, rand_int=None, seed=0, xoff=0):
+def natural_compress(x, rand_int=None, seed=0, xoff=0, out=None):
     """xoff (a multiple of 4): the element of a larger bucket x[0] is, for the device generator."""
     x = dev_f32(x)
-    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    codes = _out_buf(out, x.numel(), torch.uint8, x.device, "natural_compress")
     _lib.call("grace_natural_compress_at", _p(x), int(xoff), x.numel(), _opt(rand_int), int(seed) & (2 ** 64 - 1),
               _p(codes), _stream())
     return codes
 
 
-def cnat_compress(x, rand=None, deterministic=False, seed=0, xoff=0):
+def cnat_compress(x, rand=None, deterministic=False, seed=0, xoff=0, out=None):
     """xoff (a multiple of 4): the element of a larger bucket x[0] is, for the device generator."""
     x = dev_f32(x)
-    codes = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    codes = _out_buf(out, x.numel(), torch.uint8, x.device, "cnat_compress")
     _lib.call("grace_cnat_compress_at", _p(x), int(xoff), x.numel(), _opt(rand), 1 if deterministic else 0,
               int(seed) & (2 ** 64 - 1), _p(codes), _stream())
     return codes
@@ -733,9 +774,9 @@ def natural_decompress(codes, n, flavour, world=1, aggregate=False, divisor=1.0)
     return out
 
 
-def fp16_compress(x):
+def fp16_compress(x, out=None):
     x = dev_f32(x)
-    h = torch.empty(x.numel(), dtype=torch.float16, device=x.device)
+    h = _out_buf(out, x.numel(), torch.float16, x.device, "fp16_compress")
     _lib.call("grace_fp16_compress", _p(x), _p(h), x.numel(), _stream())
     return h
 
@@ -921,10 +962,11 @@ def powersgd_p(M2d, q):
     return P
 
 
-def powersgd_p_draw(M2d, r, seed):
-    """P = M q with q = ops.normal((m, r), seed), drawn inside the contraction (no q buffer)."""
+def powersgd_p_draw(M2d, r, seed, out=None):
+    """P = M q with q = ops.normal((m, r), seed), drawn inside the contraction (no q buffer);
+    out: an n x r f32 view to write P into (a send record)."""
     n, m = M2d.shape
-    P = torch.empty(n, r, dtype=F32, device=M2d.device)
+    P = _out_buf(out.reshape(-1) if out is not None else None, n * r, F32, M2d.device, "powersgd_p_draw").view(n, r)
     ws = workspace("powersgd", _lib.query("grace_powersgd_workspace_bytes", n, m, r), M2d.device)
     _lib.call("grace_powersgd_p_draw", _p(M2d), n, m, int(seed) & (2 ** 64 - 1), int(r), _p(P), _p(ws), _stream())
     return P

@@ -262,6 +262,16 @@ grace_status_t grace_qsgd_decompress(const void* codes, const float* norms, int6
                                      const int64_t* bkt_off, int32_t nseg, int64_t n, int32_t quantum_num,
                                      int32_t bucket_size, int32_t variant, int32_t aggregate, float divisor,
                                      float* out, void* stream);
+/* Sharded QSGD (grace_amd/dist/sharded_quant.py, bucket_size 128): the whole bucket decoded straight
+ * from the W gathered per-rank records (no copy into flat code / norm buffers).  Rank w holds the
+ * buckets [w U, (w + 1) U) (U = units_per_rank) and the elements from rank_lo[w] (device int64[W]);
+ * its record starts at records + w * rec_bytes with the codes of its elements from byte 0 and the
+ * f32 norms of its buckets from byte norm_off_bytes (both 16-B multiples).  Same arithmetic as
+ * grace_qsgd_decompress at world 1. */
+grace_status_t grace_qsgd_decompress_records(const void* records, int64_t rec_bytes, int64_t norm_off_bytes,
+                                             int32_t world, int64_t units_per_rank, const int64_t* rank_lo,
+                                             const int64_t* seg_off, const int64_t* bkt_off, int32_t nseg, int64_t n,
+                                             int32_t quantum_num, int32_t variant, float* out, void* stream);
 /* QSGD, Horovod flavour (grace_dl/torch/compressor/qsgd.py:12-31): ONE norm over the whole tensor
  * (tensor.norm(); no buckets), same codeword rule.  norm_out[1] f32 (f64 accumulation), norm_in
  * (optional) injects it; ws = grace_qsgd_global_workspace_bytes().  Decode with
@@ -294,6 +304,14 @@ grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, co
  * every segment's scale reduced exactly as the single-GPU encoder (bit-identical codes), and
  * grace_terngrad_scalars derives every segment's scalar the same way (nothing but the slots
  * travels before the codes). */
+/* Sharded TernGrad's replicated decode straight from the W gathered records: rank w's codes of the
+ * elements [rank_lo[w], rank_lo[w + 1]) (device int64[W + 1], W <= 64) at records + w * rec_bytes,
+ * int8 (packed = 0) or code + 1 in the 2-bit planar layout of grace_tern_pack (packed = 1);
+ * out = code * scalars[segment], as grace_terngrad_decompress at world 1.  16-B aligned out. */
+grace_status_t grace_terngrad_decompress_records(const void* records, int64_t rec_bytes, int32_t world,
+                                                 const int64_t* rank_lo, int32_t packed, const float* scalars,
+                                                 const int64_t* seg_off, int32_t nseg, int64_t n, float* out,
+                                                 void* stream);
 int32_t grace_terngrad_slot_bytes(void);
 grace_status_t grace_terngrad_shard_stats(const float* x, int64_t xoff, const int64_t* seg_off,
                                           const int64_t* unit_off, int32_t nseg, int64_t unit0, int64_t nunits_local,

@@ -78,3 +78,14 @@ def test_sharded_powersgd_matches_single_gpu(world, n, m, dense, memory):
         if dense == "replicated":   # every rank forms the identical result
             for o in outs[1:]:
                 assert np.array_equal(o[f"out{s}"], outs[0][f"out{s}"])
+        if not memory:
+            # against the reference restatement directly (oracle/grace_oracle.py: powersgd.py:45-52
+            # with MGS), fed the same q the engine draws on the device for this step
+            from grace_amd import ops
+            from oracle import grace_oracle as O
+            r = min(n, m, 4)
+            q = ops.normal((m, r), ops.step_seed("powersgd-q", NAME, s + 1), torch.device("cuda", 0)).cpu().numpy()
+            ref = O.powersgd_decode(*O.powersgd_compress(_mat(n, m, s), q))
+            scale = float(np.abs(ref).max())
+            for gi in got:
+                assert float(np.abs(gi - ref).max()) <= tol * scale, (s, "sharded vs oracle")

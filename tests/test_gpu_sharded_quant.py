@@ -71,6 +71,30 @@ def _single(codec, x, s, det, q, sizes=SIZES):
     return ops.qsgd_decompress(codes, norms, q, BUCKET, n, sizes=sizes)
 
 
+def _oracle(codec, xv, s, det, q, sizes=SIZES):
+    """The reference restatement (oracle/grace_oracle.py) on the whole bucket, where it is fully
+    determined: the deterministic codecs, and the stochastic ones with the injected stream (QSGD
+    tensor by tensor, every bucket counted from its tensor's start); None otherwise."""
+    from oracle import grace_oracle as O
+    codec = codec.partition(":")[0]
+    if codec == "sign":
+        return O.sign_decode(O.sign_encode(xv))
+    if codec == "fp16":
+        return O.fp16_decode(O.fp16_compress(xv))
+    if codec == "natural":
+        return O.natural_decode(O.natural_compress(xv, s)) if s is not None else None
+    if codec == "cnat":
+        return O.cnat_decode(O.cnat_compress(xv, None if det else s)) if (det or s is not None) else None
+    if s is None or q >= 128:
+        return None
+    out, a = [], 0
+    for n in sizes:
+        c, nm = O.qsgd_compress(xv[a:a + n], s[a:a + n], q, BUCKET)
+        out.append(O.qsgd_decode(c, nm, q, BUCKET, n))
+        a += n
+    return np.concatenate(out)
+
+
 def _bits(a, b):
     return np.array_equal(np.asarray(a, F32).view(np.uint32), np.asarray(b, F32).view(np.uint32))
 
@@ -98,6 +122,12 @@ def test_sharded_quant_native_matches_single_gpu(world, codec, use_u, det, q, de
     for step in range(2):
         x = torch.from_numpy(flat * F32(step + 1)).cuda()
         exp = _single(codec, x, torch.from_numpy(s).cuda() if s is not None else None, det, q).cpu().numpy()
+        ref = _oracle(codec, flat * F32(step + 1), s, det, q)
+        if ref is not None:   # the native result against the reference restatement directly too
+            assert _bits(exp, np.asarray(ref, F32)), (step, codec, "single-GPU codec vs oracle")
+            for o in outs:
+                if dense == "replicated":
+                    assert _bits(o[f"out{step}"], np.asarray(ref, F32)), (step, codec, "sharded vs oracle")
         if dense == "shard":
             assert _bits(np.concatenate([o[f"out{step}"] for o in outs]), exp), (step, codec)
         else:

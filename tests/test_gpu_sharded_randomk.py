@@ -65,3 +65,19 @@ def test_sharded_randomk_native_matches_single_gpu(world, n, dense, rng):
         else:
             for o in outs:
                 assert _bits(o[f"out{s}"], exp), s
+    if rng == "torch_cpu":
+        # the torch-CPU stream is the reference's own: the reference restatement directly
+        # (randomk.py:11-40 with ResidualMemory, residual.py:10-20), step by step
+        from oracle import grace_oracle as O
+        r = None
+        for s in range(3):
+            g = _grad(s, n)
+            t = g if r is None else (r + g).astype(F32)
+            idx, _ = O.randomk_indices(NAME, s, n, RATIO)
+            d = O.randomk_decode(t[idx], idx, n)
+            r = (t - d).astype(F32)
+            assert _bits(np.concatenate([o[f"res{s}"] for o in outs]), r), (s, "residual vs oracle")
+            out = (F32(0) + d).astype(F32)
+            if dense == "replicated":
+                for o in outs:
+                    assert _bits(o[f"out{s}"], out), (s, "sharded vs oracle")

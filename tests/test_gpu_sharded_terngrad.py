@@ -73,6 +73,22 @@ def test_sharded_terngrad_native_matches_single_gpu(world, mode):
         dec = ops.terngrad_decompress(codes, scalars, flat.size, SIZES).cpu().numpy()
         codes, scalars = codes.cpu().numpy(), scalars.cpu().numpy()
         assert np.array_equal(np.concatenate([o[f"codes{step}"] for o in outs]), codes), (step, mode)
+        if use_u and use_clip:
+            # fully determined: the reference restatement tensor by tensor, directly
+            from oracle import grace_oracle as O
+            xv, a = flat * F32(step + 1), 0
+            oc, od, osc = [], [], []
+            for i, n in enumerate(SIZES):
+                c, sc = O.terngrad_compress(xv[a:a + n], u[a:a + n], clip[i])
+                oc.append(c)
+                od.append(O.terngrad_decode(c, sc))
+                osc.append(sc[0])
+                a += n
+            assert np.array_equal(np.concatenate([o[f"codes{step}"] for o in outs]), np.concatenate(oc)), step
+            for o in outs:
+                assert _bits(o[f"scalars{step}"], np.array(osc, F32)), step
+                if dense == "replicated":
+                    assert _bits(o[f"out{step}"], np.concatenate(od)), step
         for o in outs:
             assert _bits(o[f"scalars{step}"], scalars), (step, mode)
         if dense == "shard":

@@ -26,8 +26,12 @@ def _q(seed, m, r):
 
 
 class OraclePowerSGDKernels:
-    def p_draw(self, Mi, r, seed):
-        return Mi @ _q(seed, Mi.shape[1], r)
+    def p_draw(self, Mi, r, seed, out=None):
+        P = Mi @ _q(seed, Mi.shape[1], r)
+        if out is not None:
+            out.copy_(P)
+            return out
+        return P
 
     def orthogonalize_(self, P):
         P.copy_(torch.from_numpy(O.orthogonalize(P.numpy())))

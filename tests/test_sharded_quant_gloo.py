@@ -47,6 +47,25 @@ class OracleQuantKernels:
             a += s
         return torch.from_numpy(np.concatenate(codes)), torch.from_numpy(np.concatenate(norms).astype(F32))
 
+    def encode_into(self, codec, x, xoff, sizes, u, seed, q, bucket, variant, deterministic, codes, norms):
+        c, nm = self.encode(codec, x, xoff, sizes, u, seed, q, bucket, variant, deterministic)
+        codes.copy_(c.view(codes.dtype))
+        if norms is not None:
+            norms.copy_(nm)
+
+    def decode_records(self, records, rec_bytes, norm_off, plan, rank_lo, q, variant):
+        """the product's record layout read back in numpy: rank w's codes from w * rec_bytes, its
+        bucket norms from w * rec_bytes + norm_off"""
+        rec = records.numpy().view(np.uint8)
+        cdt = np.float16 if q >= 128 else np.int8
+        codes, norms = [], []
+        for w, ((a, b), (u0, u1)) in enumerate(zip(plan.ranges, plan.units)):
+            blk = rec[w * rec_bytes:(w + 1) * rec_bytes]
+            codes.append(blk[:(b - a) * np.dtype(cdt).itemsize].view(cdt))
+            norms.append(blk[norm_off:norm_off + (u1 - u0) * 4].view(F32))
+        return self.decode("qsgd", torch.from_numpy(np.concatenate(codes)), torch.from_numpy(np.concatenate(norms)),
+                           list(plan.sizes), plan.n, q, 128, variant)
+
     def encode_bits(self, x, words):
         b = O.sign_encode(x.numpy()).astype(np.uint8)
         by = np.zeros(4 * words.numel(), np.uint8)

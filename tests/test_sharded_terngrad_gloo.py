@@ -88,6 +88,23 @@ class OracleTernKernels:
         sc = np.repeat(scalars.numpy().astype(F32), sizes)
         return torch.from_numpy((codes.numpy().astype(F32) * sc).astype(F32))
 
+    def decode_records(self, records, rec_bytes, world, rank_lo, packed, scalars, sizes, n):
+        """the product's record layout read back in numpy (each rank's block at w * rec_bytes)"""
+        lo = rank_lo.numpy()
+        rec = records.numpy().view(np.uint8)
+        parts = []
+        for w in range(world):
+            L = int(lo[w + 1] - lo[w])
+            if L == 0:
+                continue
+            blk = rec[w * rec_bytes:(w + 1) * rec_bytes]
+            if packed:
+                parts.append(O.pack2_decode(blk[:self.pack_bytes(L)], L) - 1)
+            else:
+                parts.append(blk[:L].view(np.int8).astype(np.int64))
+        codes = torch.from_numpy(np.concatenate(parts).astype(np.int8))
+        return self.decode(codes, scalars, sizes, n)
+
     def pack_bytes(self, n):
         return n // 4 + 1   # packing.py pads with range(0, 4 - n % 4)
 

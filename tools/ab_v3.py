@@ -71,7 +71,8 @@ def step(i, L, ws, st, mode, s):
         st.res[j], st.res2[j] = st.res2[j], st.res[j]
 
 
-modes = ["nomem_rec", "nomem_dense", "fused", "swap"]
+import os
+modes = os.environ.get("AB_MODES", "nomem_rec,nomem_dense,fused,swap").split(",")
 # bit-exactness across builds: 4 steps of every mode from the same start
 ref = {}
 for i, L in enumerate(libs):

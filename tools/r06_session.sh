@@ -39,6 +39,21 @@ for s in "$@"; do
             -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
           python3 tools/prof_steady.py $O/prof_topk --last 20 --out $O/prof_topk_steady.json; echo "steady rc=$?" ;;
     bench) run bench 300 python3 bench.py ;;
+    shardcodecs) run shard_codecs 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard_codecs -o run \
+                   -- python3 tools/exp_shard_codecs.py 8
+                 python3 tools/shard_codecs_summary.py $O/shard_codecs 8 > $O/shard_codecs_summary.txt; echo "summary rc=$?"
+                 cat $O/shard_codecs_summary.txt ;;
+    shardtests) run shardtests 900 python3 -u -m pytest tests/test_gpu_sharded_quant.py tests/test_gpu_sharded_terngrad.py \
+        tests/test_gpu_sharded_powersgd.py tests/test_gpu_sharded_randomk.py -q -x --timeout 300 --timeout-method thread ;;
+    abnv) AB_MODES=nomem_rec,nomem_dense run ab_nv 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+            grace_amd/lib/libgrace_hip_nv16.so grace_amd/lib/libgrace_hip_nv24.so grace_amd/lib/libgrace_hip_nv40.so \
+            grace_amd/lib/libgrace_hip_nv48.so grace_amd/lib/libgrace_hip_nv64.so ;;
+    abnv2) AB_MODES=nomem_rec,nomem_dense run ab_nv2 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_nv64.so \
+            grace_amd/lib/libgrace_hip_nv80.so grace_amd/lib/libgrace_hip_nv96.so grace_amd/lib/libgrace_hip_nv128.so ;;
+    abvec) AB_MODES=fused run ab_vec 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+            grace_amd/lib/libgrace_hip_vec16.so grace_amd/lib/libgrace_hip_vec20.so grace_amd/lib/libgrace_hip_vec24.so ;;
+    ab12b) AB_MODES=swap run ab_12b 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+            grace_amd/lib/libgrace_hip_v12b28.so grace_amd/lib/libgrace_hip_v12b32.so grace_amd/lib/libgrace_hip_v12b40.so ;;
     abv3) run ab_v3 300 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_main_v2.so grace_amd/lib/libgrace_hip.so ;;
     topktests) run topktests 900 python3 -u -m pytest tests/test_gpu_topk.py tests/test_gpu_topk_recycle.py \
         tests/test_gpu_topk_carry.py tests/test_gpu_harness.py tests/test_gpu_sparse.py -q -x --timeout 300 --timeout-method thread ;;
