@@ -595,7 +595,11 @@ def bench_topk_nomem(args, world, rank, dev):
                         "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
                         "step_algorithmic_bytes": step_bytes, "kernel": "topk_main",
                         "kernel_avg_us": round(main_avg_ms * 1e3, 2),
-                        "kernel_frac": round(main_bytes / (main_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                        "kernel_frac": round(main_bytes / (main_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        # BASELINE.md section 4's definition of this row (>= 70 % target): 8n + 16k
+                        # per step whatever the output mode
+                        "baseline_bytes": 8 * n + 16 * k,
+                        "frac_of_baseline_bytes": round((8 * n + 16 * k) / t / 1e9 / HBM_PEAK_GBS, 4)}
     return line
 
 

@@ -1629,39 +1629,82 @@ __global__ __launch_bounds__(kQBlock) void tern_decode_records_kernel(const uint
   __shared__ SegTables tab;
   __shared__ int64_t rlo[kRecRanksMax + 1];
   for (int i = threadIdx.x; i <= world; i += blockDim.x) rlo[i] = rank_lo[i];
-  const SegView sv = stage_tables(tab, seg_off, nullptr, nseg);
+  // the segment table in LDS only (nseg <= kSegLds, checked at launch): a SegView may point to global
+  // memory, so its reads compile to flat loads with a vmcnt(0) lgkmcnt(0) wait in every table walk
+  for (int i = threadIdx.x; i <= nseg; i += blockDim.x) tab.seg[i] = seg_off[i];
   __syncthreads();
-  int w = 0, s = 0;
-  for (int64_t e = 4 * ((int64_t)blockIdx.x * kQBlock + threadIdx.x); e < n; e += 4 * (int64_t)gridDim.x * kQBlock) {
-    while (w + 1 < world && rlo[w + 1] <= e) ++w;   // e grows: the rank and segment only advance
-    s = seg_advance(sv.seg, nseg, s, e);
-    const uint32_t i = (uint32_t)(e - rlo[w]), L = (uint32_t)(rlo[w + 1] - rlo[w]);
-    const uint8_t* r = rec + w * rec_bytes;
-    if (e + 3 < n && e + 3 < rlo[w + 1] && e + 3 < sv.seg[s + 1]) {
-      float c[4];
-      if (packed) {
-        const uint32_t Q = (L + (4u - L % 4u)) / 4u, pl = i / Q, j = i - pl * Q;
-        if (j + 3u < Q) {   // the quad's four codes in one plane: four adjacent bytes
+  const int64_t* sg = tab.seg;
+  // a contiguous range per workgroup, so that a thread's rank and segment only step forward a little
+  // (a grid-stride walk jumped over whole segments: a linear segment walk of up to nseg per quad)
+  int64_t lo, hi;
+  block_range(n, 4 * kQBlock, lo, hi);
+  const int64_t e0 = lo + 4 * threadIdx.x;
+  int w = 0;
+  while (w + 1 < world && rlo[w + 1] <= e0) ++w;
+  int s = lo < hi ? find_seg(sg, nseg, e0 < hi ? e0 : lo) : 0;
+  // the element's place in its rank's block: plane pl, byte j (packed: i = pl Q + j), advanced
+  // incrementally -- one division per rank a thread enters, not one per quad
+  int wc = -1;
+  uint32_t L = 0, Q = 1, pl = 0, j = 0;
+  const uint32_t lim = (uint32_t)min(rec_bytes, (int64_t)0xFFFFFFFF);
+  constexpr int kU = 4;   // quads per thread per round: every load issued before any is used
+  const uint32_t wlast = lim / 4u - 1u;   // the record's last dword (rec_bytes: a 16-B multiple)
+  for (int64_t eb = e0; eb < hi; eb += 4 * kQBlock * kU) {
+    uint32_t w0[kU], w1[kU], jb[kU], plu[kU];
+    float sc[kU];
+    bool fast[kU];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) c[t] = (float)((int)((r[j + t] >> (2u * pl)) & 3u) - 1);
+    for (int u = 0; u < kU; ++u) {
+      const int64_t e = eb + (int64_t)u * 4 * kQBlock;
+      const bool in = e < hi;
+      if (in) {
+        while (w + 1 < world && rlo[w + 1] <= e) ++w;   // e grows: the rank and segment only advance
+        s = seg_advance(sg, nseg, s, e);
+        const uint32_t i = (uint32_t)(e - rlo[w]);
+        if (w != wc) {
+          wc = w;
+          L = (uint32_t)(rlo[w + 1] - rlo[w]);
+          Q = packed ? (L + (4u - L % 4u)) / 4u : 0xFFFFFFFFu;
+          pl = packed ? i / Q : 0u;
+          j = i - pl * (packed ? Q : 0u);
         } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) c[t] = tern_rec_code(r, i + t, L, 1);
+          j = packed ? j + 4u * kQBlock : i;
+          while (j >= Q) { j -= Q; ++pl; }
         }
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) c[t] = (float)(int8_t)r[i + t];
       }
-      const float sc = scalars[s];
-      __builtin_nontemporal_store(f4v{c[0] * sc, c[1] * sc, c[2] * sc, c[3] * sc}, reinterpret_cast<f4v*>(out + e));
-    } else {
-      // the quad crosses the bucket's end, a rank's range or a segment: element by element
-      for (int64_t x = e; x < e + 4 && x < n; ++x) {
-        int wx = 0;
-        while (wx + 1 < world && rlo[wx + 1] <= x) ++wx;
-        const int sx = find_seg(sv.seg, nseg, x);
-        out[x] = tern_rec_code(rec + wx * rec_bytes, (uint32_t)(x - rlo[wx]), (uint32_t)(rlo[wx + 1] - rlo[wx]), packed) *
-                 scalars[sx];
+      fast[u] = in && e + 3 < hi && e + 3 < rlo[w + 1] && e + 3 < sg[s + 1] && j + 3u < Q;
+      jb[u] = fast[u] ? j : 0u;
+      plu[u] = pl;
+      // unconditional loads (a load under a branch makes the compiler wait for it at the join):
+      // the two dwords holding bytes [j, j + 3] of the rank's record, and the segment's scalar
+      const uint32_t* rp = reinterpret_cast<const uint32_t*>(rec + w * rec_bytes);
+      w0[u] = rp[jb[u] >> 2];
+      w1[u] = rp[min((jb[u] >> 2) + 1u, wlast)];
+      sc[u] = scalars[s];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t e = eb + (int64_t)u * 4 * kQBlock;
+      if (e >= hi) continue;
+      if (fast[u]) {
+        const uint32_t b = __builtin_amdgcn_alignbyte(w1[u], w0[u], jb[u] & 3u);   // bytes j .. j + 3
+        float c[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t by = (b >> (8 * t)) & 0xFFu;
+          c[t] = packed ? (float)((int)((by >> (2u * plu[u])) & 3u) - 1) : (float)(int8_t)by;
+        }
+        __builtin_nontemporal_store(f4v{c[0] * sc[u], c[1] * sc[u], c[2] * sc[u], c[3] * sc[u]},
+                                    reinterpret_cast<f4v*>(out + e));
+      } else {
+        // the quad crosses the bucket's end, a rank's range, a segment or a plane: element by element
+        for (int64_t x = e; x < e + 4 && x < hi; ++x) {
+          int wx = 0;
+          while (wx + 1 < world && rlo[wx + 1] <= x) ++wx;
+          const int sx = find_seg(sg, nseg, x);
+          out[x] = tern_rec_code(rec + wx * rec_bytes, (uint32_t)(x - rlo[wx]), (uint32_t)(rlo[wx + 1] - rlo[wx]),
+                                 packed) * scalars[sx];
+        }
       }
     }
   }
@@ -2217,10 +2260,12 @@ grace_status_t grace_terngrad_decompress_records(const void* records, int64_t re
                                                  const int64_t* seg_off, int32_t nseg, int64_t n, float* out,
                                                  void* stream) {
   GRACE_REQUIRE(records && rank_lo && scalars && seg_off && out && world >= 1 && world <= kRecRanksMax && nseg >= 1 &&
-                    n >= 0 && n < (int64_t(1) << 31) && rec_bytes >= 0 && (uintptr_t)out % 16 == 0,
-                "grace_terngrad_decompress_records: bad arguments (1 <= world <= 64, n < 2^31, 16-B aligned out)");
+                    nseg <= kSegLds && n >= 0 && n < (int64_t(1) << 31) && rec_bytes >= 16 && rec_bytes % 16 == 0 &&
+                    (uintptr_t)records % 16 == 0 && (uintptr_t)out % 16 == 0,
+                "grace_terngrad_decompress_records: bad arguments (1 <= world <= 64, nseg <= 512, n < 2^31, "
+                "16-B aligned records of a 16-B multiple, 16-B aligned out)");
   if (n == 0) return GRACE_OK;
-  tern_decode_records_kernel<<<stream_grid((n + 3) / 4, kQBlock, 8192), kQBlock, 0, as_stream(stream)>>>(
+  tern_decode_records_kernel<<<stream_grid((n + 15) / 16, kQBlock, 8192), kQBlock, 0, as_stream(stream)>>>(
       reinterpret_cast<const uint8_t*>(records), rec_bytes, world, rank_lo, packed ? 1 : 0, scalars, seg_off, nseg, n,
       out);
   GRACE_CHECK_LAUNCH("grace_terngrad_decompress_records");

@@ -65,6 +65,10 @@ class NativeQuantKernels:
             ops.qsgd_compress(x, q, bucket, sizes=sizes, variant=variant, u=u, seed=seed, xoff=xoff,
                               codes_out=codes, norms_out=norms)
 
+    def seg_max(self):
+        """the most tensors grace_qsgd_decompress_records takes (its segment table sits in LDS)"""
+        return int(_lib.query("grace_qsgd_seg_max"))
+
     def decode_records(self, records, rec_bytes, norm_off, plan, rank_lo, q, variant):
         """QSGD (bucket 128): the whole bucket from the W gathered records in ONE launch
         (grace_qsgd_decompress_records), no copy into flat code / norm buffers"""
@@ -237,7 +241,7 @@ class ShardedQuant:
         self.last_codes, self.last_norms = codes, norms
         gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=dev)
         dist.all_gather_into_tensor(gathered, rec, group=self.group)
-        if self.bucket == 128:
+        if self.bucket == 128 and len(plan.sizes) <= K.seg_max():
             key = ("lo", plan.sizes, world, str(dev))
             rank_lo = self._plans.get(key)
             if rank_lo is None:

@@ -67,6 +67,9 @@ class NativeTernKernels:
     def decode(self, codes, scalars, sizes, n):
         return ops.terngrad_decompress(codes, scalars, n, sizes)
 
+    def seg_max(self):
+        return int(_lib.query("grace_qsgd_seg_max"))
+
     def decode_records(self, records, rec_bytes, world, rank_lo, packed, scalars, sizes, n):
         """the whole bucket straight from the W gathered records, one launch (no unpack, no copy)"""
         return ops.terngrad_decompress_records(records, rec_bytes, world, rank_lo, packed, scalars, n, sizes)
@@ -175,8 +178,9 @@ class ShardedTernGrad:
             dist.all_gather_into_tensor(slots[:world * plan.U], slots[u0:u0 + plan.U].clone(), group=self.group)
         seed = self.seed if seed is None else seed
         packed = self.wire == "packed2"
+        cbytes = (plan.max_len + 15) // 16 * 16   # int8 wire: 16-B aligned records
         if self.dense == "replicated" and world > 1 and not packed:
-            sendc = torch.empty(plan.max_len, dtype=torch.int8, device=dev)
+            sendc = torch.empty(cbytes, dtype=torch.int8, device=dev)
             codes = sendc[:hi - lo]
         else:
             codes = torch.empty(hi - lo, dtype=torch.int8, device=dev)
@@ -197,6 +201,8 @@ class ShardedTernGrad:
         if rank_lo is None:
             rank_lo = self._slots[lkey] = torch.tensor([a for a, _ in plan.ranges] + [plan.n], dtype=torch.int64,
                                                        device=dev)
+        # the decode through the records holds the segment table in LDS: up to seg_max() tensors
+        direct = len(plan.sizes) <= K.seg_max() and world <= 64
         if packed:
             # every rank's block padded to the longest range's packed size (16-B multiples); the
             # padding is never read
@@ -206,7 +212,17 @@ class ShardedTernGrad:
                 K.pack(codes, send)
             gathered = torch.empty(world * pb, dtype=torch.uint8, device=dev)
             dist.all_gather_into_tensor(gathered, send, group=self.group)
-            return K.decode_records(gathered, pb, world, rank_lo, True, scalars, plan.sizes, plan.n)
-        gathered = torch.empty(world * plan.max_len, dtype=torch.int8, device=dev)
+            if direct:
+                return K.decode_records(gathered, pb, world, rank_lo, True, scalars, plan.sizes, plan.n)
+            full = torch.empty(plan.n, dtype=torch.int8, device=dev)
+            for w, (a, b) in enumerate(plan.ranges):   # each block unpacked into its range
+                if b > a:
+                    K.unpack(gathered[w * pb:(w + 1) * pb], b - a, full[a:b])
+            return K.decode(full, scalars, plan.sizes, plan.n)
+        gathered = torch.empty(world * cbytes, dtype=torch.int8, device=dev)
         dist.all_gather_into_tensor(gathered, sendc, group=self.group)
-        return K.decode_records(gathered, plan.max_len, world, rank_lo, False, scalars, plan.sizes, plan.n)
+        if direct:
+            return K.decode_records(gathered, cbytes, world, rank_lo, False, scalars, plan.sizes, plan.n)
+        full = torch.cat([gathered[w * cbytes:w * cbytes + (b - a)]
+                          for w, (a, b) in enumerate(plan.ranges) if b > a])
+        return K.decode(full, scalars, plan.sizes, plan.n)

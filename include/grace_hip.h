@@ -307,7 +307,8 @@ grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, co
 /* Sharded TernGrad's replicated decode straight from the W gathered records: rank w's codes of the
  * elements [rank_lo[w], rank_lo[w + 1]) (device int64[W + 1], W <= 64) at records + w * rec_bytes,
  * int8 (packed = 0) or code + 1 in the 2-bit planar layout of grace_tern_pack (packed = 1);
- * out = code * scalars[segment], as grace_terngrad_decompress at world 1.  16-B aligned out. */
+ * out = code * scalars[segment], as grace_terngrad_decompress at world 1.  16-B aligned records and
+ * out, rec_bytes a 16-B multiple, nseg <= grace_qsgd_seg_max(). */
 grace_status_t grace_terngrad_decompress_records(const void* records, int64_t rec_bytes, int32_t world,
                                                  const int64_t* rank_lo, int32_t packed, const float* scalars,
                                                  const int64_t* seg_off, int32_t nseg, int64_t n, float* out,

@@ -71,10 +71,12 @@ def _single(codec, x, s, det, q, sizes=SIZES):
     return ops.qsgd_decompress(codes, norms, q, BUCKET, n, sizes=sizes)
 
 
-def _oracle(codec, xv, s, det, q, sizes=SIZES):
+def _oracle(codec, xv, s, det, q, sizes=SIZES, norms=None):
     """The reference restatement (oracle/grace_oracle.py) on the whole bucket, where it is fully
     determined: the deterministic codecs, and the stochastic ones with the injected stream (QSGD
-    tensor by tensor, every bucket counted from its tensor's start); None otherwise."""
+    tensor by tensor, every bucket counted from its tensor's start, with the device's bucket norms
+    injected: the parity bar is bit-exact codewords given the reference's u and norm, the norms
+    themselves within 4 ulp of torch's f32 reduction, test_gpu_quant.py); None otherwise."""
     from oracle import grace_oracle as O
     codec = codec.partition(":")[0]
     if codec == "sign":
@@ -87,11 +89,13 @@ def _oracle(codec, xv, s, det, q, sizes=SIZES):
         return O.cnat_decode(O.cnat_compress(xv, None if det else s)) if (det or s is not None) else None
     if s is None or q >= 128:
         return None
-    out, a = [], 0
+    out, a, b = [], 0, 0
     for n in sizes:
-        c, nm = O.qsgd_compress(xv[a:a + n], s[a:a + n], q, BUCKET)
+        nb = -(-n // BUCKET)
+        c, nm = O.qsgd_compress(xv[a:a + n], s[a:a + n], q, BUCKET, norms=norms[b:b + nb])
         out.append(O.qsgd_decode(c, nm, q, BUCKET, n))
         a += n
+        b += nb
     return np.concatenate(out)
 
 
@@ -122,7 +126,11 @@ def test_sharded_quant_native_matches_single_gpu(world, codec, use_u, det, q, de
     for step in range(2):
         x = torch.from_numpy(flat * F32(step + 1)).cuda()
         exp = _single(codec, x, torch.from_numpy(s).cuda() if s is not None else None, det, q).cpu().numpy()
-        ref = _oracle(codec, flat * F32(step + 1), s, det, q)
+        norms = None
+        if codec == "qsgd" and s is not None:
+            from grace_amd import ops
+            norms = ops.qsgd_compress(x, q, BUCKET, sizes=SIZES, u=torch.from_numpy(s).cuda(), seed=13)[1].cpu().numpy()
+        ref = _oracle(codec, flat * F32(step + 1), s, det, q, norms=norms)
         if ref is not None:   # the native result against the reference restatement directly too
             assert _bits(exp, np.asarray(ref, F32)), (step, codec, "single-GPU codec vs oracle")
             for o in outs:

@@ -24,6 +24,9 @@ SIZES = [500, 128, 1, 1234, 96, 257, 3000, 5]
 class OracleQuantKernels:
     """numpy restatement of the codec calls (test infrastructure)."""
 
+    def seg_max(self):
+        return 512
+
     def code_dtype(self, codec, q):
         if codec == "fp16" or (codec == "qsgd" and q >= 128):
             return torch.float16

@@ -27,6 +27,9 @@ class OracleTernKernels:
 
     UNIT = 97
 
+    def seg_max(self):
+        return 512
+
     def unit(self):
         return self.UNIT
 

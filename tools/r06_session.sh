@@ -39,6 +39,17 @@ for s in "$@"; do
             -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
           python3 tools/prof_steady.py $O/prof_topk --last 20 --out $O/prof_topk_steady.json; echo "steady rc=$?" ;;
     bench) run bench 300 python3 bench.py ;;
+    shardlocal) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
+    wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
+    abdec1) run ab_decode1 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so ;;
+    abdec) run ab_decode 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so grace_amd/lib/libgrace_hip_qnb1g8k.so \
+             grace_amd/lib/libgrace_hip_qnb1g32k.so grace_amd/lib/libgrace_hip_qnb2g16k.so ;;
+    psgdab) run psgd_ab 300 python3 tools/ab_psgd.py grace_amd/lib/libgrace_hip_psgd_r04.so \
+              grace_amd/lib/libgrace_hip_psgd_r05.so grace_amd/lib/libgrace_hip.so ;;
+    ternsq) sqpasses sq_tern python3 bench.py --workload terngrad --steps 5 --warmup 2 --no-cpu-baseline
+            run sq_tern_kt 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sq_tern_kt -o run \
+              -- python3 bench.py --workload terngrad --steps 20 --warmup 5 --no-cpu-baseline
+            python3 tools/pmc_sq_summary.py $O/sq_tern > $O/sq_tern_summary.json; echo "sq summary rc=$?" ;;
     shardcodecs) run shard_codecs 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shard_codecs -o run \
                    -- python3 tools/exp_shard_codecs.py 8
                  python3 tools/shard_codecs_summary.py $O/shard_codecs 8 > $O/shard_codecs_summary.txt; echo "summary rc=$?"
