@@ -576,11 +576,13 @@ def bench_topk_nomem(args, world, rank, dev):
     main_ms, launches = ops.timer_collect()
     ops.timer_enable(False)
     recycled = world == 1 and rec.hits - hits0 == args.steps
-    t_unfused = timed(step_unfused, args.steps, args.warmup, world, dev)
+    # (profiling passes skip the comparison: its kernels would mix into the step's per-kernel counters)
+    t_unfused = None if os.environ.get("GRACE_BENCH_NO_UNFUSED") else timed(step_unfused, args.steps, args.warmup, world, dev)
     line = base_line(args, world, elapsed, 4.0 * n,
                      metric="grad-codec GB/s (device-resident encode+decode), 256 MiB fp32 bucket, top-k 1 %, no memory")
     line["config"] = {"workload": "Allgather(TopK 1%, NoneMemory).step on a 256 MiB fp32 bucket (BASELINE.md section 4)",
-                      "numel": n, "k": k, "unfused_ms_per_step": round(t_unfused / args.steps * 1e3, 4)}
+                      "numel": n, "k": k,
+                      "unfused_ms_per_step": round(t_unfused / args.steps * 1e3, 4) if t_unfused else None}
     # 8n + 16k; with the recycled output (each dropped result handed back)
     # the dense write shrinks to the selection: 4n + payload 8k + previous indices 4k + their clear
     # 4k + the new selection 4k
@@ -910,6 +912,11 @@ def bench_cast(args, world, rank, dev):
 
 
 # ------------------------------------------------------------------------------------------ PowerSGD
+def ops_ratio_k(n, ratio):
+    from grace_amd import ops
+    return ops.ratio_k(n, ratio)
+
+
 def bench_sparse(args, world, rank, dev):
     """SURVEY.md 8a rows a6 / a7 on the 256 MiB bucket with ResidualMemory: Allgather(RandomK 1 %)
     and Allgather(Threshold), the threshold at 2.5758 (|x| above it: 1 % of N(0, 1) on the first
@@ -941,10 +948,16 @@ def bench_sparse(args, world, rank, dev):
     if args.workload == "randomk":       # random-k's world-1 step recycles its dropped output
         mode = "recycled" if rec is not None and rec.hits > 0 else "dense"
         line["config"]["output"] = mode
+        if mode == "recycled":
+            # g, r read, r' written (12n); the output: the previous k positions cleared and the new
+            # k written (4 B each), the drawn indices written and read back (8 B each with grouping)
+            k = ops_ratio_k(n, args.ratio)
+            alg = 12.0 * n + 16.0 * k
     traffic, ratio, tsrc = pmc_traffic(args.workload, alg, mode=mode)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg}
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": alg,
+                        "frac_of_16n": round(16.0 * n / t / 1e9 / HBM_PEAK_GBS, 4)}
     return line
 
 
@@ -1031,13 +1044,19 @@ def bench_powersgd(args, world, rank, dev):
                      metric="grad-codec GB/s (device-resident encode+decode), PowerSGD rank 4, 4096x4096")
     line["config"] = {"workload": "Allreduce(PowerSGD rank 4, NoneMemory).step, 4096x4096 fp32 (BASELINE configs[3])",
                       "numel": n * m, "rank": r}
-    traffic, ratio, tsrc = pmc_traffic("powersgd", 12.0 * n * m)
-    line["roofline"] = {"bound": "hbm", "achieved": round(12 * n * m / t / 1e9, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc,
+    # the world-1 one-pass compress reads M once (P and the f64 Qraw partials from the same registers)
+    # and the decode writes P Q^T: 8 B per element, plus the partials written and read back (64-row
+    # slabs x m x r x 8 B); SURVEY.md §8d's 12n (M read twice) is kept as frac_of_survey_bytes
+    moved = 8.0 * n * m + 2.0 * (n // 64) * m * r * 8 if world == 1 else 12.0 * n * m
+    traffic, ratio, tsrc = pmc_traffic("powersgd", moved)
+    line["roofline"] = {"bound": "hbm", "achieved": round(moved / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(moved / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": ratio, "traffic_source": tsrc, "algorithmic_bytes_per_step": moved,
+                        "frac_of_survey_bytes": round(12 * n * m / t / 1e9 / HBM_PEAK_GBS, 4),
                         "mfma_tflops": round(flops / t / 1e12, 3),
                         "mfma_util": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 5),
-                        "note": "12n algorithmic bytes, 6nmr flops (SURVEY.md §8d config 4; AI = 2 flop/B)"}
+                        "note": "frac on the bytes the one-pass step moves (8 B per element + the f64 partials); "
+                                "frac_of_survey_bytes on SURVEY.md §8d config 4's 12n; 6nmr flops (AI = 2 flop/B)"}
     return line
 
 

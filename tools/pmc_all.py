@@ -3,7 +3,7 @@
 wide (16-B per lane) streaming read is tallied at half its bytes (x2); WRITE_SIZE is in KB and
 exact for 16-B-per-lane stores.  Other access widths (the codecs' 4-B code stores, 8-B loads) are
 uncalibrated, so the per-kernel figures are reported raw-corrected and flagged.
-usage: python tools/pmc_all.py OUT_JSON [--last N] [--exclude WL:REGEX] WORKLOAD=FETCH_DIR,WRITE_DIR [...]"""
+usage: python tools/pmc_all.py OUT_JSON [--last N] [--exclude WL:REGEX] [--mode WL=MODE] WORKLOAD=FETCH_DIR,WRITE_DIR [...]"""
 import collections
 import csv
 import json
@@ -42,13 +42,16 @@ def main():
     import re
     res = {"correction": "FETCH_SIZE KB x1024 x2 (gfx950 16-B streaming reads), WRITE_SIZE KB x1024",
            "workloads": {}}
-    args, last, excl = sys.argv[2:], 0, {}
+    args, last, excl, modes = sys.argv[2:], 0, {}, {}
     while args and args[0].startswith("--"):
         if args[0] == "--last":
             last = int(args[1])
         elif args[0] == "--exclude":
             w, rx = args[1].split(":", 1)
             excl[w] = re.compile(rx)
+        elif args[0] == "--mode":   # WL=MODE: the output mode the passes ran in (bench.py checks it)
+            w, m = args[1].split("=", 1)
+            modes[w] = m
         args = args[2:]
     if last:
         res["steady_state"] = f"mean of each kernel's last {last} dispatches"
@@ -72,6 +75,8 @@ def main():
             step += f + w
         res["workloads"][wl] = {"kernels": kern, "hbm_bytes_per_step": round(step),
                                 "source": [fdir, wdir]}
+        if wl in modes:
+            res["workloads"][wl]["mode"] = modes[wl]
     with open(sys.argv[1], "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps({w: v["hbm_bytes_per_step"] for w, v in res["workloads"].items()}))

@@ -29,16 +29,50 @@ sqpasses() {   # $1 tag, rest: the program
 for s in "$@"; do
   case $s in
     scatter) run scatter 120 ./tools/scatter_probe ;;
-    nomemkt) run nomem_kt 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sq_nomem_kt -o run \
+    nomemkt) GRACE_BENCH_NO_UNFUSED=1 run nomem_kt 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sq_nomem_kt -o run \
                -- python3 bench.py --workload topk_nomem --steps 20 --warmup 5 --no-cpu-baseline ;;
-    nomemsq) sqpasses sq_nomem python3 bench.py --workload topk_nomem --steps 5 --warmup 2 --no-cpu-baseline
+    nomemsq) GRACE_BENCH_NO_UNFUSED=1 sqpasses sq_nomem python3 bench.py --workload topk_nomem --steps 5 --warmup 2 --no-cpu-baseline
              python3 tools/pmc_sq_summary.py $O/sq_nomem > $O/sq_nomem_summary.json; echo "sq summary rc=$?" ;;
-    headsq) GRACE_BENCH_NO_PROBE=1 sqpasses sq_head python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-overlap
-            python3 tools/pmc_sq_summary.py $O/sq_head > $O/sq_head_summary.json; echo "sq summary rc=$?" ;;
+    headsq) # the headline's main pass AND its streaming skeleton (the in-bench probe launches), one box
+            tag=sq_head_${BOXTAG:-a}
+            sqpasses $tag python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-overlap
+            run ${tag}_kt 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${tag}_kt -o run \
+              -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
+            python3 tools/pmc_sq_summary.py $O/$tag > $O/${tag}_summary.json; echo "sq summary rc=$?"
+            grep -h '^{' $O/${tag}_kt.log | tail -1 > $O/${tag}_line.json ;;
     prof) GRACE_BENCH_NO_PROBE=1 run prof_topk 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_topk -o run \
             -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-overlap
           python3 tools/prof_steady.py $O/prof_topk --last 20 --out $O/prof_topk_steady.json; echo "steady rc=$?" ;;
     bench) run bench 300 python3 bench.py ;;
+    secondary)
+      : > $O/secondary.jsonl
+      for wl in ${WL:-topk_nomem topk_sharded ddp_segmented sign sign256 qsgd qsgd_step terngrad terngrad_step powersgd randomk threshold dgc natural cnat fp16 sign_bits}; do
+        st=20; case $wl in sign) st=200 ;; esac
+        run "bench_$wl" 300 python3 bench.py --workload $wl --steps $st --no-cpu-baseline
+        grep '^{' "$O/bench_$wl.log" | tail -1 >> $O/secondary.jsonl
+      done ;;
+    pmc) # FETCH_SIZE / WRITE_SIZE passes (one counter per run) of the headline and every secondary
+         # workload -> $O/pmc_topk_main.json and $O/r06_pmc_secondary.json (bench.py reads both from profiles/)
+         export GRACE_BENCH_NO_PROBE=1 GRACE_BENCH_NO_UNFUSED=1
+         for c in FETCH_SIZE WRITE_SIZE; do
+           run pmc_head_$c 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_head_$c -o pmc \
+               -- python3 bench.py --steps 3 --warmup 3 --no-cpu-baseline --no-overlap
+         done
+         python3 tools/pmc_summary.py $O/pmc_head_FETCH_SIZE $O/pmc_head_WRITE_SIZE "topk_main<true" 67108864 1 \
+             $O/pmc_topk_main.json; echo "head summary rc=$?"
+         args=""
+         for wl in ${PMC_WL:-topk_nomem topk_sharded randomk qsgd terngrad powersgd sign sign256 qsgd_step terngrad_step ddp_segmented threshold dgc natural cnat fp16 sign_bits}; do
+           for c in FETCH_SIZE WRITE_SIZE; do
+             run pmc_${wl}_$c 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${wl}_$c -o pmc \
+                 -- python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline
+           done
+           args="$args $wl=$O/pmc_${wl}_FETCH_SIZE,$O/pmc_${wl}_WRITE_SIZE"
+         done
+         # the output modes these passes ran in (the default: recycled outputs at world 1)
+         python3 tools/pmc_all.py $O/r06_pmc_secondary.json --last 3 --mode topk_nomem=recycled \
+             --mode topk_sharded=recycled --mode randomk=recycled --exclude "threshold:<1>" --exclude "randomk:<false>" \
+             --exclude "dgc:spec_kernel<false>" --exclude "ddp_segmented:seg_main_kernel<false|seg_prep_kernel<false" \
+             --exclude "topk_sharded:topk_main<false|topk_bracket<false|stream_kernel" $args; echo "pmc_all rc=$?" ;;
     shardlocal) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
     abdec1) run ab_decode1 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so ;;
