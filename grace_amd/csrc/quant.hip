@@ -2310,6 +2310,8 @@ int32_t grace_terngrad_slot_bytes(void) { return (int32_t)sizeof(TernSlot); }
 grace_status_t grace_terngrad_shard_stats(const float* x, int64_t xoff, const int64_t* seg_off,
                                           const int64_t* unit_off, int32_t nseg, int64_t unit0, int64_t nunits_local,
                                           void* ws, void* stream) {
+  GRACE_REQUIRE(kTernEncReduce, "grace_terngrad_shard_stats: needs the encode-side scale reduction "
+                "(a GRACE_TERN_ENC_REDUCE=0 build has no global slot protocol)");
   GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && unit0 >= 0 && nunits_local >= 0 && xoff >= 0 && ws &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0,
                 "grace_terngrad_shard_stats: bad arguments (16-B aligned shard)");
@@ -2324,6 +2326,8 @@ grace_status_t grace_terngrad_shard_encode(const float* x, int64_t xoff, const i
                                            const int64_t* unit_off, int32_t nseg, int64_t unit0,
                                            int64_t nunits_local, const float* clip_in, const float* u, uint64_t seed,
                                            int8_t* codes, const void* ws, void* stream) {
+  GRACE_REQUIRE(kTernEncReduce, "grace_terngrad_shard_encode: needs the encode-side scale reduction "
+                "(a GRACE_TERN_ENC_REDUCE=0 build has no global slot protocol)");
   GRACE_REQUIRE(x && seg_off && unit_off && nseg >= 1 && unit0 >= 0 && nunits_local >= 0 && xoff >= 0 && codes &&
                     ws && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(u) |
                             reinterpret_cast<uintptr_t>(codes)) & 15) == 0,

@@ -2033,13 +2033,14 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
                           kBracketBlock, 0, s>>>(a, w);
   GRACE_CHECK_LAUNCH("topk_bracket");
   bool big = false;
-  if constexpr (!HAS_RES && kMainV3) {
+  if constexpr (!HAS_RES && kMainV3 && kVecOf<HAS_RES, MODE> == GRACE_MAIN_VEC_NORES) {
     // 4 / 8 B per element (no residual stream): large buckets take chunks of kNoresBigVec float4 per
     // lane, so that the grid is ONE balanced generation (2^26 elements: 1024 workgroups, 4 per CU;
     // 32 float4 gave 2048 for 1536 resident slots).  r06 A/B (tools/ab_v3.py, 256 MiB, 1 %): main
     // pass with the recycled output, 32 / 40 / 48 / 64 / 80 / 96 / 128 float4 -> 72.2 / 67.4 / 67.3 /
     // 59.2-60.6 / 69.2 / 72.7 / 58.5 us (820 and 683 workgroups leave CUs unevenly loaded).  Only for
     // k <= n / 50: a wave's LDS region holds 512 flagged elements, ~1.45 % of 16384 at k = 1 %.
+    // (only the 4 / 8 B classes: the first residual step's 12 B pass keeps its 20-float4 chunks)
     big = a.n >= kNoresBigMinN && a.k <= a.n / 50;
     if (big) launch_main<HAS_RES, MODE, kNoresBigVec>(a, w, sparse, vec, s);
   }

@@ -106,12 +106,20 @@ class TopKCompressor(Compressor):
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
         # world > 1: the new residual goes to a second buffer (no dense output to park t in), so the
         # main pass zeroes its provisional picks at once (grace_topk_residual_step_swap)
-        res_new = mem.spare_for(name, g)
-        buf, vals, idx = ops.topk_residual_step_swap(g, res if has else None, has, mem.beta, mem.gamma, k, res_new,
-                                                     carry=carry, carry_valid=carry_valid)
-        mem.retire(name, res if has else None)
-        mem.residuals[name] = res_new
-        mem.carry_written(name, res_new, carry)
+        if getattr(mem, "keep_spare", True):
+            res_new = mem.spare_for(name, g)
+            buf, vals, idx = ops.topk_residual_step_swap(g, res if has else None, has, mem.beta, mem.gamma, k,
+                                                         res_new, carry=carry, carry_valid=carry_valid)
+            mem.retire(name, res if has else None)
+            mem.residuals[name] = res_new
+            mem.carry_written(name, res_new, carry)
+        else:
+            # ResidualMemory(keep_spare=False): one residual buffer per name, updated in place (4 B
+            # per parameter less; the finalize zeroes the selected positions instead)
+            buf, vals, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=None, carry=carry,
+                                                    carry_valid=carry_valid)
+            mem.residuals[name] = res
+            mem.carry_written(name, res, carry)
         divisor = world if self.average else 1
         if n > ops.SORT_PAYLOAD_MAX_N:
             # beyond the index-sorted grouping's range (payload.hip): gather as-is and decode with

@@ -28,7 +28,10 @@ rank by ``ShardPartitionError`` (never a hang, never a silent mix of partitions)
 set the bit in a pinned word of this engine, one per step parity; step N + 2 waits for step N's
 select (an event: by then step N + 1 is queued, so the device never idles) and takes that word,
 so every rank raises at the same step N + 2 -- step N + 1's bits, which one rank may already see
-and another not, are in the other word.
+and another not, are in the other word.  The parity counts this engine's steps over all names, so
+a bad step of a name that is not stepped again surfaces at the engine's next-but-one step of ANY
+name -- and not at all if training ends within two steps: call ``check()`` at the end of training
+or of an epoch (it waits for the device and reads both words).
 ``check_sizes=True`` instead agrees the partition at every step (one small all_gather and one host
 read per step), so a resize is handled in the step where it happens: every rank re-plans with the
 new sizes, a rank whose shard kept its size keeps its error feedback, a resized rank starts from

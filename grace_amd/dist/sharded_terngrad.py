@@ -8,7 +8,11 @@ A tensor's scale needs statistics of the whole tensor, which may span ranks.  Th
 (sum, sum of squares, max |x|, NaN) and reduces a tensor's unit partials in a fixed order.  So the
 units are the partition, and the SURVEY's "one fp64 allreduce of (Σx, Σx², max|x|) per tensor"
 becomes ONE all-gather of the unit partials: every rank then reduces the same partials in the same
-order as the single-GPU encoder, and its scales are bit-identical to it, not just within ulps.
+order as the single-GPU encoder, and its scales are bit-identical to it, not just within ulps --
+when every work unit starts on a multiple of 4 elements of the bucket (units of tensors whose
+offsets are multiples of 4).  A unit at an odd offset is summed by the shard kernel in another quad
+phase than by the whole-bucket kernel, so its f64 sum of squares may round differently: the clip
+(2.5 std) and through it the scalar can then differ by an ulp, rarely.
 
 Per step on rank r (grace_terngrad_shard_*, grace_terngrad_scalars):
   1. shard_stats: the partials of this rank's units into their slots of the global slot array;

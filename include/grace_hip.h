@@ -301,7 +301,9 @@ grace_status_t grace_terngrad_step_w1(const float* x, const int64_t* seg_off, co
  * point there, 16-B aligned).  ws = the GLOBAL slot array (grace_terngrad_workspace_bytes(nunits),
  * grace_terngrad_slot_bytes() per unit): shard_stats writes this rank's units' slots; after the
  * caller has all-gathered every rank's slots into it, shard_encode writes this rank's codes with
- * every segment's scale reduced exactly as the single-GPU encoder (bit-identical codes), and
+ * every segment's scale reduced exactly as the single-GPU encoder (bit-identical codes when every
+ * unit starts on a multiple of 4 elements; a unit at another offset sums its f64 partials in another
+ * quad phase, so the clip and scalar may differ by an ulp, rarely), and
  * grace_terngrad_scalars derives every segment's scalar the same way (nothing but the slots
  * travels before the codes). */
 /* Sharded TernGrad's replicated decode straight from the W gathered records: rank w's codes of the

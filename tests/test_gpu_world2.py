@@ -37,6 +37,12 @@ def _worker(rank, path, outdir, golden_path):
         res[f"big_g{s}"] = g
         res[f"big_out{s}"] = comm.step(torch.from_numpy(g).cuda(), "big").cpu().numpy()
         res[f"big_res{s}"] = comm.memory.residuals["big"].cpu().numpy()
+    # the same steps with one residual buffer per name (ResidualMemory(keep_spare=False): the in-place
+    # W > 1 step instead of the second buffer) -- the same results bit for bit
+    comm = Allgather(TopKCompressor(0.01), ResidualMemory(keep_spare=False), 2)
+    for s in range(2):
+        res[f"bigip_out{s}"] = comm.step(torch.from_numpy(res[f"big_g{s}"]).cuda(), "big").cpu().numpy()
+        res[f"bigip_res{s}"] = comm.memory.residuals["big"].cpu().numpy()
     # variable-size payloads: threshold + residual, one host read per step (threshold.fused_step)
     from grace_amd.dist.compressor.threshold import ThresholdCompressor
     comm = Allgather(ThresholdCompressor(1.5), ResidualMemory(), 2)
@@ -84,6 +90,8 @@ def test_fused_topk_and_sign_world2(golden):
             exp = (O.python_sum(decs) / np.float32(2)).astype(np.float32)
             for r in range(2):
                 assert np.array_equal(zs[r][f"big_out{s}"].view(np.uint32), exp.view(np.uint32))
+                assert np.array_equal(zs[r][f"bigip_out{s}"].view(np.uint32), exp.view(np.uint32)), "keep_spare=False"
+                assert np.array_equal(zs[r][f"bigip_res{s}"].view(np.uint32), zs[r][f"big_res{s}"].view(np.uint32))
 
 
 def test_variable_size_threshold_world2_one_read():
