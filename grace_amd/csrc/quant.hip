@@ -1606,6 +1606,60 @@ __global__ __launch_bounds__(kQBlock) void tern_decode_kernel(const int8_t* __re
   }
 }
 
+// A/B knob (r06): a tile decoder -- one 16-B output quad per lane and QPT quads per lane, i.e. a
+// contiguous 4 KB x QPT output tile per workgroup (r05's write probes: a workgroup writing 4 KB runs
+// at the box's write rate, 16 KB tiles at 0.87 of it) -- instead of the 16-lane row decoder.  World 1.
+// Measured slower (tools/ab_decode.py, ResNet-50 set, one process): row decoder 22.4 us, tiles of
+// 4 / 8 / 16 KB 26.6 / 24.1 / 24.2 us (the per-workgroup segment-table staging and search); off.
+#ifndef GRACE_TERN_TILE_QPT
+#define GRACE_TERN_TILE_QPT 0
+#endif
+constexpr int kTernTileQpt = GRACE_TERN_TILE_QPT;
+
+template <int QPT>
+__global__ __launch_bounds__(kQBlock) void tern_decode_tile_kernel(const int8_t* __restrict__ codes,
+                                                                  const float* __restrict__ scalars,
+                                                                  const int64_t* __restrict__ seg_off, int nseg,
+                                                                  int64_t n, float divisor, int aggregate,
+                                                                  float* __restrict__ out) {
+  __shared__ int64_t sg[kSegLds + 1];
+  for (int i = threadIdx.x; i <= nseg; i += blockDim.x) sg[i] = seg_off[i];
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kQBlock * 4 * QPT + 4 * threadIdx.x;
+  uint32_t cw[QPT];
+  int sq[QPT];
+  bool fast[QPT];
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {   // every load issued first, unconditionally (clamped address)
+    const int64_t e = base + (int64_t)q * kQBlock * 4;
+    sq[q] = find_seg(sg, nseg, e < n ? e : n - 1);
+    fast[q] = e + 3 < n && e + 3 < sg[sq[q] + 1];
+    cw[q] = *reinterpret_cast<const uint32_t*>(codes + (fast[q] ? e : 0));
+  }
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int64_t e = base + (int64_t)q * kQBlock * 4;
+    if (e >= n) continue;
+    if (fast[q]) {
+      const float sc = scalars[sq[q]];
+      float a[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (float)(int8_t)((cw[q] >> (8 * j)) & 0xFFu) * sc;
+        a[j] = aggregate ? 0.f + d : d;
+        if (divisor != 1.0f) a[j] = a[j] / divisor;
+      }
+      __builtin_nontemporal_store(f4v{a[0], a[1], a[2], a[3]}, reinterpret_cast<f4v*>(out + e));
+    } else {
+      for (int64_t x = e; x < e + 4 && x < n; ++x) {
+        const float d = (float)codes[x] * scalars[find_seg(sg, nseg, x)];
+        float v = aggregate ? 0.f + d : d;
+        out[x] = divisor == 1.0f ? v : v / divisor;
+      }
+    }
+  }
+}
+
 // Sharded TernGrad (grace_amd/dist/sharded_terngrad.py): the whole bucket decoded straight from the
 // gathered per-rank records.  Rank w's codes of its elements [rank_lo[w], rank_lo[w + 1]) sit in
 // its record at w * rec_bytes, as int8 or (packed) in the 2-bit planar layout of the reference's
@@ -2381,6 +2435,16 @@ grace_status_t grace_terngrad_decompress(const int8_t* codes, const float* scala
                 "grace_terngrad_decompress: bad arguments");
   if (n == 0) return GRACE_OK;
   const int vec = (code_stride % 4 == 0) && ((uintptr_t)codes % 4 == 0);
+  if constexpr (kTernTileQpt > 0) {
+    if (world == 1 && vec && nseg <= kSegLds && (uintptr_t)out % 16 == 0) {
+      constexpr int64_t kTile = (int64_t)kQBlock * 4 * (kTernTileQpt > 0 ? kTernTileQpt : 1);
+      tern_decode_tile_kernel<(kTernTileQpt > 0 ? kTernTileQpt : 1)><<<(unsigned)((n + kTile - 1) / kTile), kQBlock, 0,
+                                                                     as_stream(stream)>>>(
+          codes, scalars, seg_off, nseg, n, divisor, aggregate, out);
+      GRACE_CHECK_LAUNCH("grace_terngrad_decompress");
+      return GRACE_OK;
+    }
+  }
   if (nseg <= kSegLds && n < (int64_t(1) << 31)) {
     tern_decode_row_kernel<<<stream_grid((n + 127) / 128, kQNB * kQBlock / 16, kQGridCap), kQBlock, 0,
                              as_stream(stream)>>>(codes, scalars, code_stride, scal_stride, world, seg_off, nseg,
