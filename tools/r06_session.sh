@@ -75,6 +75,8 @@ for s in "$@"; do
              --exclude "topk_sharded:topk_main<false|topk_bracket<false|stream_kernel" $args; echo "pmc_all rc=$?" ;;
     shardlocal) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
+    abvec2) AB_MODES=fused,swap run ab_vec2 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+            grace_amd/lib/libgrace_hip_vec8.so grace_amd/lib/libgrace_hip_vec4.so ;;
     abtile) run ab_tile 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so grace_amd/lib/libgrace_hip_tile1.so \
               grace_amd/lib/libgrace_hip_tile2.so grace_amd/lib/libgrace_hip_tile4.so ;;
     abdec1) run ab_decode1 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so ;;
