@@ -18,10 +18,16 @@
 //        shard_coarse  a 2048-bin histogram of key >> 20 (1/8 octave) over the W * cap entries;
 //        shard_apply   every workgroup finds the coarse bin C1 of the k-th key from it; entries
 //                      above C1 are selected, below rejected; the C1 entries go to a list and a
-//                      2048-bin histogram of key bits 19..9 (sub-bins);
+//                      2048-bin histogram of key bits 19..9 (sub-bins).  The list is kept in blocks:
+//                      a round's 4096 entries put their C1 entries, compacted, in the same block of
+//                      the list with the count beside it, so no workgroup reserves list space
+//                      through a global atomic (r06);
 //        shard_bnd     every workgroup finds the sub-bin B2 of the cut; the C1 list is decided in
-//                      parallel by sub-bin; the few B2 entries (sharing key bits 31..9) are ranked
-//                      exactly by the composite (key, global index) by the last arriver.
+//                      parallel, one list block per workgroup; the few B2 entries (sharing key bits
+//                      31..9) are ranked exactly by the composite (key, global index) by the last
+//                      arriver, from whole entries carried in the cut list (no record reads).
+//      Each kernel issues its first round's loads before it sums the histogram copies, so the two
+//      round trips overlap (r06: 41.5 -> 34.0 us at configs[4], profiles/r06_shard_select_ab.txt).
 //      A selected entry is written to the dense output (0 + v); an own entry the global cut rejects
 //      gets its t back in the residual (r' = v: the engine had zeroed it), and pay_idx marks this
 //      rank's record entries with their global index (selected) or -1.
@@ -48,9 +54,8 @@ constexpr int kShBins = 2048;        // coarse bins (key >> 20) and sub-bins (ke
 constexpr int kShGroups = 8;         // histogram copies (arrival groups: blockIdx % 8)
 constexpr int kShMaxWorld = 1024;
 constexpr int kShMaxGrid = 512;
-constexpr int kShTakePer = 8;        // shard_bnd: list entries per thread per round
+constexpr uint32_t kShListBlock = kShBlock * kShPer;   // one apply round = one block of the C1 list
 constexpr int kShPairCap = 1024;     // cut sub-bin entries ranked pairwise
-constexpr int64_t kShBndGrid = 64;   // shard_bnd workgroups at most
 
 // Diagnostic build only (-DGRACE_STAMPS): s_memrealtime stamps (100 MHz) in the free tail of the
 // 256-byte ctl block (slots 0..23).  Never in shipped builds.
@@ -67,7 +72,7 @@ constexpr int64_t kShBndGrid = 64;   // shard_bnd workgroups at most
 struct ShCtl {
   int32_t c1;        // coarse bin of the k-th key; -1 = every valid entry is selected
   uint32_t need;     // entries still to take from bin C1
-  uint32_t nb;       // C1 list fill counter (reset by the last shard_bnd)
+  uint32_t nb;       // diagnostic builds: the C1 list's length (reset by the last shard_bnd)
   uint32_t n2;       // cut sub-bin list fill counter (reset by the last shard_bnd)
   uint32_t ticket;   // shard_bnd arrivals (reset by the last)
   uint32_t pad[11];
@@ -89,8 +94,10 @@ struct ShArgs {
   ShCtl* ctl;
   uint32_t* hist;       // [kShGroups][kShBins] coarse copies, left zeroed
   uint32_t* hist2;      // [kShGroups][kShBins] sub-bin copies, left zeroed
-  uint4* bnd;           // C1 entries {entry number, global index, value bits, 0} [world * cap]
-  uint32_t* bnd2;       // entries of the cut's sub-bin [world * cap]
+  uint4* bnd;           // C1 entries {entry number, global index, value bits, 0} [world * cap], in blocks
+                        // of kShListBlock: block b holds bcnt[b] entries from its start
+  uint32_t* bcnt;       // [ceil(world * cap / kShListBlock)]
+  uint4* bnd2;          // entries of the cut's sub-bin, the same form [world * cap]
   int32_t* status;      // pinned host word (system-scope fetch_or), may be null
 };
 
@@ -155,19 +162,24 @@ __device__ __forceinline__ void flush_copy(uint32_t* gh, const uint32_t* hl) {
 // holding the rank-th largest (descending); -1 if fewer than `rank` counts, kShBins if rank == 0
 __device__ __forceinline__ int find_from_copies(const uint32_t* gh, uint32_t* hl, uint32_t rank, uint32_t* s_w,
                                                 uint32_t* s_res, uint32_t& above, uint32_t& total) {
-  for (int b = threadIdx.x; b < kShBins; b += kShBlock) {
-    uint32_t c[kShGroups];
+  // every copy of both of this thread's bins loaded before any is summed: ONE round trip
+  constexpr int PER = kShBins / kShBlock;
+  static_assert(kShBins % kShBlock == 0, "whole bins per thread");
+  uint32_t c[PER][kShGroups];
 #pragma unroll
-    for (int q = 0; q < kShGroups; ++q) c[q] = gh[q * kShBins + b];
+  for (int p = 0; p < PER; ++p)
+#pragma unroll
+    for (int q = 0; q < kShGroups; ++q) c[p][q] = gh[q * kShBins + p * kShBlock + threadIdx.x];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
     uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < kShGroups; ++q) sum += c[q];
-    hl[b] = sum;
+    for (int q = 0; q < kShGroups; ++q) sum += c[p][q];
+    hl[p * kShBlock + threadIdx.x] = sum;
+    mine += sum;
   }
-  __syncthreads();
-  uint32_t c = 0;
-  for (int b = threadIdx.x; b < kShBins; b += kShBlock) c += hl[b];
-  block_excl_scan<kShBlock>(c, s_w, &total);
+  block_excl_scan<kShBlock>(mine, s_w, &total);   // (its barriers also publish hl)
   if (rank == 0 || total < rank) { above = total; return rank == 0 ? kShBins : -1; }
   const uint32_t r1[1] = {rank};
   int d[1];
@@ -202,16 +214,21 @@ __global__ __launch_bounds__(kShBlock) void shard_coarse_kernel(ShArgs a) {
 __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   __shared__ int64_t s_base[kShMaxWorld];
   __shared__ uint32_t hl[kShBins];
-  __shared__ uint4 s_stage[kShBlock * kShPer];      // this round's C1 entries, staged
   __shared__ uint32_t s_w[kShBlock / kWave + 1];
   __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_cnt, s_gbase;
+  __shared__ uint32_t s_cnt;
   const int t = threadIdx.x;
   SH_STAMP(blockIdx.x == 0, a.ctl, 2);
   for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
   const uint32_t k = (uint32_t)a.k;
   uint32_t above, total;
+  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
+  // the first round's entries are loaded before the histogram copies: both in flight together
+  int32_t li[kShPer];
+  float v[kShPer];
+  if (blockIdx.x * kShListBlock < N) load_entries(a, blockIdx.x * kShListBlock + t, N, li, v);
   const int c1 = find_from_copies(a.hist, hl, k, s_w, s_res, above, total);   // -1: every valid entry selected
+  SH_STAMP(blockIdx.x == 0, a.ctl, 8);
   if (blockIdx.x == 0) {
     // the partition every rank planned with vs the shard lengths the records carry
     uint32_t bad = 0;
@@ -228,13 +245,13 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
   for (int b = t; b < kShBins; b += kShBlock) hl[b] = 0u;
   if (t == 0) s_cnt = 0u;
   __syncthreads();
-  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
-  // uniform rounds (the workgroup barriers below): every thread runs every round
-  for (uint32_t r0 = blockIdx.x * kShBlock * kShPer; r0 < N; r0 += gridDim.x * kShBlock * kShPer) {
+  // uniform rounds (the workgroup barriers below): every thread runs every round.  A round covers one
+  // list block of kShListBlock entries; its C1 entries go to the same block of the C1 list, compacted,
+  // with their count in bcnt: no global reservation
+  for (uint32_t r0 = blockIdx.x * kShListBlock; r0 < N; r0 += gridDim.x * kShListBlock) {
     const uint32_t e0 = r0 + t;
-    int32_t li[kShPer];
-    float v[kShPer];
-    load_entries(a, e0, N, li, v);
+    if (r0 != blockIdx.x * kShListBlock) load_entries(a, e0, N, li, v);
+    uint32_t off[kShPer];   // this thread's C1 entries: their place in the block
 #pragma unroll
     for (int u = 0; u < kShPer; ++u) {
       const uint32_t e = e0 + u * kShBlock;
@@ -252,75 +269,84 @@ __global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
           else shard_take(a, cb > c1, w, j, li[u], v[u], s_base[w]);
         }
       }
-      // C1 entries staged in LDS (one LDS atomic per wave); the round's list leaves with ONE
-      // global reservation per workgroup
+      // C1 entries placed by one LDS atomic per wave
       const uint64_t m = __ballot(inb);
+      off[u] = ~0u;
       if (m) {
         uint32_t base0 = 0;
         if (lane_rank(m) == 0 && inb) base0 = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
         base0 = __shfl(base0, __builtin_ctzll(m), 64);
-        if (inb) {
-          // the entry with its global index and value: shard_bnd decides it without going back
-          // to the records (a dependent load chain per entry)
-          const uint32_t w = e / cap;
-          s_stage[base0 + lane_rank(m)] = make_uint4(e, (uint32_t)(s_base[w] + li[u]), f2u(v[u]), 0u);
-        }
+        if (inb) off[u] = base0 + lane_rank(m);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u) {
+      if (off[u] != ~0u) {
+        // the entry with its global index and value: shard_bnd decides it without going back to
+        // the records (a dependent load chain per entry); read after the kernel boundary
+        const uint32_t e = e0 + u * kShBlock;
+        const uint32_t w = e / cap;
+        a.bnd[r0 + off[u]] = make_uint4(e, (uint32_t)(s_base[w] + li[u]), f2u(v[u]), 0u);
       }
     }
     __syncthreads();
-    const uint32_t cnt = s_cnt;
-    if (t == 0 && cnt) s_gbase = atomicAdd(&a.ctl->nb, cnt);
-    __syncthreads();
-    for (uint32_t q = t; q < cnt; q += kShBlock) a.bnd[s_gbase + q] = s_stage[q];   // read after the boundary
-    __syncthreads();
-    if (t == 0) s_cnt = 0u;
+    if (t == 0) {
+      a.bcnt[r0 / kShListBlock] = s_cnt;
+#ifdef GRACE_STAMPS
+      atomicAdd(&a.ctl->nb, s_cnt);   // diagnostic: the C1 list's length (ctl slot 12)
+#endif
+      s_cnt = 0u;
+    }
     __syncthreads();
   }
+  SH_STAMP(blockIdx.x == 0, a.ctl, 9);
   flush_copy(a.hist2, hl);
   SH_STAMP(blockIdx.x == 0, a.ctl, 3);
 }
 
 // 3c. the sub-bin cut over the C1 list in parallel; the last arriver ranks the cut sub-bin
 __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
+  static_assert(kShPairCap <= kShBlock, "the pairwise ranking holds one cut entry per thread");
   __shared__ int64_t s_base[kShMaxWorld];
   __shared__ uint32_t hl[kShBins];
-  __shared__ uint32_t s_stage[kShBlock * kShTakePer];
   __shared__ uint64_t s_comp[kShPairCap];
-  __shared__ uint32_t s_ent[kShPairCap];
   __shared__ uint32_t s_w[kShBlock / kWave + 1];
   __shared__ uint32_t s_res[2];
   __shared__ uint32_t s_cnt, s_gbase, s_last;
   const int t = threadIdx.x;
   SH_STAMP(blockIdx.x == 0, a.ctl, 4);
   for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
-  const uint32_t nb = a.ctl->nb, need = a.ctl->need;   // kernel boundary: plain loads
+  const uint32_t need = a.ctl->need;   // kernel boundary: plain loads
   if (t == 0) s_cnt = 0u;
-  int b2 = kShBins;       // need == 0: every C1 entry is rejected
-  uint32_t need2 = 0;
-  if (need >= nb) {
-    b2 = -1;              // every C1 entry is selected
-    __syncthreads();
-  } else if (need > 0) {
-    uint32_t above2, total2;
-    b2 = find_from_copies(a.hist2, hl, need, s_w, s_res, above2, total2);
-    need2 = need - above2;
-  } else {
-    __syncthreads();
+  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
+  const uint32_t nblk = (N + kShListBlock - 1) / kShListBlock;
+  // the first list block is loaded before the histogram copies: both in flight together
+  uint32_t cnt_b = 0;
+  uint4 q4[kShPer];
+  if (blockIdx.x < nblk) {
+    cnt_b = a.bcnt[blockIdx.x];
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u)   // unconditional (the list is whole blocks long)
+      q4[u] = a.bnd[blockIdx.x * kShListBlock + t + u * kShBlock];
   }
-  const uint32_t cap = (uint32_t)a.cap;
-  const uint32_t step = gridDim.x * kShBlock * kShTakePer;
-  for (uint32_t r0 = blockIdx.x * kShBlock * kShTakePer; r0 < nb; r0 += step) {   // uniform rounds
-    const uint32_t j0 = r0 + t;
-    uint4 q4[kShTakePer];
+  // b2: the sub-bin of the cut within C1; kShBins (need == 0): every C1 entry is rejected, -1 (need
+  // above the C1 count): every C1 entry is selected
+  uint32_t above2, total2;
+  const int b2 = find_from_copies(a.hist2, hl, need, s_w, s_res, above2, total2);
+  const uint32_t need2 = b2 >= 0 && b2 < kShBins ? need - above2 : 0u;
+  SH_STAMP(blockIdx.x == 0, a.ctl, 10);
+  for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // uniform rounds: one list block each
+    const uint32_t r0 = blk * kShListBlock;
+    if (blk != blockIdx.x) {
+      cnt_b = a.bcnt[blk];
 #pragma unroll
-    for (int u = 0; u < kShTakePer; ++u) {
-      const uint32_t jj = j0 + u * kShBlock;
-      q4[u] = a.bnd[jj < nb ? jj : nb - 1];
+      for (int u = 0; u < kShPer; ++u) q4[u] = a.bnd[r0 + t + u * kShBlock];   // in flight with cnt_b
     }
+    uint32_t off[kShPer];   // this thread's cut entries: their place in the workgroup's share
 #pragma unroll
-    for (int u = 0; u < kShTakePer; ++u) {
+    for (int u = 0; u < kShPer; ++u) {
       bool in2 = false;
-      if (j0 + u * kShBlock < nb) {
+      if (t + u * kShBlock < cnt_b) {
         uint32_t w, j;
         split_entry(q4[u].x, cap, w, j);
         const float v = u2f(q4[u].z);
@@ -329,23 +355,35 @@ __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
         if (!in2) shard_take(a, sb > b2, w, j, (int32_t)((int64_t)q4[u].y - s_base[w]), v, s_base[w]);
       }
       const uint64_t m = __ballot(in2);
+      off[u] = ~0u;
       if (m) {
         uint32_t base0 = 0;
         if (lane_rank(m) == 0 && in2) base0 = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
         base0 = __shfl(base0, __builtin_ctzll(m), 64);
-        if (in2) s_stage[base0 + lane_rank(m)] = q4[u].x;
+        if (in2) off[u] = base0 + lane_rank(m);
       }
     }
     __syncthreads();
     const uint32_t cnt = s_cnt;
     if (t == 0 && cnt) s_gbase = atomicAdd(&a.ctl->n2, cnt);
     __syncthreads();
-    for (uint32_t q = t; q < cnt; q += kShBlock)   // write-through (sc1) for the last arriver
-      __hip_atomic_store(&a.bnd2[s_gbase + q], s_stage[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the whole entry (entry number, global index, value bits) from registers, write-through (sc1)
+    // for the last arriver, which then ranks and decides from the list alone
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u) {
+      if (off[u] != ~0u) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(&a.bnd2[s_gbase + off[u]]);
+        __hip_atomic_store(d, (uint64_t)q4[u].x | ((uint64_t)q4[u].y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, (uint64_t)q4[u].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     __syncthreads();
     if (t == 0) s_cnt = 0u;
     __syncthreads();
   }
+  // the coarse histogram's copies were last read by shard_apply: re-zeroed here by every workgroup
+  // (the sub-bin copies, read above, by the last arriver)
+  for (int b = blockIdx.x * kShBlock + t; b < kShGroups * kShBins; b += gridDim.x * kShBlock) a.hist[b] = 0u;
   // arrival (DESIGN §4 memory-model table, row 1: write-through stores, vmcnt(0), barrier, ticket)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -353,58 +391,73 @@ __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
   if (t == 0) s_last = atomicAdd(&a.ctl->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // several workgroups per CU possible: keep the acquire
   SH_STAMP(true, a.ctl, 6);
+  // the counter and, below, the cut list are read with agent-scope atomic loads (as they were
+  // written): no acquire fence on the common path
   const uint32_t n2 = __hip_atomic_load(&a.ctl->n2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // a cut-list entry: its record slot (w, j), local index and value
+  auto entry = [&](const uint4& q, uint32_t& w, uint32_t& j, int32_t& l, float& x) {
+    split_entry(q.x, cap, w, j);
+    l = (int32_t)((int64_t)q.y - s_base[w]);
+    x = u2f(q.z);
+  };
   if (n2 <= (uint32_t)kShPairCap) {
-    // rank the cut sub-bin's entries pairwise (unique composites): the need2 highest are selected
-    for (uint32_t q = t; q < n2; q += kShBlock) {
-      const uint32_t e = a.bnd2[q];
-      uint32_t w, j;
-      split_entry(e, cap, w, j);
-      s_ent[q] = e;
-      s_comp[q] = comp_key(abs_key(rec_vals(a, w)[j]), (uint32_t)(s_base[w] + rec_idx(a, w)[j]));
-    }
+    // rank the cut sub-bin's entries pairwise (unique composites): the need2 highest are selected;
+    // one entry per thread, kept in registers
+    // unconditional (the list is whole blocks long): in flight with n2
+    uint64_t* qp = reinterpret_cast<uint64_t*>(&a.bnd2[t]);
+    const uint64_t q01 = __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t q23 = __hip_atomic_load(qp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint4 q = make_uint4((uint32_t)q01, (uint32_t)(q01 >> 32), (uint32_t)q23, 0u);
+    if ((uint32_t)t < n2) s_comp[t] = comp_key(abs_key(u2f(q.z)), q.y);
     __syncthreads();
-    for (uint32_t q = t; q < n2; q += kShBlock) {
-      const uint64_t me = s_comp[q];
+    if ((uint32_t)t < n2) {
+      const uint64_t me = s_comp[t];
       uint32_t rk = 0;
-      for (uint32_t o = 0; o < n2; ++o) rk += s_comp[o] > me;
+      uint32_t o = 0;
+      // 8 LDS reads in flight per step (one at a time, the loop waited an LDS latency per entry:
+      // 5 us at n2 = 225)
+      for (; o + 8 <= n2; o += 8) {
+        uint64_t c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = s_comp[o + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rk += c[u] > me;
+      }
+      for (; o < n2; ++o) rk += s_comp[o] > me;
+      SH_STAMP(true, a.ctl, 13);
       uint32_t w, j;
-      split_entry(s_ent[q], cap, w, j);
-      shard_take(a, rk < need2, w, j, rec_idx(a, w)[j], rec_vals(a, w)[j], s_base[w]);
+      int32_t l;
+      float x;
+      entry(q, w, j, l, x);
+      shard_take(a, rk < need2, w, j, l, x, s_base[w]);
     }
   } else {
     // massive ties (more than kShPairCap entries share key bits 31..9): exact radix select over
-    // the cut sub-bin's list
-    const uint32_t* lst = a.bnd2;
-    const ShArgs* ap = &a;
-    const int64_t* bp = s_base;
-    auto src = [lst, ap, bp](int64_t jj) {
-      const uint32_t e = lst[jj];
-      uint32_t w, j;
-      split_entry(e, (uint32_t)ap->cap, w, j);
-      return comp_key(abs_key(rec_vals(*ap, w)[j]), (uint32_t)(bp[w] + rec_idx(*ap, w)[j]));
+    // the cut sub-bin's list (plain loads, after the acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint4* lst = a.bnd2;
+    auto src = [lst](int64_t jj) {
+      const uint4 q = lst[jj];
+      return comp_key(abs_key(u2f(q.z)), q.y);
     };
     const uint64_t T = block_select_comp<kShBlock>(src, (int64_t)n2, need2, hl, s_w, s_res);
     for (uint32_t jj = t; jj < n2; jj += kShBlock) {
-      const uint32_t e = a.bnd2[jj];
+      const uint4 q = a.bnd2[jj];
       uint32_t w, j;
-      split_entry(e, cap, w, j);
-      const int32_t l = rec_idx(a, w)[j];
-      const float x = rec_vals(a, w)[j];
-      shard_take(a, comp_key(abs_key(x), (uint32_t)(s_base[w] + l)) >= T, w, j, l, x, s_base[w]);
+      int32_t l;
+      float x;
+      entry(q, w, j, l, x);
+      shard_take(a, comp_key(abs_key(x), q.y) >= T, w, j, l, x, s_base[w]);
     }
   }
+  SH_STAMP(true, a.ctl, 14);
   // every launch before has finished and every workgroup of this one has arrived: re-zero the
-  // histogram copies and counters for the next call
-  for (int b = t; b < kShGroups * kShBins; b += kShBlock) {
-    a.hist[b] = 0u;
-    a.hist2[b] = 0u;
-  }
+  // sub-bin histogram copies and the counters for the next call
+  for (int b = t; b < kShGroups * kShBins; b += kShBlock) a.hist2[b] = 0u;
   if (t == 0) {
 #ifdef GRACE_STAMPS
-    reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.ctl) + 64)[2 * 12] = nb;   // slot 12: nb, n2
+    reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.ctl) + 64)[2 * 12] = a.ctl->nb;   // slot 12: nb, n2
     reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.ctl) + 64)[2 * 12 + 1] = n2;
 #endif
     a.ctl->nb = 0u;
@@ -434,9 +487,15 @@ __global__ __launch_bounds__(256) void shard_clear_kernel(float* __restrict__ ou
   }
 }
 
-static size_t sh_list_bytes(int64_t world, int64_t cap) { return (sizeof(uint32_t) * world * cap + 255) & ~(size_t)255; }
+// one list (bnd or bnd2, uint4 entries): whole blocks of kShListBlock entries
+static size_t sh_list_bytes(int64_t world, int64_t cap) {
+  return sizeof(uint4) * kShListBlock * ((world * cap + kShListBlock - 1) / kShListBlock);
+}
+static size_t sh_bcnt_bytes(int64_t world, int64_t cap) {
+  return (sizeof(uint32_t) * ((world * cap + kShListBlock - 1) / kShListBlock) + 255) & ~(size_t)255;
+}
 static size_t sh_ws_bytes(int64_t world, int64_t cap) {
-  return 256 + 2 * sizeof(uint32_t) * kShGroups * kShBins + 5 * sh_list_bytes(world, cap);
+  return 256 + 2 * sizeof(uint32_t) * kShGroups * kShBins + 2 * sh_list_bytes(world, cap) + sh_bcnt_bytes(world, cap);
 }
 
 }  // namespace grace
@@ -488,7 +547,8 @@ grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t ra
   a.hist = reinterpret_cast<uint32_t*>(p + 256);
   a.hist2 = a.hist + kShGroups * kShBins;
   a.bnd = reinterpret_cast<uint4*>(a.hist2 + kShGroups * kShBins);
-  a.bnd2 = reinterpret_cast<uint32_t*>(a.bnd) + 4 * (sh_list_bytes(world, cap) / sizeof(uint32_t));
+  a.bnd2 = a.bnd + sh_list_bytes(world, cap) / sizeof(uint4);
+  a.bcnt = reinterpret_cast<uint32_t*>(a.bnd2 + sh_list_bytes(world, cap) / sizeof(uint4));
   a.status = status_host;
   const int64_t N = (int64_t)world * cap;
   int64_t g = (N + kShBlock * kShPer - 1) / (kShBlock * kShPer);
@@ -498,9 +558,8 @@ grace_status_t grace_shard_select(const int32_t* recs, int32_t world, int32_t ra
   GRACE_CHECK_LAUNCH("grace_shard_select");
   shard_apply_kernel<<<grid, kShBlock, 0, s>>>(a);
   GRACE_CHECK_LAUNCH("grace_shard_select");
-  // the C1 list's length is on the device: a fixed grid, each workgroup looping
-  const int64_t gb = (N + kShBlock * kShTakePer - 1) / (kShBlock * kShTakePer);
-  shard_bnd_kernel<<<(unsigned)(gb < 1 ? 1 : (gb > kShBndGrid ? kShBndGrid : gb)), kShBlock, 0, s>>>(a);
+  // one workgroup per block of the C1 list (the apply's grid)
+  shard_bnd_kernel<<<grid, kShBlock, 0, s>>>(a);
   GRACE_CHECK_LAUNCH("grace_shard_select");
   return GRACE_OK;
 }

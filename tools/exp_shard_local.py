@@ -84,6 +84,10 @@ for step in range(6):
         print(f"step {step} select stamps, us from the coarse launch's start (workgroup 0 unless noted): "
               f"coarse {us(0, 1)}, boundary {us(1, 2)}, apply {us(2, 3)}, boundary {us(3, 4)}, bnd to arrival "
               f"{us(4, 5)}, to the last arriver {us(5, 6)}, its ranking {us(6, 7)}; total {us(0, 7)}")
+        nbv = ws[64 + 8 * 12:64 + 8 * 13].cpu().numpy().view(np.uint32)
+        print(f"  apply: find c1 {us(2, 8)}, round {us(8, 9)}, flush {us(9, 3)}; bnd: find b2 {us(4, 10)}, "
+              f"rounds to arrival {us(10, 5)}; last arriver: load+pairwise {us(6, 13)}, decisions {us(13, 14)}, "
+              f"re-zero {us(14, 7)}; nb {int(nbv[0])} n2 {int(nbv[1])}")
 med = [statistics.median(r[i] for r in rows[2:]) for i in range(3)]
 print(f"W={W} n={n} k={k} per-rank device time, us (median of steps 2..5): local top-k {med[0]:.1f}, "
       f"dense zero-fill {med[1]:.1f}, select {med[2]:.1f}; serial sum {sum(med):.1f} "

@@ -74,9 +74,22 @@ for s in "$@"; do
              --exclude "dgc:spec_kernel<false>" --exclude "ddp_segmented:seg_main_kernel<false|seg_prep_kernel<false" \
              --exclude "topk_sharded:topk_main<false|topk_bracket<false|stream_kernel" $args; echo "pmc_all rc=$?" ;;
     shardlocal) run shard_local 180 python3 tools/exp_shard_local.py 8 ;;
+    shardstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run shard_local_stamps 180 python3 tools/exp_shard_local.py 8 ;;
+    abshard) for i in 1 2; do
+               GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_shold.so run shard_old_$i 180 python3 tools/exp_shard_local.py 8
+               GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_shpre.so run shard_pre_$i 180 python3 tools/exp_shard_local.py 8
+               run shard_new_$i 180 python3 tools/exp_shard_local.py 8
+             done ;;
+    shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
+               -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
     abvec2) AB_MODES=fused,swap run ab_vec2 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
             grace_amd/lib/libgrace_hip_vec8.so grace_amd/lib/libgrace_hip_vec4.so ;;
+    abpick) AB_MODES=nomem_rec,nomem_dense,fused run ab_pick 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_pickmain.so \
+              grace_amd/lib/libgrace_hip.so ;;
+    abplace) run ab_place 300 python3 tools/ab_place.py grace_amd/lib/libgrace_hip.so 6 ;;
+    abpick2) AB_MODES=fused,nomem_rec run ab_pick2 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+              grace_amd/lib/libgrace_hip_pickmain.so ;;
     abtile) run ab_tile 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so grace_amd/lib/libgrace_hip_tile1.so \
               grace_amd/lib/libgrace_hip_tile2.so grace_amd/lib/libgrace_hip_tile4.so ;;
     abdec1) run ab_decode1 300 python3 tools/ab_decode.py grace_amd/lib/libgrace_hip.so ;;
