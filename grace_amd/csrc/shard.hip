@@ -35,7 +35,11 @@
 // per group of workgroups, blockIdx % 8) that its readers sum.  A one-launch variant with two
 // software grid barriers measured 30 us against 55 us for an earlier three-launch form, but a
 // barrier needs the whole grid resident, and two processes sharing one GPU (or any concurrent
-// kernel that fills the CUs) left it waiting on workgroups that could not be scheduled.
+// kernel that fills the CUs) left it waiting on workgroups that could not be scheduled.  A one-launch
+// form WITHOUT that hazard (r06: each phase's blocks claimed through a counter by running
+// workgroups, a workgroup waiting only on a phase's done count) was bit-exact but slower, 48-49 us
+// against 33-34 us: its per-phase claims and done counts are same-address atomics from every
+// workgroup (profiles/r06_shard_select_ab.txt), more than the two kernel boundaries it removes.
 // No sample exchange, no capacity guess and no bracket-miss protocol: the record capacity is k
 // (a rank can hold at most k of the global top-k), and a degenerate local bucket is handled inside
 // the local engine's own exact fallback.  The partition (shard lengths) is agreed on a name's first
@@ -189,209 +193,143 @@ __device__ __forceinline__ int find_from_copies(const uint32_t* gh, uint32_t* hl
   return d[0];
 }
 
-// 3a. the coarse histogram (key >> 20) of the valid gathered entries
-__global__ __launch_bounds__(kShBlock) void shard_coarse_kernel(ShArgs a) {
-  __shared__ uint32_t hl[kShBins];
-  const int t = threadIdx.x;
-  SH_STAMP(blockIdx.x == 0, a.ctl, 0);
-  for (int b = t; b < kShBins; b += kShBlock) hl[b] = 0u;
-  __syncthreads();
-  const uint32_t N = (uint32_t)a.world * (uint32_t)a.cap;
-  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += gridDim.x * kShBlock * kShPer) {
-    int32_t li[kShPer];
-    float v[kShPer];
-    load_entries(a, e0, N, li, v);
-#pragma unroll
-    for (int u = 0; u < kShPer; ++u)
-      if (e0 + u * kShBlock < N && li[u] >= 0) atomicAdd(&hl[coarse_bin(abs_key(v[u]))], 1u);
+// list entries: plain accesses across a kernel boundary; WT: the cut list, read by the last
+// arriver of the SAME launch -- agent-scope atomics (written through, read past the non-coherent
+// caches)
+template <bool WT>
+__device__ __forceinline__ void put_entry(uint4* d, const uint4& q) {
+  if constexpr (WT) {
+    uint64_t* p = reinterpret_cast<uint64_t*>(d);
+    __hip_atomic_store(p, (uint64_t)q.x | ((uint64_t)q.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, (uint64_t)q.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *d = q;
   }
-  __syncthreads();
-  flush_copy(a.hist, hl);
-  SH_STAMP(blockIdx.x == 0, a.ctl, 1);
+}
+template <bool WT>
+__device__ __forceinline__ uint4 get_entry(const uint4* s) {
+  if constexpr (WT) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(s);
+    const uint64_t q01 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t q23 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)q01, (uint32_t)(q01 >> 32), (uint32_t)q23, 0u);
+  } else {
+    return *s;
+  }
 }
 
-// 3b. the coarse cut: above C1 selected, below rejected; the C1 entries listed and sub-binned
-__global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
-  __shared__ int64_t s_base[kShMaxWorld];
-  __shared__ uint32_t hl[kShBins];
-  __shared__ uint32_t s_w[kShBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_cnt;
+// the coarse histogram of one round of entries (loaded by the caller)
+__device__ __forceinline__ void coarse_round(uint32_t e0, uint32_t N, const int32_t (&li)[kShPer],
+                                             const float (&v)[kShPer], uint32_t* hl) {
+#pragma unroll
+  for (int u = 0; u < kShPer; ++u)
+    if (e0 + u * kShBlock < N && li[u] >= 0) atomicAdd(&hl[coarse_bin(abs_key(v[u]))], 1u);
+}
+
+// the coarse cut over one round = one list block (its entries loaded by the caller): above C1
+// selected, below rejected; the C1 entries counted into the LDS sub-bin histogram hl and compacted
+// into the same block of the C1 list, their count in bcnt -- no global reservation
+__device__ __forceinline__ void apply_round(const ShArgs& a, uint32_t r0, uint32_t N, int c1,
+                                            const int32_t (&li)[kShPer], const float (&v)[kShPer],
+                                            uint32_t* hl, const int64_t* s_base, uint32_t* s_cnt) {
   const int t = threadIdx.x;
-  SH_STAMP(blockIdx.x == 0, a.ctl, 2);
-  for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
-  const uint32_t k = (uint32_t)a.k;
-  uint32_t above, total;
-  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
-  // the first round's entries are loaded before the histogram copies: both in flight together
-  int32_t li[kShPer];
-  float v[kShPer];
-  if (blockIdx.x * kShListBlock < N) load_entries(a, blockIdx.x * kShListBlock + t, N, li, v);
-  const int c1 = find_from_copies(a.hist, hl, k, s_w, s_res, above, total);   // -1: every valid entry selected
-  SH_STAMP(blockIdx.x == 0, a.ctl, 8);
-  if (blockIdx.x == 0) {
-    // the partition every rank planned with vs the shard lengths the records carry
-    uint32_t bad = 0;
-    for (int w = t; w < a.world; w += kShBlock)
-      if ((int64_t)(uint32_t)a.recs[(int64_t)w * a.stride] != a.tab[w]) bad = 1u;
-    if (a.status && bad) __hip_atomic_fetch_or(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (a.status && t == 0 && total < k) __hip_atomic_fetch_or(a.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (t == 0) {   // for shard_bnd (kernel boundary)
-      a.ctl->c1 = c1;
-      a.ctl->need = c1 < 0 ? 0u : k - above;
+  const uint32_t cap = (uint32_t)a.cap;
+  const uint32_t e0 = r0 + t;
+  uint32_t off[kShPer];   // this thread's C1 entries: their place in the block
+#pragma unroll
+  for (int u = 0; u < kShPer; ++u) {
+    const uint32_t e = e0 + u * kShBlock;
+    bool inb = false;
+    if (e < N) {
+      uint32_t w, j;
+      split_entry(e, cap, w, j);
+      if (li[u] < 0) {
+        shard_pad(a, w, j);
+      } else {
+        const uint32_t key = abs_key(v[u]);
+        const int cb = coarse_bin(key);
+        inb = cb == c1;
+        if (inb) atomicAdd(&hl[sub_bin(key)], 1u);
+        else shard_take(a, cb > c1, w, j, li[u], v[u], s_base[w]);
+      }
+    }
+    // C1 entries placed by one LDS atomic per wave
+    const uint64_t m = __ballot(inb);
+    off[u] = ~0u;
+    if (m) {
+      uint32_t base0 = 0;
+      if (lane_rank(m) == 0 && inb) base0 = atomicAdd(s_cnt, (uint32_t)__popcll(m));
+      base0 = __shfl(base0, __builtin_ctzll(m), 64);
+      if (inb) off[u] = base0 + lane_rank(m);
     }
   }
-  __syncthreads();   // every thread has read hl
-  for (int b = t; b < kShBins; b += kShBlock) hl[b] = 0u;
-  if (t == 0) s_cnt = 0u;
-  __syncthreads();
-  // uniform rounds (the workgroup barriers below): every thread runs every round.  A round covers one
-  // list block of kShListBlock entries; its C1 entries go to the same block of the C1 list, compacted,
-  // with their count in bcnt: no global reservation
-  for (uint32_t r0 = blockIdx.x * kShListBlock; r0 < N; r0 += gridDim.x * kShListBlock) {
-    const uint32_t e0 = r0 + t;
-    if (r0 != blockIdx.x * kShListBlock) load_entries(a, e0, N, li, v);
-    uint32_t off[kShPer];   // this thread's C1 entries: their place in the block
 #pragma unroll
-    for (int u = 0; u < kShPer; ++u) {
+  for (int u = 0; u < kShPer; ++u) {
+    if (off[u] != ~0u) {
+      // the entry with its global index and value: the sub-bin pass decides it without going back
+      // to the records (a dependent load chain per entry)
       const uint32_t e = e0 + u * kShBlock;
-      bool inb = false;
-      if (e < N) {
-        uint32_t w, j;
-        split_entry(e, cap, w, j);
-        if (li[u] < 0) {
-          shard_pad(a, w, j);
-        } else {
-          const uint32_t key = abs_key(v[u]);
-          const int cb = coarse_bin(key);
-          inb = cb == c1;
-          if (inb) atomicAdd(&hl[sub_bin(key)], 1u);
-          else shard_take(a, cb > c1, w, j, li[u], v[u], s_base[w]);
-        }
-      }
-      // C1 entries placed by one LDS atomic per wave
-      const uint64_t m = __ballot(inb);
-      off[u] = ~0u;
-      if (m) {
-        uint32_t base0 = 0;
-        if (lane_rank(m) == 0 && inb) base0 = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
-        base0 = __shfl(base0, __builtin_ctzll(m), 64);
-        if (inb) off[u] = base0 + lane_rank(m);
-      }
+      const uint32_t w = e / cap;
+      put_entry<false>(&a.bnd[r0 + off[u]], make_uint4(e, (uint32_t)(s_base[w] + li[u]), f2u(v[u]), 0u));
     }
-#pragma unroll
-    for (int u = 0; u < kShPer; ++u) {
-      if (off[u] != ~0u) {
-        // the entry with its global index and value: shard_bnd decides it without going back to
-        // the records (a dependent load chain per entry); read after the kernel boundary
-        const uint32_t e = e0 + u * kShBlock;
-        const uint32_t w = e / cap;
-        a.bnd[r0 + off[u]] = make_uint4(e, (uint32_t)(s_base[w] + li[u]), f2u(v[u]), 0u);
-      }
-    }
-    __syncthreads();
-    if (t == 0) {
-      a.bcnt[r0 / kShListBlock] = s_cnt;
-#ifdef GRACE_STAMPS
-      atomicAdd(&a.ctl->nb, s_cnt);   // diagnostic: the C1 list's length (ctl slot 12)
-#endif
-      s_cnt = 0u;
-    }
-    __syncthreads();
   }
-  SH_STAMP(blockIdx.x == 0, a.ctl, 9);
-  flush_copy(a.hist2, hl);
-  SH_STAMP(blockIdx.x == 0, a.ctl, 3);
+  __syncthreads();
+  if (t == 0) {
+    a.bcnt[r0 / kShListBlock] = *s_cnt;
+#ifdef GRACE_STAMPS
+    atomicAdd(&a.ctl->nb, *s_cnt);   // diagnostic: the C1 list's length (ctl slot 12)
+#endif
+    *s_cnt = 0u;
+  }
+  __syncthreads();
 }
 
-// 3c. the sub-bin cut over the C1 list in parallel; the last arriver ranks the cut sub-bin
-__global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
-  static_assert(kShPairCap <= kShBlock, "the pairwise ranking holds one cut entry per thread");
-  __shared__ int64_t s_base[kShMaxWorld];
-  __shared__ uint32_t hl[kShBins];
-  __shared__ uint64_t s_comp[kShPairCap];
-  __shared__ uint32_t s_w[kShBlock / kWave + 1];
-  __shared__ uint32_t s_res[2];
-  __shared__ uint32_t s_cnt, s_gbase, s_last;
+// the sub-bin cut over one block of the C1 list (its count and entries loaded by the caller): the
+// entries outside the cut sub-bin b2 decided; the b2 entries appended, whole, to the cut list
+// (write-through for the last arriver)
+__device__ __forceinline__ void bnd_round(const ShArgs& a, uint32_t cnt_b, const uint4 (&q4)[kShPer], int b2,
+                                          const int64_t* s_base, uint32_t* s_cnt, uint32_t* s_gbase) {
   const int t = threadIdx.x;
-  SH_STAMP(blockIdx.x == 0, a.ctl, 4);
-  for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
-  const uint32_t need = a.ctl->need;   // kernel boundary: plain loads
-  if (t == 0) s_cnt = 0u;
-  const uint32_t cap = (uint32_t)a.cap, N = (uint32_t)a.world * cap;
-  const uint32_t nblk = (N + kShListBlock - 1) / kShListBlock;
-  // the first list block is loaded before the histogram copies: both in flight together
-  uint32_t cnt_b = 0;
-  uint4 q4[kShPer];
-  if (blockIdx.x < nblk) {
-    cnt_b = a.bcnt[blockIdx.x];
+  const uint32_t cap = (uint32_t)a.cap;
+  uint32_t off[kShPer];   // this thread's cut entries: their place in the workgroup's share
 #pragma unroll
-    for (int u = 0; u < kShPer; ++u)   // unconditional (the list is whole blocks long)
-      q4[u] = a.bnd[blockIdx.x * kShListBlock + t + u * kShBlock];
+  for (int u = 0; u < kShPer; ++u) {
+    bool in2 = false;
+    if (t + u * kShBlock < cnt_b) {
+      uint32_t w, j;
+      split_entry(q4[u].x, cap, w, j);
+      const float v = u2f(q4[u].z);
+      const int sb = sub_bin(abs_key(v));
+      in2 = sb == b2;
+      if (!in2) shard_take(a, sb > b2, w, j, (int32_t)((int64_t)q4[u].y - s_base[w]), v, s_base[w]);
+    }
+    const uint64_t m = __ballot(in2);
+    off[u] = ~0u;
+    if (m) {
+      uint32_t base0 = 0;
+      if (lane_rank(m) == 0 && in2) base0 = atomicAdd(s_cnt, (uint32_t)__popcll(m));
+      base0 = __shfl(base0, __builtin_ctzll(m), 64);
+      if (in2) off[u] = base0 + lane_rank(m);
+    }
   }
-  // b2: the sub-bin of the cut within C1; kShBins (need == 0): every C1 entry is rejected, -1 (need
-  // above the C1 count): every C1 entry is selected
-  uint32_t above2, total2;
-  const int b2 = find_from_copies(a.hist2, hl, need, s_w, s_res, above2, total2);
-  const uint32_t need2 = b2 >= 0 && b2 < kShBins ? need - above2 : 0u;
-  SH_STAMP(blockIdx.x == 0, a.ctl, 10);
-  for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // uniform rounds: one list block each
-    const uint32_t r0 = blk * kShListBlock;
-    if (blk != blockIdx.x) {
-      cnt_b = a.bcnt[blk];
-#pragma unroll
-      for (int u = 0; u < kShPer; ++u) q4[u] = a.bnd[r0 + t + u * kShBlock];   // in flight with cnt_b
-    }
-    uint32_t off[kShPer];   // this thread's cut entries: their place in the workgroup's share
-#pragma unroll
-    for (int u = 0; u < kShPer; ++u) {
-      bool in2 = false;
-      if (t + u * kShBlock < cnt_b) {
-        uint32_t w, j;
-        split_entry(q4[u].x, cap, w, j);
-        const float v = u2f(q4[u].z);
-        const int sb = sub_bin(abs_key(v));
-        in2 = sb == b2;
-        if (!in2) shard_take(a, sb > b2, w, j, (int32_t)((int64_t)q4[u].y - s_base[w]), v, s_base[w]);
-      }
-      const uint64_t m = __ballot(in2);
-      off[u] = ~0u;
-      if (m) {
-        uint32_t base0 = 0;
-        if (lane_rank(m) == 0 && in2) base0 = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
-        base0 = __shfl(base0, __builtin_ctzll(m), 64);
-        if (in2) off[u] = base0 + lane_rank(m);
-      }
-    }
-    __syncthreads();
-    const uint32_t cnt = s_cnt;
-    if (t == 0 && cnt) s_gbase = atomicAdd(&a.ctl->n2, cnt);
-    __syncthreads();
-    // the whole entry (entry number, global index, value bits) from registers, write-through (sc1)
-    // for the last arriver, which then ranks and decides from the list alone
-#pragma unroll
-    for (int u = 0; u < kShPer; ++u) {
-      if (off[u] != ~0u) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(&a.bnd2[s_gbase + off[u]]);
-        __hip_atomic_store(d, (uint64_t)q4[u].x | ((uint64_t)q4[u].y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 1, (uint64_t)q4[u].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    if (t == 0) s_cnt = 0u;
-    __syncthreads();
-  }
-  // the coarse histogram's copies were last read by shard_apply: re-zeroed here by every workgroup
-  // (the sub-bin copies, read above, by the last arriver)
-  for (int b = blockIdx.x * kShBlock + t; b < kShGroups * kShBins; b += gridDim.x * kShBlock) a.hist[b] = 0u;
-  // arrival (DESIGN §4 memory-model table, row 1: write-through stores, vmcnt(0), barrier, ticket)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  SH_STAMP(blockIdx.x == 0, a.ctl, 5);
-  if (t == 0) s_last = atomicAdd(&a.ctl->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  const uint32_t cnt = *s_cnt;
+  if (t == 0 && cnt) *s_gbase = atomicAdd(&a.ctl->n2, cnt);
   __syncthreads();
-  if (!s_last) return;
-  SH_STAMP(true, a.ctl, 6);
+#pragma unroll
+  for (int u = 0; u < kShPer; ++u)
+    if (off[u] != ~0u) put_entry<true>(&a.bnd2[*s_gbase + off[u]], q4[u]);
+  __syncthreads();
+  if (t == 0) *s_cnt = 0u;
+  __syncthreads();
+}
+
+// the last arriver: the cut sub-bin's entries ranked exactly by the composite (key, global index),
+// the need2 highest selected; then the sub-bin histogram copies re-zeroed
+__device__ __forceinline__ void rank_cut(const ShArgs& a, uint32_t need2, const int64_t* s_base, uint64_t* s_comp,
+                                         uint32_t* hl, uint32_t* s_w, uint32_t* s_res) {
+  const int t = threadIdx.x;
+  const uint32_t cap = (uint32_t)a.cap;
   // the counter and, below, the cut list are read with agent-scope atomic loads (as they were
   // written): no acquire fence on the common path
   const uint32_t n2 = __hip_atomic_load(&a.ctl->n2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -402,21 +340,16 @@ __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
     x = u2f(q.z);
   };
   if (n2 <= (uint32_t)kShPairCap) {
-    // rank the cut sub-bin's entries pairwise (unique composites): the need2 highest are selected;
-    // one entry per thread, kept in registers
-    // unconditional (the list is whole blocks long): in flight with n2
-    uint64_t* qp = reinterpret_cast<uint64_t*>(&a.bnd2[t]);
-    const uint64_t q01 = __hip_atomic_load(qp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t q23 = __hip_atomic_load(qp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint4 q = make_uint4((uint32_t)q01, (uint32_t)(q01 >> 32), (uint32_t)q23, 0u);
+    // rank pairwise (unique composites); one entry per thread, kept in registers, loaded
+    // unconditionally (the list is whole blocks long): in flight with n2
+    const uint4 q = get_entry<true>(&a.bnd2[t]);
     if ((uint32_t)t < n2) s_comp[t] = comp_key(abs_key(u2f(q.z)), q.y);
     __syncthreads();
     if ((uint32_t)t < n2) {
       const uint64_t me = s_comp[t];
       uint32_t rk = 0;
       uint32_t o = 0;
-      // 8 LDS reads in flight per step (one at a time, the loop waited an LDS latency per entry:
-      // 5 us at n2 = 225)
+      // 8 LDS reads in flight per step (one at a time, the loop waited an LDS latency per entry)
       for (; o + 8 <= n2; o += 8) {
         uint64_t c[8];
 #pragma unroll
@@ -452,8 +385,6 @@ __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
     }
   }
   SH_STAMP(true, a.ctl, 14);
-  // every launch before has finished and every workgroup of this one has arrived: re-zero the
-  // sub-bin histogram copies and the counters for the next call
   for (int b = t; b < kShGroups * kShBins; b += kShBlock) a.hist2[b] = 0u;
   if (t == 0) {
 #ifdef GRACE_STAMPS
@@ -462,8 +393,128 @@ __global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
 #endif
     a.ctl->nb = 0u;
     a.ctl->n2 = 0u;
-    a.ctl->ticket = 0u;
   }
+}
+
+// the partition every rank planned with vs the shard lengths the records carry (status bit 1),
+// and fewer valid entries than k (bit 2)
+__device__ __forceinline__ void check_records(const ShArgs& a, uint32_t total) {
+  const int t = threadIdx.x;
+  uint32_t bad = 0;
+  for (int w = t; w < a.world; w += kShBlock)
+    if ((int64_t)(uint32_t)a.recs[(int64_t)w * a.stride] != a.tab[w]) bad = 1u;
+  if (a.status && bad) __hip_atomic_fetch_or(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.status && t == 0 && total < (uint32_t)a.k) __hip_atomic_fetch_or(a.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 3a. the coarse histogram (key >> 20) of the valid gathered entries
+__global__ __launch_bounds__(kShBlock) void shard_coarse_kernel(ShArgs a) {
+  __shared__ uint32_t hl[kShBins];
+  const int t = threadIdx.x;
+  SH_STAMP(blockIdx.x == 0, a.ctl, 0);
+  for (int b = t; b < kShBins; b += kShBlock) hl[b] = 0u;
+  __syncthreads();
+  const uint32_t N = (uint32_t)a.world * (uint32_t)a.cap;
+  for (uint32_t e0 = blockIdx.x * kShBlock * kShPer + t; e0 < N; e0 += gridDim.x * kShBlock * kShPer) {
+    int32_t li[kShPer];
+    float v[kShPer];
+    load_entries(a, e0, N, li, v);
+    coarse_round(e0, N, li, v, hl);
+  }
+  __syncthreads();
+  flush_copy(a.hist, hl);
+  SH_STAMP(blockIdx.x == 0, a.ctl, 1);
+}
+
+// 3b. the coarse cut: above C1 selected, below rejected; the C1 entries listed and sub-binned
+__global__ __launch_bounds__(kShBlock) void shard_apply_kernel(ShArgs a) {
+  __shared__ int64_t s_base[kShMaxWorld];
+  __shared__ uint32_t hl[kShBins];
+  __shared__ uint32_t s_w[kShBlock / kWave + 1];
+  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_cnt;
+  const int t = threadIdx.x;
+  SH_STAMP(blockIdx.x == 0, a.ctl, 2);
+  for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
+  const uint32_t k = (uint32_t)a.k;
+  uint32_t above, total;
+  const uint32_t N = (uint32_t)a.world * (uint32_t)a.cap;
+  // the first round's entries are loaded before the histogram copies: both in flight together
+  int32_t li[kShPer];
+  float v[kShPer];
+  if (blockIdx.x * kShListBlock < N) load_entries(a, blockIdx.x * kShListBlock + t, N, li, v);
+  const int c1 = find_from_copies(a.hist, hl, k, s_w, s_res, above, total);   // -1: every valid entry selected
+  SH_STAMP(blockIdx.x == 0, a.ctl, 8);
+  if (blockIdx.x == 0) {
+    check_records(a, total);
+    if (t == 0) a.ctl->need = c1 < 0 ? 0u : k - above;   // for shard_bnd (kernel boundary)
+  }
+  __syncthreads();   // every thread has read hl
+  for (int b = t; b < kShBins; b += kShBlock) hl[b] = 0u;
+  if (t == 0) s_cnt = 0u;
+  __syncthreads();
+  // uniform rounds (the workgroup barriers inside): every thread runs every round
+  for (uint32_t r0 = blockIdx.x * kShListBlock; r0 < N; r0 += gridDim.x * kShListBlock) {
+    if (r0 != blockIdx.x * kShListBlock) load_entries(a, r0 + t, N, li, v);
+    apply_round(a, r0, N, c1, li, v, hl, s_base, &s_cnt);
+  }
+  SH_STAMP(blockIdx.x == 0, a.ctl, 9);
+  flush_copy(a.hist2, hl);
+  SH_STAMP(blockIdx.x == 0, a.ctl, 3);
+}
+
+// 3c. the sub-bin cut over the C1 list in parallel; the last arriver ranks the cut sub-bin
+__global__ __launch_bounds__(kShBlock) void shard_bnd_kernel(ShArgs a) {
+  static_assert(kShPairCap <= kShBlock, "the pairwise ranking holds one cut entry per thread");
+  __shared__ int64_t s_base[kShMaxWorld];
+  __shared__ uint32_t hl[kShBins];
+  __shared__ uint64_t s_comp[kShPairCap];
+  __shared__ uint32_t s_w[kShBlock / kWave + 1];
+  __shared__ uint32_t s_res[2];
+  __shared__ uint32_t s_cnt, s_gbase, s_last;
+  const int t = threadIdx.x;
+  SH_STAMP(blockIdx.x == 0, a.ctl, 4);
+  for (int w = t; w < a.world; w += kShBlock) s_base[w] = a.tab[a.world + w];
+  const uint32_t need = a.ctl->need;   // kernel boundary: plain loads
+  if (t == 0) s_cnt = 0u;
+  const uint32_t N = (uint32_t)a.world * (uint32_t)a.cap;
+  const uint32_t nblk = (N + kShListBlock - 1) / kShListBlock;
+  // the first list block is loaded before the histogram copies: both in flight together
+  uint32_t cnt_b = 0;
+  uint4 q4[kShPer];
+  if (blockIdx.x < nblk) {
+    cnt_b = a.bcnt[blockIdx.x];
+#pragma unroll
+    for (int u = 0; u < kShPer; ++u)   // unconditional (the list is whole blocks long)
+      q4[u] = a.bnd[blockIdx.x * kShListBlock + t + u * kShBlock];
+  }
+  // b2: the sub-bin of the cut within C1; kShBins (need == 0): every C1 entry is rejected, -1 (need
+  // above the C1 count): every C1 entry is selected
+  uint32_t above2, total2;
+  const int b2 = find_from_copies(a.hist2, hl, need, s_w, s_res, above2, total2);
+  const uint32_t need2 = b2 >= 0 && b2 < kShBins ? need - above2 : 0u;
+  SH_STAMP(blockIdx.x == 0, a.ctl, 10);
+  for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {   // uniform rounds: one list block each
+    if (blk != blockIdx.x) {
+      cnt_b = a.bcnt[blk];
+#pragma unroll
+      for (int u = 0; u < kShPer; ++u) q4[u] = a.bnd[blk * kShListBlock + t + u * kShBlock];   // in flight with cnt_b
+    }
+    bnd_round(a, cnt_b, q4, b2, s_base, &s_cnt, &s_gbase);
+  }
+  // the coarse histogram's copies were last read by shard_apply: re-zeroed here by every workgroup
+  // (the sub-bin copies, read above, by the last arriver)
+  for (int b = blockIdx.x * kShBlock + t; b < kShGroups * kShBins; b += gridDim.x * kShBlock) a.hist[b] = 0u;
+  // arrival (DESIGN §4 memory-model table, row 1: write-through stores, vmcnt(0), barrier, ticket)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  SH_STAMP(blockIdx.x == 0, a.ctl, 5);
+  if (t == 0) s_last = atomicAdd(&a.ctl->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  SH_STAMP(true, a.ctl, 6);
+  rank_cut(a, need2, s_base, s_comp, hl, s_w, s_res);
+  if (t == 0) a.ctl->ticket = 0u;
   SH_STAMP(true, a.ctl, 7);
 }
 

@@ -81,10 +81,10 @@ for step in range(6):
         ws = ops.workspace("shardsel", ops._lib.query("grace_shard_select_workspace_bytes", W, cap), dev)
         sv = ws[64:256].cpu().numpy().view(np.uint64)
         us = lambda a, b: round((int(sv[b]) - int(sv[a])) / 100.0, 1)   # noqa: E731
+        nbv = ws[64 + 8 * 12:64 + 8 * 13].cpu().numpy().view(np.uint32)
         print(f"step {step} select stamps, us from the coarse launch's start (workgroup 0 unless noted): "
               f"coarse {us(0, 1)}, boundary {us(1, 2)}, apply {us(2, 3)}, boundary {us(3, 4)}, bnd to arrival "
               f"{us(4, 5)}, to the last arriver {us(5, 6)}, its ranking {us(6, 7)}; total {us(0, 7)}")
-        nbv = ws[64 + 8 * 12:64 + 8 * 13].cpu().numpy().view(np.uint32)
         print(f"  apply: find c1 {us(2, 8)}, round {us(8, 9)}, flush {us(9, 3)}; bnd: find b2 {us(4, 10)}, "
               f"rounds to arrival {us(10, 5)}; last arriver: load+pairwise {us(6, 13)}, decisions {us(13, 14)}, "
               f"re-zero {us(14, 7)}; nb {int(nbv[0])} n2 {int(nbv[1])}")
