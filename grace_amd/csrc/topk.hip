@@ -144,8 +144,14 @@ constexpr int kSampleMax = GRACE_SAMPLE_MAX;               // stratified sample 
 // A/B at BASELINE configs[4]'s 8.4 M-element shard: one sample per 256 elements, 32 K instead of
 // 131 K, took the bracket from 16.6 to 14.1 us but doubled the candidates, finalize 11.8 -> 17.0
 // us: local step 59.5 -> 58.7 us, within the spread -- the bracket's cost is its fixed LDS zeroing,
-// flush and fan-in, not its random reads.)
-__host__ __device__ inline int64_t bracket_sample_n(int64_t n) { return n < kSampleMax ? n : kSampleMax; }
+// flush and fan-in, not its random reads.)  r06, same shard, one box, two runs each: 64 K samples
+// 54.0 / 54.4 us, 32 K 54.6 / 54.8, 131 K 55.6 / 56.6 (profiles/r06_sample_ab.txt) -- while at the
+// 2^26-element headline 64 K costs +3 us: half the sample up to 2^24 elements.
+constexpr int64_t kHalfSampleMaxN = (int64_t)1 << 24;
+__host__ __device__ inline int64_t bracket_sample_n(int64_t n) {
+  const int64_t cap = n <= kHalfSampleMaxN ? kSampleMax / 2 : kSampleMax;
+  return n < cap ? n : cap;
+}
 constexpr int kSampleBlock = 1024;
 #ifndef GRACE_BRACKET_BLOCK
 #define GRACE_BRACKET_BLOCK 1024
@@ -169,6 +175,13 @@ constexpr int kCoarseBins = 2048;                          // key >> 20: 1/8-oct
 #endif
 constexpr bool kMainSearch = GRACE_MAIN_SEARCH != 0;       // the bracket's search in the main pass
 constexpr int kHistStride = 1;
+// copies of the bracket's sample histograms (workgroup b flushes into copy b % kSampleCopies; the
+// search sums them): same-address device atomics serialise, and every sampling workgroup adds to
+// the same popular bins
+#ifndef GRACE_SAMPLE_COPIES
+#define GRACE_SAMPLE_COPIES 1
+#endif
+constexpr int kSampleCopies = GRACE_SAMPLE_COPIES;
 
 // Workspace layout.  Every counter / histogram region is left zeroed by the step that used it
 // (the select kernel re-zeroes what the next step accumulates into), so the caller only has to
@@ -215,9 +228,9 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
   w.hist = reinterpret_cast<uint32_t*>(p);
   p += align256(sizeof(uint32_t) * kHistBins * kHistStride);
   w.chist = reinterpret_cast<uint32_t*>(p);
-  p += align256(sizeof(uint32_t) * kCoarseBins);
+  p += align256(sizeof(uint32_t) * kCoarseBins * kSampleCopies);
   w.shist = reinterpret_cast<uint32_t*>(p);
-  p += align256(sizeof(uint32_t) * kBracketBins);
+  p += align256(sizeof(uint32_t) * kBracketBins * kSampleCopies);
   w.cand = reinterpret_cast<int2*>(p);
   p += align256(sizeof(int2) * w.cap);
   w.bnd = reinterpret_cast<int2*>(p);
@@ -229,7 +242,8 @@ static TopkWs carve(void* ws, int64_t n, int64_t k) {
 static size_t ws_bytes(int64_t n, int64_t k) {
   const int64_t cap = topk_cap(n, k);
   return 256 + align256(sizeof(uint32_t) * kHistBins * kHistStride) +
-         align256(sizeof(uint32_t) * kCoarseBins) + align256(sizeof(uint32_t) * kBracketBins) +
+         align256(sizeof(uint32_t) * kCoarseBins * kSampleCopies) +
+         align256(sizeof(uint32_t) * kBracketBins * kSampleCopies) +
          2 * align256(sizeof(int2) * cap) + align256(sizeof(uint32_t) * kFbWordsHost);
 }
 
@@ -470,7 +484,13 @@ __device__ __forceinline__ BracketThr bracket_search(const StepArgs& a, const To
   uint32_t hc[kCPT], hs = 0;
 #pragma unroll
   for (int c = 0; c < kCPT; ++c) {
-    hc[c] = __hip_atomic_load(w.chist + top - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t x[kSampleCopies];
+#pragma unroll
+    for (int q = 0; q < kSampleCopies; ++q)
+      x[q] = __hip_atomic_load(w.chist + q * kCoarseBins + top - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hc[c] = 0;
+#pragma unroll
+    for (int q = 0; q < kSampleCopies; ++q) hc[c] += x[q];
     hs += hc[c];
   }
   if (tid < 6) s_fc[tid] = 0;
@@ -494,7 +514,15 @@ __device__ __forceinline__ BracketThr bracket_search(const StepArgs& a, const To
     const int q = tid >> 4, j = tid & 15;
     const bool act = q < 3;
     const uint32_t bin = act ? s_fc[2 * q] * 16 + (15 - j) : 0u;
-    uint32_t v = act ? __hip_atomic_load(w.shist + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t v = 0u;
+    if (act) {
+      uint32_t x[kSampleCopies];
+#pragma unroll
+      for (int c = 0; c < kSampleCopies; ++c)
+        x[c] = __hip_atomic_load(w.shist + c * kBracketBins + bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int c = 0; c < kSampleCopies; ++c) v += x[c];
+    }
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) {
       const uint32_t u = __shfl_up(v, o, 16);
@@ -611,10 +639,11 @@ __global__ __launch_bounds__(kBracketBlock) void topk_bracket(StepArgs a, TopkWs
     }
   }
   __syncthreads();
+  const int cp = (int)(blockIdx.x % kSampleCopies);
   for (int b = tid; b < kBracketBins; b += kBracketBlock)
-    if (lh[b]) atomicAdd(&w.shist[b], lh[b]);
+    if (lh[b]) atomicAdd(&w.shist[cp * kBracketBins + b], lh[b]);
   for (int b = tid; b < kCoarseBins; b += kBracketBlock)
-    if (lc[b]) atomicAdd(&w.chist[b], lc[b]);
+    if (lc[b]) atomicAdd(&w.chist[cp * kCoarseBins + b], lc[b]);
   STAMP(w.ctl, 2);
   // kMainSearch: no last arriver here -- every main-pass workgroup runs the search itself, a kernel
   // boundary later (the tail of waiting for the last sampler and one workgroup's search leaves the
@@ -1800,14 +1829,15 @@ __device__ bool finalize_run(const StepArgs& a, const TopkWs& w, int fi, int fcn
      // (agent scope): the parallel fallback below accumulates into this memory with device
      // atomics in the same launch, which a dirty zero line left in some XCD's L2 would overwrite.
      // 16-B sc1 buffer stores: one fabric write per 16 B
-    constexpr int kZ4 = (kBracketBins + kCoarseBins) / 4;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(w.shist, (short)0, kBracketBins * 4, 0x00020000);
-    const auto rc = __builtin_amdgcn_make_buffer_rsrc(w.chist, (short)0, kCoarseBins * 4, 0x00020000);
+    constexpr int kS4 = kBracketBins * kSampleCopies / 4;
+    constexpr int kZ4 = kS4 + kCoarseBins * kSampleCopies / 4;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(w.shist, (short)0, kS4 * 16, 0x00020000);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(w.chist, (short)0, (kZ4 - kS4) * 16, 0x00020000);
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v zero = {0.f, 0.f, 0.f, 0.f};
     for (int z = fi * BLOCK + t; w.shist && z < kZ4; z += fcnt * BLOCK) {
-      if (z < kBracketBins / 4) __builtin_amdgcn_raw_buffer_store_b128(zero, rs, z * 16, 0, 16);
-      else __builtin_amdgcn_raw_buffer_store_b128(zero, rc, (z - kBracketBins / 4) * 16, 0, 16);
+      if (z < kS4) __builtin_amdgcn_raw_buffer_store_b128(zero, rs, z * 16, 0, 16);
+      else __builtin_amdgcn_raw_buffer_store_b128(zero, rc, (z - kS4) * 16, 0, 16);
     }
   }
   // every finalize workgroup: the parallel fallback (slices claimed, so no co-residency needed);
@@ -2021,8 +2051,8 @@ static grace_status_t run_topk(StepArgs a, void* ws, size_t bytes, hipStream_t s
   // >= 33 sample workgroups (n > kSmallN): the first two zero the candidate histogram
   static_assert(kSmallN >= kHistBins, "bracket grid covers the histogram zeroing");
   // runs of kBracketRun samples only when the sample tiles the bucket into whole runs
-  static_assert(kSampleMax % (kBracketRun * kBracketBlock) == 0, "sample runs tile the grid");
-  if (kBracketRun > 1 && a.sample_n != kSampleMax) {
+  static_assert((kSampleMax / 2) % (kBracketRun * kBracketBlock) == 0, "sample runs tile the grid");
+  if (kBracketRun > 1 && a.sample_n < kSampleMax / 2) {
     set_error_msg("grace_topk: sample runs need n >= the sample size (A/B build)");
     return GRACE_ERR_ARG;
   }

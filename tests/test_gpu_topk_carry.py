@@ -21,7 +21,7 @@ def _np(t):
 
 def sample_positions(n):
     """The bracket's stratified sample positions (topk.hip sample_pos), restated in numpy."""
-    sn = min(n, SAMPLE_MAX)
+    sn = min(n, SAMPLE_MAX // 2 if n <= (1 << 24) else SAMPLE_MAX)   # topk.hip bracket_sample_n
     st = n // sn
     s = np.arange(sn, dtype=np.uint64)
     x = ((s * np.uint64(0x9E3779B9) + np.uint64(0x5EED)) & np.uint64(0xFFFFFFFF)).astype(np.uint64)

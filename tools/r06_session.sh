@@ -81,12 +81,14 @@ for s in "$@"; do
                run shard_new_$i 180 python3 tools/exp_shard_local.py 8
              done ;;
     absample) for i in 1 2; do
-                for v in "" _s64k _s32k; do
+                for v in "" _s64k _s32k _c8; do
                   GRACE_HIP_LIB=grace_amd/lib/libgrace_hip$v.so run shard_smp${v}_$i 180 python3 tools/exp_shard_local.py 8
                 done
               done
-              AB_MODES=fused,swap run ab_sample 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
-                grace_amd/lib/libgrace_hip_s64k.so grace_amd/lib/libgrace_hip_s32k.so ;;
+              AB_MODES=fused,swap,nomem_rec run ab_sample 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so \
+                grace_amd/lib/libgrace_hip_s64k.so grace_amd/lib/libgrace_hip_s32k.so grace_amd/lib/libgrace_hip_c8.so ;;
+    smpcheck) for i in 1 2; do run shard_half_$i 180 python3 tools/exp_shard_local.py 8; done
+              AB_MODES=fused,swap,nomem_rec run ab_half 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
