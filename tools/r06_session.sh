@@ -89,6 +89,9 @@ for s in "$@"; do
                 grace_amd/lib/libgrace_hip_s64k.so grace_amd/lib/libgrace_hip_s32k.so grace_amd/lib/libgrace_hip_c8.so ;;
     smpcheck) for i in 1 2; do run shard_half_$i 180 python3 tools/exp_shard_local.py 8; done
               AB_MODES=fused,swap,nomem_rec run ab_half 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so ;;
+    localstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so N=8388608 K=67108 RES_ONLY=1 PATH_KIND=plain \
+                   run stamps_local 120 python3 tools/exp_stamps.py
+                 GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run stamps_head 120 python3 tools/exp_stamps.py ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
