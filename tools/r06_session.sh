@@ -92,6 +92,12 @@ for s in "$@"; do
     localstamps) GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so N=8388608 K=67108 RES_ONLY=1 PATH_KIND=plain \
                    run stamps_local 120 python3 tools/exp_stamps.py
                  GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_stamps.so run stamps_head 120 python3 tools/exp_stamps.py ;;
+    abfin) for i in 1 2; do
+             GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_prefin.so run shard_prefin_$i 180 python3 tools/exp_shard_local.py 8
+             run shard_fin_$i 180 python3 tools/exp_shard_local.py 8
+           done
+           AB_MODES=fused,swap,nomem_rec run ab_fin 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_prefin.so grace_amd/lib/libgrace_hip.so ;;
+    abplace2) run ab_place2 400 python3 tools/ab_place2.py grace_amd/lib/libgrace_hip.so 8 ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
