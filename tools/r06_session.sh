@@ -98,6 +98,15 @@ for s in "$@"; do
            done
            AB_MODES=fused,swap,nomem_rec run ab_fin 400 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_prefin.so grace_amd/lib/libgrace_hip.so ;;
     abplace2) run ab_place2 400 python3 tools/ab_place2.py grace_amd/lib/libgrace_hip.so 8 ;;
+    abgrid) AB_MODES=fused run ab_grid 500 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so grace_amd/lib/libgrace_hip_v16c1k.so \
+              grace_amd/lib/libgrace_hip_v8c1k.so grace_amd/lib/libgrace_hip_v12c1k.so grace_amd/lib/libgrace_hip_v16c2k.so ;;
+    abgrid2) AB_MODES=fused,swap run ab_grid2a 500 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip_v16c1k.so grace_amd/lib/libgrace_hip.so
+             AB_MODES=fused,swap run ab_grid2b 500 python3 tools/ab_v3.py grace_amd/lib/libgrace_hip.so grace_amd/lib/libgrace_hip_v16c1k.so
+             for i in 1 2; do
+               GRACE_HIP_LIB=grace_amd/lib/libgrace_hip_v16c1k.so run bench_v16c1k_$i 300 python3 bench.py --no-cpu-baseline
+               run bench_base_$i 300 python3 bench.py --no-cpu-baseline
+             done ;;
+    abplace3) run ab_place3 500 python3 tools/ab_place3.py grace_amd/lib/libgrace_hip.so 12 ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
