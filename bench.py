@@ -320,7 +320,7 @@ def bench_topk(args, world, rank, dev):
     for i in range(args.warmup):        # warm-up steps, untimed and outside the kernel timer
         step(i)
     rec = comm.compressor._recycler
-    hits0 = rec.hits
+    hits0, dense0 = rec.hits, rec.dense_hits
     ops.timer_enable(True)
     elapsed = timed(step, args.steps, 0, world, dev)
     main_ms, launches = ops.timer_collect()
@@ -329,6 +329,7 @@ def bench_topk(args, world, rank, dev):
     # world 1: each step's result is consumed and dropped, so every timed step reuses its bucket's
     # previous result (ops.OutputRecycler): the main pass writes only its selection into the output
     recycled = world == 1 and rec.hits - hits0 == args.steps
+    kept = world == 1 and rec.dense_hits - dense0 == args.steps
 
     line = base_line(args, world, elapsed, 4.0 * n)
     line["config"] = {"workload": "Allgather(TopK 1%, ResidualMemory).step on a 256 MiB fp32 bucket "
@@ -336,7 +337,14 @@ def bench_topk(args, world, rank, dev):
                       "numel": n, "k": k, "parallelism": f"dp{world} replicas, RCCL allgather of payloads",
                       "output": ("recycled: each step's dropped result is handed back; its k previous non-zeros "
                                  "are cleared and only the new selection is written (bit-identical)")
-                      if recycled else "fresh dense output every step"}
+                      if recycled else ("dense output every step, written in full into the buffer of the bucket's "
+                                        "dropped previous result (kept for its placement, ops.pick_pair)"
+                                        if kept else "fresh dense output every step")}
+    if comm.compressor.place_probes:
+        # per bucket: the streaming probe's microseconds for every (residual, output) allocation pair
+        # tried at its first step; the fastest pair was kept
+        line["config"]["placement_probe_us"] = {nm: [round(x, 1) for x in us]
+                                                for nm, us in comm.compressor.place_probes.items()}
     # roofline of the dominant kernel (topk_main), HIP events on the stream it runs on; only the
     # timed steps are counted (warm-up launches ran with the timer off)
     main_avg_ms = main_ms / max(launches, 1)
@@ -380,7 +388,8 @@ def bench_topk(args, world, rank, dev):
     roofline["measured_copy_kind"] = ("grace_topk_stream_probe: the topk_main kernel itself with the classification "
                                       "compiled out (same grid, chunks, 16-B non-temporal loads / stores of g, r, r'"
                                       + (", out untouched as with the recycled output" if recycled else ", out") +
-                                      ") on 3 rotated 256 MiB buffer sets, each launch interleaved with a real "
+                                      ") on 3 rotated 256 MiB buffer sets (r / out of each placed by ops.pick_pair, "
+                                      "as the engine places its own), each launch interleaved with a real "
                                       "step, dispatch-packet events like the main pass; ceiling = fastest launch")
     roofline["frac_of_measured_copy"] = round(achieved / skel, 4) if skel else None
     roofline["frac_of_measured_copy_median"] = round(achieved / skel_med, 4) if skel_med else None
@@ -434,7 +443,14 @@ def skeleton_ceiling(step, main_bytes, n, dev, sets=3, rounds=12, sparse=False):
     step so it runs at the same clocks, timed with the library's dispatch-packet events exactly as
     the main pass is.  Returns (GB/s of the fastest launch, GB/s of the median launch)."""
     from grace_amd import _lib, ops
-    bufs = [tuple(torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(3)) for _ in range(sets)]
+    bufs = []
+    for _ in range(sets):
+        g = torch.zeros(n, dtype=torch.float32, device=dev)
+        # r and out placed as the engine places its own (ops.pick_pair), so the ceiling is the
+        # best-placed layout's, not a chance placement's
+        r, o = ops.pick_pair(g)[:2] if ops.PLACE_PROBE and n >= ops.PLACE_MIN_N else (torch.zeros_like(g),
+                                                                                        torch.zeros_like(g))
+        bufs.append((g, r, o))
     ws = torch.zeros(int(_lib.query("grace_topk_stream_probe_workspace_bytes", n)), dtype=torch.uint8, device=dev)
     ts = []
     for i in range(rounds + sets):

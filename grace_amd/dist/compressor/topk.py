@@ -33,6 +33,7 @@ class TopKCompressor(Compressor):
         # recycle_output="always" turns it on there as well, False everywhere off.
         self.recycle_output = recycle_output
         self._recycler = ops.OutputRecycler()
+        self.place_probes = {}   # name -> probe microseconds per (residual, output) pair tried (diagnostic)
 
     def compress(self, tensor, name):
         flat = ops.dev_f32(tensor)
@@ -93,15 +94,26 @@ class TopKCompressor(Compressor):
         carry, carry_valid = mem.carry_for(name, res, has, k)
         if world == 1:
             recycle = self.recycle_output == "always" and n > ops.TOPK_SMALL_N
+            # a large bucket's first step takes the residual and output allocations that stream fastest
+            # together (ops.pick_pair: the pair of allocations decides the main pass's rate); the name
+            # keeps that output buffer (its dropped previous result comes back, rewritten densely)
+            place = (not recycle and self.recycle_output is not False and ops.PLACE_PROBE
+                     and n >= ops.PLACE_MIN_N)
             if recycle:
                 out, prev_idx = self._recycler.take(name, g)
+            elif place:
+                out, _ = self._recycler.take(name, g, dense=True)
+                prev_idx = None   # dense rewrite: every element of out is written
             else:
                 out, prev_idx = torch.empty_like(g), None
+            if place and not has:
+                res, out, self.place_probes[name] = ops.pick_pair(g)
+                carry, carry_valid = mem.carry_for(name, res, has, k)
             _, _, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out, carry=carry,
                                                carry_valid=carry_valid, prev_idx=prev_idx)
             mem.residuals[name] = res
             mem.carry_written(name, res, carry)
-            if recycle:
+            if recycle or place:
                 self._recycler.keep(name, out, idx)
             return out.view(tensor.shape)   # (0 + d) / 1: the fused kernel writes exactly this
         # world > 1: the new residual goes to a second buffer (no dense output to park t in), so the

@@ -159,12 +159,15 @@ class OutputRecycler:
     def __init__(self):
         self._hit = {}
         self.hits = 0      # steps that got their previous result back (sparse write)
+        self.dense_hits = 0   # steps that got it back to rewrite densely (take(dense=True))
         self.misses = 0    # steps that allocated (first step, result held / edited, other stream)
 
-    def take(self, name, like, alloc=True):
+    def take(self, name, like, alloc=True, dense=False):
         """(out tensor, prev_idx or None) for the next step of `name` shaped like `like` (a tensor, or
         a (numel, device) pair for an f32 vector).  A miss allocates (torch.empty_like) unless
-        alloc=False, which returns (None, None) and leaves the allocation to the caller."""
+        alloc=False, which returns (None, None) and leaves the allocation to the caller.  dense=True:
+        the caller rewrites every element (the buffer is kept for its placement, not to skip
+        writes); such hits are counted in dense_hits."""
         numel, device = (like.numel(), like.device) if isinstance(like, torch.Tensor) else (int(like[0]), like[1])
         hit = self._hit.pop(name, None)
         if hit is not None:
@@ -172,7 +175,10 @@ class OutputRecycler:
             # references to buf: the popped tuple, the local name, getrefcount's argument
             if (REUSE_OK and key == (numel, torch.device(device), _stream()) and _getrefcount(buf) == 3
                     and _storage_uses(cdata) == 2 and buf._version == version):
-                self.hits += 1
+                if dense:
+                    self.dense_hits += 1
+                else:
+                    self.hits += 1
                 return buf, prev_idx
         self.misses += 1
         if not alloc:
@@ -362,6 +368,46 @@ def topk_fallback_spin_limit(limit=-1):
 def topk_workspace(n, k, device):
     _topk_status()
     return workspace("topk", _lib.query("grace_topk_workspace_bytes", n, k), device)
+
+
+# Buffer placement (r06): on MI355X the fused step's main pass (g, r read; r', out
+# written) runs at 171-174 us or at 184-193 us on a 256 MiB bucket depending on WHICH pair of
+# allocations holds r and out -- a property of the pair, not of offsets inside them
+# (profiles/r06_place4_5.txt).  At a large bucket's first step, pick_pair tries a few residual and
+# output allocations against the step's gradient with the pass's own streaming skeleton
+# (grace_topk_stream_probe) and keeps the fastest pair; the output buffer then stays with the name
+# (the dropped previous result comes back and is rewritten densely).  One host synchronisation per
+# name; GRACE_PLACE_PROBE=0 turns it off.
+PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
+PLACE_MIN_N = 1 << 24
+PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "4"))
+PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "2"))
+
+
+def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
+    """(residual, output, probe microseconds per pair): the fastest of n_res x n_out fresh
+    allocation pairs under the stream probe over g (their contents are garbage: the caller's first
+    step writes both densely)."""
+    g = dev_f32(g)
+    n = g.numel()
+    ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
+    rs = [torch.empty_like(g) for _ in range(n_res)]
+    outs = [torch.empty_like(g) for _ in range(n_out)]
+    pairs = [(i, j) for j in range(n_out) for i in range(n_res)]
+    evs = []
+    for i, j in pairs:
+        for rep in range(2):   # the second launch is timed (first-touch costs out of the figure)
+            if rep == 1:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            _lib.call("grace_topk_stream_probe", _p(g), _p(rs[i]), _p(outs[j]), n, 0, _p(ws), ws.numel(), _stream())
+        e1.record()
+        evs.append((e0, e1))
+    evs[-1][1].synchronize()
+    us = [a.elapsed_time(b) * 1e3 for a, b in evs]
+    best = min(range(len(pairs)), key=lambda q: us[q])
+    i, j = pairs[best]
+    return rs[i], outs[j], us
 
 
 def new_payload(k, device):
