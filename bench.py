@@ -969,6 +969,10 @@ def bench_sparse(args, world, rank, dev):
             # k written (4 B each), the drawn indices written and read back (8 B each with grouping)
             k = ops_ratio_k(n, args.ratio)
             alg = 12.0 * n + 16.0 * k
+    if args.workload == "threshold" and getattr(comp, "place_probes", None):
+        line["config"]["output"] = ("dense every step, written in full into the bucket's kept buffer (residual / "
+                                    "output allocation pair placed by ops.pick_pair)")
+        line["config"]["placement_probe_us"] = {nm: [round(x, 1) for x in us] for nm, us in comp.place_probes.items()}
     traffic, ratio, tsrc = pmc_traffic(args.workload, alg, mode=mode)
     line["roofline"] = {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,

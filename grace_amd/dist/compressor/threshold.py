@@ -43,6 +43,10 @@ class ThresholdCompressor(Compressor):
         self.capacity = {}        # name -> exchange capacity (entries per rank)
         self._pending = {}        # name -> (pinned stat, event) of a deferred step
         self.overflows = 0        # capacity overflows seen (retried or deferred)
+        # world-1 residual step on a large bucket: the residual / output allocation pair probed at
+        # the first step and the output kept (rewritten in full), as TopKCompressor does (ops.pick_pair)
+        self._recycler = ops.OutputRecycler()
+        self.place_probes = {}
 
     def compress(self, tensor, name):
         values, indices = ops.threshold_compress(tensor, self.threshold)
@@ -118,15 +122,21 @@ class ThresholdCompressor(Compressor):
             # world 1: no payload at all -- t and the bound's statistics from one read, then one pass
             # for out = (0 + decompress) / 1 and r = t - decompress (grace_threshold_step_w1)
             ws = ops.workspace("threshold", _lib.query("grace_threshold_workspace_bytes", n), dev)
-            out = torch.empty_like(g)
+            place = residual and ops.PLACE_PROBE and n >= ops.PLACE_MIN_N
+            out = self._recycler.take(name, g, dense=True)[0] if place else torch.empty_like(g)
             if residual:
                 r = mem.residuals.get(name)
                 has = r is not None and r.numel() == n and r.device == dev and r.is_contiguous()
-                buf = r.reshape(-1) if has else torch.empty_like(g)
+                if not has and place:
+                    buf, out, self.place_probes[name] = ops.pick_pair(g)
+                else:
+                    buf = r.reshape(-1) if has else torch.empty_like(g)
                 _lib.call("grace_threshold_step_w1", g.data_ptr(), buf.data_ptr(), 2 if has else 1, float(mem.beta),
                           float(mem.gamma), n, float(np.float32(self.threshold)), ws.data_ptr(), out.data_ptr(),
                           ops._stream())
                 mem.residuals[name] = buf.view(tensor.shape)
+                if place:
+                    self._recycler.keep(name, out, None)
             else:
                 _lib.call("grace_threshold_step_w1", g.data_ptr(), None, 0, 1.0, 1.0, n,
                           float(np.float32(self.threshold)), ws.data_ptr(), out.data_ptr(), ops._stream())

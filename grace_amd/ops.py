@@ -381,7 +381,7 @@ def topk_workspace(n, k, device):
 PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
 PLACE_MIN_N = 1 << 24
 PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "4"))
-PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "2"))
+PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "3"))
 
 
 def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):

@@ -114,6 +114,10 @@ for s in "$@"; do
             run bench_place_$i 300 python3 bench.py --no-cpu-baseline
             GRACE_PLACE_PROBE=0 run bench_noplace_$i 300 python3 bench.py --no-cpu-baseline
           done ;;
+    abthr) for i in 1 2 3; do
+             run bench_thr_place_$i 300 python3 bench.py --workload threshold --steps 20 --no-cpu-baseline
+             GRACE_PLACE_PROBE=0 run bench_thr_noplace_$i 300 python3 bench.py --workload threshold --steps 20 --no-cpu-baseline
+           done ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
