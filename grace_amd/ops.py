@@ -382,6 +382,8 @@ PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
 PLACE_MIN_N = 1 << 24
 PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "4"))
 PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "3"))
+PLACE_SPACER_GIB = float(os.environ.get("GRACE_PLACE_SPACER_GIB", "3"))
+PLACE_SPACER_STEP_GIB = float(os.environ.get("GRACE_PLACE_SPACER_STEP_GIB", "1.25"))
 
 
 def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
@@ -392,7 +394,14 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     n = g.numel()
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
     rs = [torch.empty_like(g) for _ in range(n_res)]
-    outs = [torch.empty_like(g) for _ in range(n_out)]
+    # the output candidates 3, 4.25, 5.5, ... GiB of allocations past the residual candidates: pairs
+    # allocated back to back were never fast in tools/ab_spacer.py, pairs 1-6 GiB apart often were
+    # (profiles/r06_spacer.txt); the spacers go back to torch's cache right after the probe
+    spacers, outs = [], []
+    for j in range(n_out):
+        gib = PLACE_SPACER_GIB if j == 0 else PLACE_SPACER_STEP_GIB
+        spacers.append(torch.empty(int(gib * (1 << 28)), dtype=F32, device=g.device))
+        outs.append(torch.empty_like(g))
     pairs = [(i, j) for j in range(n_out) for i in range(n_res)]
     evs = []
     for i, j in pairs:
@@ -407,6 +416,7 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     us = [a.elapsed_time(b) * 1e3 for a, b in evs]
     best = min(range(len(pairs)), key=lambda q: us[q])
     i, j = pairs[best]
+    del spacers
     return rs[i], outs[j], us
 
 

@@ -118,6 +118,13 @@ for s in "$@"; do
              run bench_thr_place_$i 300 python3 bench.py --workload threshold --steps 20 --no-cpu-baseline
              GRACE_PLACE_PROBE=0 run bench_thr_noplace_$i 300 python3 bench.py --workload threshold --steps 20 --no-cpu-baseline
            done ;;
+    abspacer) run ab_spacer 500 python3 tools/ab_spacer.py ;;
+    abpb2) for i in 1 2; do
+             run bench_sp_$i 300 python3 bench.py --no-cpu-baseline
+             GRACE_PLACE_SPACER_GIB=0 GRACE_PLACE_SPACER_STEP_GIB=0 run bench_nosp_$i 300 python3 bench.py --no-cpu-baseline
+             GRACE_PLACE_PROBE=0 run bench_off_$i 300 python3 bench.py --no-cpu-baseline
+             run bench_thr_sp_$i 300 python3 bench.py --workload threshold --steps 20 --no-cpu-baseline
+           done ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
