@@ -128,7 +128,9 @@ class ThresholdCompressor(Compressor):
                 r = mem.residuals.get(name)
                 has = r is not None and r.numel() == n and r.device == dev and r.is_contiguous()
                 if not has and place:
-                    buf, out, self.place_probes[name] = ops.pick_pair(g)
+                    buf, out, probes = ops.pick_pair(g)
+                    if probes:
+                        self.place_probes[name] = probes
                 else:
                     buf = r.reshape(-1) if has else torch.empty_like(g)
                 _lib.call("grace_threshold_step_w1", g.data_ptr(), buf.data_ptr(), 2 if has else 1, float(mem.beta),

@@ -107,7 +107,9 @@ class TopKCompressor(Compressor):
             else:
                 out, prev_idx = torch.empty_like(g), None
             if place and not has:
-                res, out, self.place_probes[name] = ops.pick_pair(g)
+                res, out, probes = ops.pick_pair(g)
+                if probes:
+                    self.place_probes[name] = probes
                 carry, carry_valid = mem.carry_for(name, res, has, k)
             _, _, idx = ops.topk_residual_step(g, res, has, mem.beta, mem.gamma, k, out=out, carry=carry,
                                                carry_valid=carry_valid, prev_idx=prev_idx)

@@ -392,16 +392,26 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     step writes both densely)."""
     g = dev_f32(g)
     n = g.numel()
+    # the trial needs (n_res + n_out) buckets and the spacers on top of what the caller holds: on a
+    # device without that much free memory the first two plain allocations are taken instead
+    spacer_bytes = int((PLACE_SPACER_GIB + PLACE_SPACER_STEP_GIB * max(n_out - 1, 0)) * (1 << 30))
+    need = 4 * n * (n_res + n_out) + spacer_bytes
+    if torch.cuda.mem_get_info(g.device)[0] < need + (4 << 30):
+        return torch.empty_like(g), torch.empty_like(g), []
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
-    rs = [torch.empty_like(g) for _ in range(n_res)]
-    # the output candidates 3, 4.25, 5.5, ... GiB of allocations past the residual candidates: pairs
-    # allocated back to back were never fast in tools/ab_spacer.py, pairs 1-6 GiB apart often were
-    # (profiles/r06_spacer.txt); the spacers go back to torch's cache right after the probe
-    spacers, outs = [], []
-    for j in range(n_out):
-        gib = PLACE_SPACER_GIB if j == 0 else PLACE_SPACER_STEP_GIB
-        spacers.append(torch.empty(int(gib * (1 << 28)), dtype=F32, device=g.device))
-        outs.append(torch.empty_like(g))
+    try:
+        rs = [torch.empty_like(g) for _ in range(n_res)]
+        # the output candidates 3, 4.25, 5.5, ... GiB of allocations past the residual candidates:
+        # pairs allocated back to back were never fast on one box of tools/ab_spacer.py, pairs 1-6 GiB
+        # apart often were (profiles/r06_spacer.txt); the spacers go back to torch's cache after
+        spacers, outs = [], []
+        for j in range(n_out):
+            gib = PLACE_SPACER_GIB if j == 0 else PLACE_SPACER_STEP_GIB
+            spacers.append(torch.empty(int(gib * (1 << 28)), dtype=F32, device=g.device))
+            outs.append(torch.empty_like(g))
+    except torch.cuda.OutOfMemoryError:
+        rs = outs = spacers = None
+        return torch.empty_like(g), torch.empty_like(g), []
     pairs = [(i, j) for j in range(n_out) for i in range(n_res)]
     evs = []
     for i, j in pairs:

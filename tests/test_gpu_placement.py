@@ -59,3 +59,24 @@ def test_pick_pair_returns_distinct_buffers():
     assert r.data_ptr() != out.data_ptr() and r.numel() == out.numel() == g.numel()
     assert len(us) == 4
     assert torch.equal(g, g0)   # the probe only reads g
+
+
+def test_pick_pair_without_room_takes_plain_buffers(monkeypatch):
+    """A device without room for the trial (here: a spacer larger than the device) gets two plain
+    allocations and no probe; the step stays exact."""
+    from grace_amd import ops
+    from grace_amd.dist.communicator.allgather import Allgather
+    from grace_amd.dist.compressor.topk import TopKCompressor
+    from grace_amd.dist.memory.residual import ResidualMemory
+    monkeypatch.setattr(ops, "PLACE_SPACER_GIB", 1 << 20)   # 1 PiB
+    n, ratio = ops.PLACE_MIN_N, 0.01
+    g = torch.randn(n, device="cuda")
+    r, out, us = ops.pick_pair(g)
+    assert us == [] and r.numel() == out.numel() == n
+    comm = Allgather(TopKCompressor(ratio), ResidualMemory(), 1)
+    gn = _g(n, 7)
+    out = comm.step(torch.from_numpy(gn).cuda(), "b")
+    _, _, _, r_or, out_or = O.topk_residual_step(gn, None, ratio)
+    assert same_bits(out.cpu().numpy(), out_or)
+    assert same_bits(comm.memory.residuals["b"].cpu().numpy(), r_or)
+    assert "b" not in comm.compressor.place_probes
