@@ -380,10 +380,10 @@ def topk_workspace(n, k, device):
 # name; GRACE_PLACE_PROBE=0 turns it off.
 PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
 PLACE_MIN_N = 1 << 24
-PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "4"))
-PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "3"))
+PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "6"))
+PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "4"))
 PLACE_SPACER_GIB = float(os.environ.get("GRACE_PLACE_SPACER_GIB", "3"))
-PLACE_SPACER_STEP_GIB = float(os.environ.get("GRACE_PLACE_SPACER_STEP_GIB", "1.25"))
+PLACE_SPACER_STEP_GIB = float(os.environ.get("GRACE_PLACE_SPACER_STEP_GIB", "1"))
 
 
 def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
@@ -401,7 +401,7 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
     try:
         rs = [torch.empty_like(g) for _ in range(n_res)]
-        # the output candidates 3, 4.25, 5.5, ... GiB of allocations past the residual candidates:
+        # the output candidates 3, 4, 5, 6 GiB of allocations past the residual candidates:
         # pairs allocated back to back were never fast on one box of tools/ab_spacer.py, pairs 1-6 GiB
         # apart often were (profiles/r06_spacer.txt); the spacers go back to torch's cache after
         spacers, outs = [], []
