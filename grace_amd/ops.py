@@ -384,6 +384,7 @@ PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "6"))
 PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "4"))
 PLACE_SPACER_GIB = float(os.environ.get("GRACE_PLACE_SPACER_GIB", "3"))
 PLACE_SPACER_STEP_GIB = float(os.environ.get("GRACE_PLACE_SPACER_STEP_GIB", "1"))
+PLACE_RES_SPACER_GIB = float(os.environ.get("GRACE_PLACE_RES_SPACER_GIB", "1"))
 
 
 def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
@@ -394,17 +395,23 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     n = g.numel()
     # the trial needs (n_res + n_out) buckets and the spacers on top of what the caller holds: on a
     # device without that much free memory the first two plain allocations are taken instead
-    spacer_bytes = int((PLACE_SPACER_GIB + PLACE_SPACER_STEP_GIB * max(n_out - 1, 0)) * (1 << 30))
+    spacer_bytes = int((PLACE_SPACER_GIB + PLACE_SPACER_STEP_GIB * max(n_out - 1, 0) +
+                        PLACE_RES_SPACER_GIB * max((n_res - 1) // 2, 0)) * (1 << 30))
     need = 4 * n * (n_res + n_out) + spacer_bytes
     if torch.cuda.mem_get_info(g.device)[0] < need + (4 << 30):
         return torch.empty_like(g), torch.empty_like(g), []
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
     try:
-        rs = [torch.empty_like(g) for _ in range(n_res)]
+        # residual candidates in twos, 1 GiB of allocations apart, so the pairs' distances vary more
+        spacers, rs = [], []
+        for i in range(n_res):
+            if i and i % 2 == 0 and PLACE_RES_SPACER_GIB > 0:
+                spacers.append(torch.empty(int(PLACE_RES_SPACER_GIB * (1 << 28)), dtype=F32, device=g.device))
+            rs.append(torch.empty_like(g))
         # the output candidates 3, 4, 5, 6 GiB of allocations past the residual candidates:
         # pairs allocated back to back were never fast on one box of tools/ab_spacer.py, pairs 1-6 GiB
         # apart often were (profiles/r06_spacer.txt); the spacers go back to torch's cache after
-        spacers, outs = [], []
+        outs = []
         for j in range(n_out):
             gib = PLACE_SPACER_GIB if j == 0 else PLACE_SPACER_STEP_GIB
             spacers.append(torch.empty(int(gib * (1 << 28)), dtype=F32, device=g.device))

@@ -130,6 +130,7 @@ for s in "$@"; do
              GRACE_PLACE_RES=6 GRACE_PLACE_OUT=4 GRACE_PLACE_SPACER_STEP_GIB=1 run bench_p64_$i 300 python3 bench.py --no-cpu-baseline --no-overlap
            done ;;
     aboutplace) run ab_out_place 400 python3 tools/ab_out_place.py ;;
+    bench2) for i in 1 2; do run bench_r$i 300 python3 bench.py --no-cpu-baseline --no-overlap; done ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
