@@ -28,6 +28,8 @@ SIGNATURES = {
     "grace_topk_fallback_spin_limit": (ctypes.c_int64, [ctypes.c_int64]),
     "grace_topk_stream_probe_workspace_bytes": (SZ, [I64]),
     "grace_topk_stream_probe": (ST, [P, P, P, I64, I32, P, SZ, P]),
+    "grace_spacer_alloc": (ST, [SZ, P]),
+    "grace_spacer_free": (ST, [P]),
     "grace_timer_enable": (ST, [ctypes.c_int]),
     "grace_timer_collect": (ST, [P, P]),
     "grace_event_create": (ST, [P]),

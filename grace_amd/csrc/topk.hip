@@ -2454,6 +2454,31 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
 
 size_t grace_topk_stream_probe_workspace_bytes(int64_t n) { return ws_bytes(n, 1); }
 
+// Placement spacers (ops.pick_pair): device memory taken straight from the HIP runtime between the
+// residual and output candidate allocations and given straight back, so the caller's allocator
+// cache keeps none of it
+grace_status_t grace_spacer_alloc(size_t bytes, void** ptr) {
+  GRACE_REQUIRE(ptr, "grace_spacer_alloc: null ptr");
+  *ptr = nullptr;
+  if (bytes == 0) return GRACE_OK;
+  if (hipMalloc(ptr, bytes) != hipSuccess) {
+    *ptr = nullptr;
+    (void)hipGetLastError();
+    set_error_msg("grace_spacer_alloc: hipMalloc failed");
+    return GRACE_ERR_HIP;
+  }
+  return GRACE_OK;
+}
+
+grace_status_t grace_spacer_free(void* ptr) {
+  if (ptr && hipFree(ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error_msg("grace_spacer_free: hipFree failed");
+    return GRACE_ERR_HIP;
+  }
+  return GRACE_OK;
+}
+
 grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, int32_t sparse, void* ws,
                                        size_t ws_bytes_, void* stream) {
   GRACE_REQUIRE(g && r && out && ws && n >= 1 && n < ((int64_t)1 << 31) &&

@@ -381,44 +381,53 @@ def topk_workspace(n, k, device):
 PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
 PLACE_MIN_N = 1 << 24
 PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "6"))
-PLACE_OUT = int(os.environ.get("GRACE_PLACE_OUT", "4"))
-PLACE_SPACER_GIB = float(os.environ.get("GRACE_PLACE_SPACER_GIB", "3"))
-PLACE_SPACER_STEP_GIB = float(os.environ.get("GRACE_PLACE_SPACER_STEP_GIB", "1"))
+# the output candidates' distances past the residual candidates, in GiB of allocations: on one GPU
+# fitting pairs were 1-6 GiB apart, on another only >= 8 GiB (profiles/r06_spacer.txt)
+PLACE_OUT_GIB = tuple(float(x) for x in os.environ.get("GRACE_PLACE_OUT_GIB", "3,8,16,32").split(","))
+PLACE_OUT = len(PLACE_OUT_GIB)
 PLACE_RES_SPACER_GIB = float(os.environ.get("GRACE_PLACE_RES_SPACER_GIB", "1"))
 
 
-def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
-    """(residual, output, probe microseconds per pair): the fastest of n_res x n_out fresh
+def _spacer(gib, held):
+    """gib GiB of device memory straight from the runtime (grace_spacer_alloc), kept in `held`."""
+    import ctypes
+    p = ctypes.c_void_p()
+    _lib.call("grace_spacer_alloc", int(gib * (1 << 30)), ctypes.addressof(p))
+    held.append(p.value)
+
+
+def pick_pair(g, n_res=PLACE_RES, out_gib=PLACE_OUT_GIB):
+    """(residual, output, probe microseconds per pair): the fastest of n_res x len(out_gib) fresh
     allocation pairs under the stream probe over g (their contents are garbage: the caller's first
-    step writes both densely)."""
+    step writes both densely).  The residual candidates are allocated in twos PLACE_RES_SPACER_GIB
+    apart, the output candidates out_gib GiB past them; the spacers between are plain runtime
+    allocations (grace_spacer_alloc), given back as soon as the candidates are placed."""
     g = dev_f32(g)
     n = g.numel()
-    # the trial needs (n_res + n_out) buckets and the spacers on top of what the caller holds: on a
-    # device without that much free memory the first two plain allocations are taken instead
-    spacer_bytes = int((PLACE_SPACER_GIB + PLACE_SPACER_STEP_GIB * max(n_out - 1, 0) +
-                        PLACE_RES_SPACER_GIB * max((n_res - 1) // 2, 0)) * (1 << 30))
-    need = 4 * n * (n_res + n_out) + spacer_bytes
+    n_out = len(out_gib)
+    spacer_gib = max(out_gib) + PLACE_RES_SPACER_GIB * max((n_res - 1) // 2, 0)
+    need = 4 * n * (n_res + n_out) + int(spacer_gib * (1 << 30))
     if torch.cuda.mem_get_info(g.device)[0] < need + (4 << 30):
         return torch.empty_like(g), torch.empty_like(g), []
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
+    held, rs, outs = [], [], []
     try:
-        # residual candidates in twos, 1 GiB of allocations apart, so the pairs' distances vary more
-        spacers, rs = [], []
         for i in range(n_res):
             if i and i % 2 == 0 and PLACE_RES_SPACER_GIB > 0:
-                spacers.append(torch.empty(int(PLACE_RES_SPACER_GIB * (1 << 28)), dtype=F32, device=g.device))
+                _spacer(PLACE_RES_SPACER_GIB, held)
             rs.append(torch.empty_like(g))
-        # the output candidates 3, 4, 5, 6 GiB of allocations past the residual candidates:
-        # pairs allocated back to back were never fast on one box of tools/ab_spacer.py, pairs 1-6 GiB
-        # apart often were (profiles/r06_spacer.txt); the spacers go back to torch's cache after
-        outs = []
-        for j in range(n_out):
-            gib = PLACE_SPACER_GIB if j == 0 else PLACE_SPACER_STEP_GIB
-            spacers.append(torch.empty(int(gib * (1 << 28)), dtype=F32, device=g.device))
+        done = 0.0
+        for gib in sorted(out_gib):
+            if gib - done > 0:
+                _spacer(gib - done, held)
+            done = gib
             outs.append(torch.empty_like(g))
-    except torch.cuda.OutOfMemoryError:
-        rs = outs = spacers = None
+    except (torch.cuda.OutOfMemoryError, _lib.GraceNativeError):
+        rs = outs = None
         return torch.empty_like(g), torch.empty_like(g), []
+    finally:
+        for q in held:
+            _lib.call("grace_spacer_free", q)
     pairs = [(i, j) for j in range(n_out) for i in range(n_res)]
     evs = []
     for i, j in pairs:
@@ -433,7 +442,6 @@ def pick_pair(g, n_res=PLACE_RES, n_out=PLACE_OUT):
     us = [a.elapsed_time(b) * 1e3 for a, b in evs]
     best = min(range(len(pairs)), key=lambda q: us[q])
     i, j = pairs[best]
-    del spacers
     return rs[i], outs[j], us
 
 

@@ -51,6 +51,11 @@ grace_status_t grace_read_status(const void* workspace, int32_t* status_host, vo
  * out = 0 written in place; sparse != 0 is the recycled-output layout (out untouched).  Its rate
  * is the ceiling of the real pass's exact memory layout. */
 size_t grace_topk_stream_probe_workspace_bytes(int64_t n);
+/* Plain device allocations for the buffer-pair placement probe's spacers (grace_amd/ops.py
+ * pick_pair): hipMalloc / hipFree, so the caller's allocator cache holds none of it.  A failed
+ * allocation returns GRACE_ERR_HIP with *ptr = NULL. */
+grace_status_t grace_spacer_alloc(size_t bytes, void** ptr);
+grace_status_t grace_spacer_free(void* ptr);
 grace_status_t grace_topk_stream_probe(const float* g, float* r, float* out, int64_t n, int32_t sparse, void* ws,
                                        size_t ws_bytes, void* stream);
 

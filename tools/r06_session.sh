@@ -131,6 +131,8 @@ for s in "$@"; do
            done ;;
     aboutplace) run ab_out_place 400 python3 tools/ab_out_place.py ;;
     bench2) for i in 1 2; do run bench_r$i 300 python3 bench.py --no-cpu-baseline --no-overlap; done ;;
+    abspacerw) python3 -c "import torch; print(torch.cuda.get_device_properties(0).pci_bus_id if hasattr(torch.cuda.get_device_properties(0), 'pci_bus_id') else '')" > $O/spacer_wide_pci.txt 2>&1
+               run ab_spacer_wide 600 python3 tools/ab_spacer_wide.py ;;
     shardtk) run shardtk 900 python3 -u -m pytest tests/test_gpu_sharded.py "tests/test_gpu_configs.py::test_sharded_topk_w8_one_device" \
                -q -x --timeout 300 --timeout-method thread ;;
     wnlocal) run wn_local 180 python3 tools/exp_wn_local.py ;;
