@@ -383,7 +383,7 @@ PLACE_MIN_N = 1 << 24
 PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "6"))
 # the output candidates' distances past the residual candidates, in GiB of allocations: on one GPU
 # fitting pairs were 1-6 GiB apart, on another only >= 8 GiB (profiles/r06_spacer.txt)
-PLACE_OUT_GIB = tuple(float(x) for x in os.environ.get("GRACE_PLACE_OUT_GIB", "3,8,16,32").split(","))
+PLACE_OUT_GIB = tuple(float(x) for x in os.environ.get("GRACE_PLACE_OUT_GIB", "0,3,8,16,32").split(","))
 PLACE_OUT = len(PLACE_OUT_GIB)
 PLACE_RES_SPACER_GIB = float(os.environ.get("GRACE_PLACE_RES_SPACER_GIB", "1"))
 
