@@ -380,12 +380,13 @@ def topk_workspace(n, k, device):
 # name; GRACE_PLACE_PROBE=0 turns it off.
 PLACE_PROBE = os.environ.get("GRACE_PLACE_PROBE", "1") != "0"
 PLACE_MIN_N = 1 << 24
-PLACE_RES = int(os.environ.get("GRACE_PLACE_RES", "6"))
+# the residual candidates' positions, in GiB of allocations from the first (in twos, spread out)
+PLACE_RES_GIB = tuple(float(x) for x in os.environ.get("GRACE_PLACE_RES_GIB", "0,0,4,4,12,12").split(","))
+PLACE_RES = len(PLACE_RES_GIB)
 # the output candidates' distances past the residual candidates, in GiB of allocations: on one GPU
 # fitting pairs were 1-6 GiB apart, on another only >= 8 GiB (profiles/r06_spacer.txt)
 PLACE_OUT_GIB = tuple(float(x) for x in os.environ.get("GRACE_PLACE_OUT_GIB", "0,3,8,16,32").split(","))
 PLACE_OUT = len(PLACE_OUT_GIB)
-PLACE_RES_SPACER_GIB = float(os.environ.get("GRACE_PLACE_RES_SPACER_GIB", "1"))
 
 
 def _spacer(gib, held):
@@ -396,25 +397,30 @@ def _spacer(gib, held):
     held.append(p.value)
 
 
-def pick_pair(g, n_res=PLACE_RES, out_gib=PLACE_OUT_GIB):
+def pick_pair(g, res_gib=None, out_gib=None):
     """(residual, output, probe microseconds per pair): the fastest of n_res x len(out_gib) fresh
     allocation pairs under the stream probe over g (their contents are garbage: the caller's first
-    step writes both densely).  The residual candidates are allocated in twos PLACE_RES_SPACER_GIB
-    apart, the output candidates out_gib GiB past them; the spacers between are plain runtime
-    allocations (grace_spacer_alloc), given back as soon as the candidates are placed."""
+    step writes both densely).  The residual candidates are allocated res_gib GiB of allocations
+    past the first one, the output candidates out_gib GiB past the last residual candidate; the
+    spacers between are plain runtime allocations (grace_spacer_alloc), given back as soon as the
+    candidates are placed."""
+    res_gib = PLACE_RES_GIB if res_gib is None else tuple(res_gib)
+    out_gib = PLACE_OUT_GIB if out_gib is None else tuple(out_gib)
     g = dev_f32(g)
     n = g.numel()
-    n_out = len(out_gib)
-    spacer_gib = max(out_gib) + PLACE_RES_SPACER_GIB * max((n_res - 1) // 2, 0)
+    n_res, n_out = len(res_gib), len(out_gib)
+    spacer_gib = max(res_gib) + max(out_gib)
     need = 4 * n * (n_res + n_out) + int(spacer_gib * (1 << 30))
     if torch.cuda.mem_get_info(g.device)[0] < need + (4 << 30):
         return torch.empty_like(g), torch.empty_like(g), []
     ws = workspace("probe", _lib.query("grace_topk_stream_probe_workspace_bytes", n), g.device)
     held, rs, outs = [], [], []
     try:
-        for i in range(n_res):
-            if i and i % 2 == 0 and PLACE_RES_SPACER_GIB > 0:
-                _spacer(PLACE_RES_SPACER_GIB, held)
+        done = 0.0
+        for gib in sorted(res_gib):
+            if gib - done > 0:
+                _spacer(gib - done, held)
+            done = gib
             rs.append(torch.empty_like(g))
         done = 0.0
         for gib in sorted(out_gib):

@@ -54,7 +54,7 @@ def test_pick_pair_returns_distinct_buffers():
     from grace_amd import ops
     g = torch.randn(ops.PLACE_MIN_N, device="cuda")
     g0 = g.clone()
-    r, out, us = ops.pick_pair(g, 2, (3.0, 8.0))
+    r, out, us = ops.pick_pair(g, (0.0, 1.0), (3.0, 8.0))
     torch.cuda.synchronize()
     assert r.data_ptr() != out.data_ptr() and r.numel() == out.numel() == g.numel()
     assert len(us) == 4
@@ -68,7 +68,7 @@ def test_pick_pair_without_room_takes_plain_buffers(monkeypatch):
     from grace_amd.dist.communicator.allgather import Allgather
     from grace_amd.dist.compressor.topk import TopKCompressor
     from grace_amd.dist.memory.residual import ResidualMemory
-    monkeypatch.setattr(ops, "PLACE_RES_SPACER_GIB", float(1 << 20))   # 1 PiB between residual candidates
+    monkeypatch.setattr(ops, "PLACE_OUT_GIB", (float(1 << 20),))   # an output candidate 1 PiB away
     n, ratio = ops.PLACE_MIN_N, 0.01
     g = torch.randn(n, device="cuda")
     r, out, us = ops.pick_pair(g)
